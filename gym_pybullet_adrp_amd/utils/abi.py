@@ -1,0 +1,115 @@
+"""ctypes mirror of include/adrp.h (struct layouts and constants).
+
+Must stay byte-identical with the header: tests/test_abi.py checks sizeof() against the
+value adrp_default_config() writes into ``struct_size``.
+"""
+import ctypes
+
+ABI_VERSION = 1
+MAX_DRONES = 8
+MAX_GATES = 4
+MAX_OBSTACLES = 4
+
+OK, ERR_INVALID, ERR_DEVICE, ERR_OOM = 0, -1, -2, -3
+
+TASK_HOVER, TASK_RACE = 0, 1
+PHYS_PYB, PHYS_DYN, PHYS_PYB_GND, PHYS_PYB_DRAG, PHYS_PYB_DW, PHYS_PYB_GND_DRAG_DW = range(6)
+ACT_RPM, ACT_ONE_D_RPM, ACT_FULLSTATE = 0, 1, 2
+RACE_COMPARE, RACE_COMPETE = 0, 1
+
+_d = ctypes.c_double
+_i32 = ctypes.c_int32
+
+
+def _arr(t, *dims):
+    for n in reversed(dims):
+        t = t * n
+    return t
+
+
+class AdrpDroneParams(ctypes.Structure):
+    _fields_ = [
+        ("m", _d), ("l", _d), ("thrust2weight", _d),
+        ("ixx", _d), ("iyy", _d), ("izz", _d),
+        ("kf", _d), ("km", _d),
+        ("collision_h", _d), ("collision_r", _d), ("collision_z_offset", _d),
+        ("max_speed_kmh", _d),
+        ("gnd_eff_coeff", _d), ("prop_radius", _d),
+        ("drag_coeff", _arr(_d, 3)),
+        ("dw_coeff", _arr(_d, 3)),
+        ("prop_pos", _arr(_d, 4, 3)),
+    ]
+
+
+class AdrpTrack(ctypes.Structure):
+    _fields_ = [
+        ("num_gates", _i32), ("num_obstacles", _i32),
+        ("gates", _arr(_d, MAX_GATES, 7)),
+        ("obstacles", _arr(_d, MAX_OBSTACLES, 6)),
+        ("bounds_hi", _arr(_d, 3)),
+        ("episode_len_sec", _d),
+        ("random_gates_obstacles", _i32),
+        ("gate_offset_range", _arr(_d, 2)),
+        ("obstacle_offset_range", _arr(_d, 2)),
+        ("random_drone_state", _i32),
+        ("pos_offset_range", _arr(_d, 3, 2)),
+        ("rot_offset_range", _arr(_d, 3, 2)),
+        ("random_drone_inertia", _i32),
+        ("inertia_offset_range", _arr(_d, 4, 2)),
+        ("disturbances", _i32),
+        ("action_noise_std", _d),
+        ("dyn_dist_low", _arr(_d, 3)), ("dyn_dist_high", _arr(_d, 3)),
+        ("init_pos", _arr(_d, MAX_DRONES, 3)),
+        ("init_vel", _arr(_d, MAX_DRONES, 3)),
+        ("init_rpy", _arr(_d, MAX_DRONES, 3)),
+        ("init_pqr", _arr(_d, MAX_DRONES, 3)),
+        ("race_mass", _d),
+        ("race_inertia", _arr(_d, 3)),
+    ]
+
+
+class AdrpConfig(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", ctypes.c_uint32),
+        ("task", _i32), ("physics", _i32), ("act_type", _i32), ("race_mode", _i32),
+        ("num_envs", _i32), ("num_drones", _i32),
+        ("pyb_freq", _i32), ("ctrl_freq", _i32),
+        ("action_buffer_size", _i32),
+        ("autoreset", _i32),
+        ("precision", _i32),
+        ("link_frame_lag", _i32),
+        ("env_offset", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("gravity", _d),
+        ("drone", AdrpDroneParams),
+        ("init_xyz", _arr(_d, MAX_DRONES, 3)),
+        ("init_rpy", _arr(_d, MAX_DRONES, 3)),
+        ("init_xyz_noise", _arr(_d, 3)),
+        ("init_rpy_noise", _arr(_d, 3)),
+        ("init_vel_noise", _arr(_d, 3)),
+        ("init_omega_noise", _arr(_d, 3)),
+        ("target_pos", _arr(_d, 3)),
+        ("episode_len_sec", _d),
+        ("track", AdrpTrack),
+    ]
+
+    def copy(self):
+        c = AdrpConfig()
+        ctypes.memmove(ctypes.byref(c), ctypes.byref(self), ctypes.sizeof(self))
+        return c
+
+
+def set_vec(arr, values):
+    """Assign a (nested) python sequence into a ctypes array in place."""
+    for k, v in enumerate(values):
+        if hasattr(arr[k], "__len__") and not isinstance(arr[k], (int, float)):
+            set_vec(arr[k], v)
+        else:
+            arr[k] = v
+
+
+def to_list(arr):
+    out = []
+    for x in arr:
+        out.append(to_list(x) if hasattr(x, "__len__") else x)
+    return out

@@ -1,0 +1,194 @@
+/*
+ * adrp.h — C-ABI of the MI355X-native batched quadrotor step (libadrp.so).
+ *
+ * One handle = one batch of E independent envs x N drones resident in the HBM of one
+ * GPU.  Every pointer argument named *_dev is a DEVICE pointer (e.g. a torch tensor's
+ * data_ptr() on the same GPU); `stream` is a hipStream_t (NULL = default stream).
+ * All calls are stream-ordered and asynchronous; none of them synchronises the host
+ * except adrp_create / adrp_destroy.  Return codes: ADRP_OK (0) or a negative
+ * ADRP_ERR_*; nothing throws across the ABI.  adrp_last_error() gives the text.
+ *
+ * Reference interfaces replaced (file:line into FelixWaiblinger/gym-pybullet-adrp
+ * snapshot 2024-10-08):
+ *   adrp_create  <- BaseAviary.__init__            envs/BaseAviary.py:25-219
+ *                   HoverAviary.__init__           envs/HoverAviary.py:11-64
+ *                   MultiRaceAviary.__init__       envs/MultiRaceAviary.py:31-123
+ *                   (+ the controller processes    envs/MultiRaceAviary.py:107-115)
+ *   adrp_reset   <- BaseAviary.reset               envs/BaseAviary.py:223-258
+ *                   MultiRaceAviary.reset          envs/MultiRaceAviary.py:127-167
+ *   adrp_step    <- BaseAviary.step                envs/BaseAviary.py:262-387
+ *                   MultiRaceAviary.step           envs/MultiRaceAviary.py:171-270
+ *                   (+ MellingerControl.computeControl control/MellingerControl.py:154-262
+ *                    + RewardWrapper._compute_reward utils/wrapper.py:121-186)
+ *   adrp_get_state / adrp_set_state
+ *                <- p.getBasePositionAndOrientation / p.resetBasePositionAndOrientation /
+ *                   p.getBaseVelocity / p.resetBaseVelocity (BaseAviary.py:520-523,
+ *                   MultiRaceAviary.py:456-467): state snapshot / teacher forcing
+ *   adrp_destroy <- BaseAviary.close / MultiRaceAviary.close
+ *                   envs/BaseAviary.py:420-425, envs/MultiRaceAviary.py:274-280
+ */
+#ifndef ADRP_H
+#define ADRP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADRP_ABI_VERSION 1
+
+#define ADRP_MAX_DRONES 8
+#define ADRP_MAX_GATES 4      /* MultiRaceAviary._computeObs hard-codes 4 (MultiRaceAviary.py:591-651) */
+#define ADRP_MAX_OBSTACLES 4
+
+/* status codes */
+#define ADRP_OK 0
+#define ADRP_ERR_INVALID (-1)   /* bad argument / config (cf. ValueError, BaseAviary.py:79-80) */
+#define ADRP_ERR_DEVICE (-2)    /* HIP runtime error */
+#define ADRP_ERR_OOM (-3)       /* device allocation failed */
+
+/* adrp_config.task */
+#define ADRP_TASK_HOVER 0       /* HoverAviary (envs/HoverAviary.py) */
+#define ADRP_TASK_RACE 1        /* MultiRaceAviary (envs/MultiRaceAviary.py) */
+
+/* adrp_config.physics — utils/enums.py:18-26 (Physics) */
+#define ADRP_PHYS_PYB 0
+#define ADRP_PHYS_DYN 1
+#define ADRP_PHYS_PYB_GND 2
+#define ADRP_PHYS_PYB_DRAG 3
+#define ADRP_PHYS_PYB_DW 4
+#define ADRP_PHYS_PYB_GND_DRAG_DW 5
+
+/* adrp_config.act_type — utils/enums.py:40-47 (ActionType) */
+#define ADRP_ACT_RPM 0          /* HoverAviary: a in [-1,1]^4 -> HOVER_RPM*(1+0.05a) (BaseRLAviary.py:192) */
+#define ADRP_ACT_ONE_D_RPM 1    /* HoverAviary: a in [-1,1]   -> 4 x HOVER_RPM*(1+0.05a) (BaseRLAviary.py:225) */
+#define ADRP_ACT_FULLSTATE 2    /* MultiRace: [x,y,z,yaw] absolute FULLSTATE setpoint (MultiRaceAviary.py:190-194) */
+
+/* adrp_config.race_mode — utils/enums.py:84-87 (RaceMode) */
+#define ADRP_RACE_COMPARE 0
+#define ADRP_RACE_COMPETE 1
+
+/* Drone constants, as BaseAviary._parseURDFParameters reads them (BaseAviary.py:989-1021). */
+typedef struct adrp_drone_params {
+    double m;                  /* base mass [kg] */
+    double l;                  /* arm [m] */
+    double thrust2weight;
+    double ixx, iyy, izz;      /* diagonal inertia [kg m^2] */
+    double kf, km;             /* thrust / torque coefficients */
+    double collision_h, collision_r, collision_z_offset;
+    double max_speed_kmh;
+    double gnd_eff_coeff, prop_radius;
+    double drag_coeff[3];      /* xy, xy, z */
+    double dw_coeff[3];
+    double prop_pos[4][3];     /* prop link COM in the body frame (URDF inertial origins) */
+} adrp_drone_params;
+
+/* MultiRace track / randomisation description: the YAML schema of config/level*.yaml. */
+typedef struct adrp_track {
+    int32_t num_gates;                               /* <= ADRP_MAX_GATES */
+    int32_t num_obstacles;                           /* <= ADRP_MAX_OBSTACLES */
+    double gates[ADRP_MAX_GATES][7];                 /* nominal x,y,z,r,p,y,type(0 tall,1 low) */
+    double obstacles[ADRP_MAX_OBSTACLES][6];         /* nominal x,y,z,r,p,y */
+    double bounds_hi[3];                             /* |pos| > bounds[1] eliminates (MultiRaceAviary.py:684) */
+    double episode_len_sec;
+    int32_t random_gates_obstacles;
+    double gate_offset_range[2];                     /* U(lo,hi) on x,y,yaw */
+    double obstacle_offset_range[2];                 /* U(lo,hi) on x,y */
+    int32_t random_drone_state;
+    double pos_offset_range[3][2];                   /* U ranges x,y,z */
+    double rot_offset_range[3][2];                   /* U ranges r,p,y */
+    int32_t random_drone_inertia;
+    double inertia_offset_range[4][2];               /* U ranges on M, Ixx, Iyy, Izz */
+    int32_t disturbances;
+    double action_noise_std;                         /* N(0,std) thrust noise per motor per sub-step */
+    double dyn_dist_low[3], dyn_dist_high[3];        /* U(low,high) world force per drone per sub-step */
+    double init_pos[ADRP_MAX_DRONES][3];             /* config init_states.droneK.pos */
+    double init_vel[ADRP_MAX_DRONES][3];
+    double init_rpy[ADRP_MAX_DRONES][3];             /* raw config value */
+    double init_pqr[ADRP_MAX_DRONES][3];
+    double race_mass;                                /* cf2x.urdf base mass used by changeDynamics (0.027) */
+    double race_inertia[3];
+} adrp_track;
+
+typedef struct adrp_config {
+    uint32_t struct_size;      /* = sizeof(adrp_config); checked by adrp_create */
+    int32_t task;              /* ADRP_TASK_* */
+    int32_t physics;           /* ADRP_PHYS_* */
+    int32_t act_type;          /* ADRP_ACT_* */
+    int32_t race_mode;         /* ADRP_RACE_* */
+    int32_t num_envs;          /* E (envs on THIS device) */
+    int32_t num_drones;        /* N drones per env */
+    int32_t pyb_freq;          /* physics Hz (must be a multiple of ctrl_freq) */
+    int32_t ctrl_freq;         /* env.step Hz */
+    int32_t action_buffer_size;/* HoverAviary obs action ring (ctrl_freq//2, BaseRLAviary.py:66) */
+    int32_t autoreset;         /* 1: done envs are reset inside adrp_step (VecEnv semantics) */
+    int32_t precision;         /* 0 = fp32 kernel, 1 = fp64 kernel */
+    int32_t link_frame_lag;    /* 1 (pybullet): LINK_FRAME forces/torques on links are rotated by the
+                                  link transform cached at the last forwardKinematics, i.e. the pose
+                                  at the start of the previous stepSimulation */
+    int64_t env_offset;        /* global id of local env 0 (RNG key; multi-GPU sharding) */
+    uint64_t seed;
+    double gravity;            /* G = 9.8 (BaseAviary.py:74) */
+    adrp_drone_params drone;
+    /* HoverAviary */
+    double init_xyz[ADRP_MAX_DRONES][3];   /* INIT_XYZS (BaseAviary.py:194-199) */
+    double init_rpy[ADRP_MAX_DRONES][3];   /* INIT_RPYS [rad] */
+    double init_xyz_noise[3];              /* extension: U(-n,n) added per reset (0 = reference) */
+    double init_rpy_noise[3];
+    double init_vel_noise[3];
+    double init_omega_noise[3];
+    double target_pos[3];                  /* HoverAviary.TARGET_POS (HoverAviary.py:51) */
+    double episode_len_sec;                /* HoverAviary.EPISODE_LEN_SEC (HoverAviary.py:52) */
+    /* MultiRaceAviary */
+    adrp_track track;
+} adrp_config;
+
+typedef struct adrp_handle adrp_t;
+
+/* ABI version of the loaded library (must equal ADRP_ABI_VERSION). */
+int adrp_abi_version(void);
+
+/* Fill *cfg with the reference defaults for `task` (HoverAviary or MultiRaceAviary,
+ * CF2X = cf2x_IROS.urdf constants, level0 track for RACE). */
+int adrp_default_config(int task, adrp_config* cfg);
+
+/* Create a handle on GPU `device`; allocates all state in HBM. */
+int adrp_create(const adrp_config* cfg, int device, adrp_t** out);
+void adrp_destroy(adrp_t* h);
+
+/* Error text of the last failing call on h (h may be NULL for adrp_create failures). */
+const char* adrp_last_error(const adrp_t* h);
+
+/* Per-drone observation width D (72 Hover/RPM, 27 Hover/ONE_D_RPM, 49 / 49+6(N-1) Race)
+ * and action width A (4 or 1). */
+int adrp_obs_dim(const adrp_t* h);
+int adrp_act_dim(const adrp_t* h);
+
+/* Reset the envs selected by env_mask_dev (uint8 [E], NULL = all) and write their
+ * observations into obs_dev (float [E,N,D]); rows of unselected envs are left as is. */
+int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev, void* stream);
+
+/* One env.step() of every env: act_dev float [E,N,A] -> obs_dev [E,N,D],
+ * rew_dev float [E], term_dev / trunc_dev uint8 [E].  With autoreset, envs whose
+ * episode ended are reset in the same launch; their final observation is written to
+ * terminal_obs_dev [E,N,D] (only those rows) when it is non-NULL, and obs_dev holds
+ * the reset observation (SB3 VecEnv semantics). */
+int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
+              uint8_t* term_dev, uint8_t* trunc_dev, float* terminal_obs_dev, void* stream);
+
+/* Snapshot layout: nf float fields and ni int32 fields, each field a contiguous
+ * [E*N] vector (drone-major within env: index e*N+n).  Field names: adrp_state_field. */
+int adrp_state_layout(const adrp_t* h, int* nf, int* ni);
+const char* adrp_state_field(const adrp_t* h, int is_int, int index);
+int adrp_get_state(adrp_t* h, float* f_dev, int32_t* i_dev, void* stream);
+int adrp_set_state(adrp_t* h, const float* f_dev, const int32_t* i_dev, void* stream);
+
+/* Algorithmic HBM bytes one adrp_step moves (roofline accounting). */
+int64_t adrp_step_bytes(const adrp_t* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ADRP_H */

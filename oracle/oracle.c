@@ -1,0 +1,800 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h).  Plain C99, float64.
+ *
+ * Structure deliberately follows the reference and Bullet, not the HIP kernel:
+ *   - each sub-step accumulates per-link external forces/torques exactly as the
+ *     reference's pybullet calls do (BaseAviary.py:683-818, MultiRaceAviary.py:510-548),
+ *   - then runs a restatement of Bullet 3.x btMultiBody's floating-base step
+ *     (computeAccelerationsArticulatedBodyAlgorithmMultiDof + stepPositionsMultiDof)
+ *     on the world-to-base quaternion Bullet stores (m_baseQuat),
+ *   - then reads the state back through pybullet's getEulerFromQuaternion convention.
+ * The kernel (gym_pybullet_adrp_amd/csrc) uses a fused closed form instead.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define PI 3.14159265358979323846
+
+static char g_err[256];
+static int fail(const char* msg) {
+    snprintf(g_err, sizeof g_err, "%s", msg);
+    return ADRP_ERR_INVALID;
+}
+const char* orc_last_error(void) { return g_err; }
+
+/* ------------------------------------------------------------------------------------ */
+/* small vector / quaternion algebra (Bullet conventions: quaternion = x,y,z,w)          */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { double x, y, z; } v3;
+typedef struct { double x, y, z, w; } qt;
+
+static v3 V(double x, double y, double z) { v3 r = {x, y, z}; return r; }
+static v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static v3 vscale(v3 a, double s) { return V(a.x * s, a.y * s, a.z * s); }
+static v3 vmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+static double vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static v3 vcross(v3 a, v3 b) {
+    return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static double vnorm(v3 a) { return sqrt(vdot(a, a)); }
+
+typedef struct { double m[3][3]; } m33;
+/* btMatrix3x3::setRotation */
+static m33 mat_from_quat(qt q) {
+    double d = q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+    double s = 2.0 / d;
+    double xs = q.x * s, ys = q.y * s, zs = q.z * s;
+    double wx = q.w * xs, wy = q.w * ys, wz = q.w * zs;
+    double xx = q.x * xs, xy = q.x * ys, xz = q.x * zs;
+    double yy = q.y * ys, yz = q.y * zs, zz = q.z * zs;
+    m33 r;
+    r.m[0][0] = 1.0 - (yy + zz); r.m[0][1] = xy - wz;         r.m[0][2] = xz + wy;
+    r.m[1][0] = xy + wz;         r.m[1][1] = 1.0 - (xx + zz); r.m[1][2] = yz - wx;
+    r.m[2][0] = xz - wy;         r.m[2][1] = yz + wx;         r.m[2][2] = 1.0 - (xx + yy);
+    return r;
+}
+static v3 mv(m33 a, v3 v) {
+    return V(a.m[0][0] * v.x + a.m[0][1] * v.y + a.m[0][2] * v.z,
+             a.m[1][0] * v.x + a.m[1][1] * v.y + a.m[1][2] * v.z,
+             a.m[2][0] * v.x + a.m[2][1] * v.y + a.m[2][2] * v.z);
+}
+static v3 mtv(m33 a, v3 v) {
+    return V(a.m[0][0] * v.x + a.m[1][0] * v.y + a.m[2][0] * v.z,
+             a.m[0][1] * v.x + a.m[1][1] * v.y + a.m[2][1] * v.z,
+             a.m[0][2] * v.x + a.m[1][2] * v.y + a.m[2][2] * v.z);
+}
+static qt qmul(qt a, qt b) { /* btQuaternion operator* */
+    qt r;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    return r;
+}
+static qt qconj(qt a) { qt r = {-a.x, -a.y, -a.z, a.w}; return r; }
+static qt qnormalize(qt a) {
+    double n = sqrt(a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w);
+    qt r = {a.x / n, a.y / n, a.z / n, a.w / n};
+    return r;
+}
+
+/* pybullet.getEulerFromQuaternion (extrinsic x-y-z roll/pitch/yaw) */
+void orc_euler_from_quat(const double q[4], double rpy[3]) {
+    double sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
+    double sarg = -2.0 * (q[0] * q[2] - q[3] * q[1]);
+    if (sarg <= -0.99999) {
+        rpy[0] = 0.0; rpy[1] = -0.5 * PI; rpy[2] = 2.0 * atan2(q[0], -q[1]);
+    } else if (sarg >= 0.99999) {
+        rpy[0] = 0.0; rpy[1] = 0.5 * PI; rpy[2] = 2.0 * atan2(-q[0], q[1]);
+    } else {
+        rpy[0] = atan2(2.0 * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+        rpy[1] = asin(sarg);
+        rpy[2] = atan2(2.0 * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
+    }
+}
+/* pybullet.getQuaternionFromEuler == utils.get_quaternion_from_euler (utils/utils.py:20-43) */
+void orc_quat_from_euler(const double rpy[3], double q[4]) {
+    double cr = cos(rpy[0] / 2), sr = sin(rpy[0] / 2);
+    double cp = cos(rpy[1] / 2), sp = sin(rpy[1] / 2);
+    double cy = cos(rpy[2] / 2), sy = sin(rpy[2] / 2);
+    q[0] = sr * cp * cy - cr * sp * sy;
+    q[1] = cr * sp * cy + sr * cp * sy;
+    q[2] = cr * cp * sy - sr * sp * cy;
+    q[3] = cr * cp * cy + sr * sp * sy;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Philox4x32-10 (Salmon et al., SC'11 "Parallel random numbers: as easy as 1, 2, 3")     */
+/* ------------------------------------------------------------------------------------ */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+/* Random-draw key schedule shared (by specification, not by code) with the kernel:
+ * ctr = {global env id (low 32), episode, tag, index}, key = {seed lo, seed hi};
+ * uniform u = (x >> 8) * 2^-24 in [0,1). */
+static void draw4(uint64_t seed, uint64_t gid, uint32_t episode, uint32_t tag, uint32_t idx,
+                  double u[4]) {
+    uint32_t c[4] = {(uint32_t)gid, episode, tag, idx}, k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)}, o[4];
+    orc_philox4x32_10(c, k, o);
+    for (int i = 0; i < 4; ++i) u[i] = (double)(o[i] >> 8) * (1.0 / 16777216.0);
+}
+#define TAG_HOVER_RESET 0x48520000u
+
+/* ------------------------------------------------------------------------------------ */
+/* configuration defaults (BaseAviary / HoverAviary / MultiRaceAviary constructors)      */
+/* ------------------------------------------------------------------------------------ */
+static void cf2x_iros(adrp_drone_params* d) { /* assets/cf2x_IROS.urdf:5,12-13,35,41-99 */
+    memset(d, 0, sizeof *d);
+    d->m = 0.03454; d->l = 0.0397; d->thrust2weight = 2.25;
+    d->ixx = 1.4e-5; d->iyy = 1.4e-5; d->izz = 2.17e-5;
+    d->kf = 3.16e-10; d->km = 7.94e-12;
+    d->collision_h = 0.025; d->collision_r = 0.06; d->collision_z_offset = 0.0;
+    d->max_speed_kmh = 30.0; d->gnd_eff_coeff = 11.36859; d->prop_radius = 2.31348e-2;
+    d->drag_coeff[0] = 9.1785e-7; d->drag_coeff[1] = 9.1785e-7; d->drag_coeff[2] = 10.311e-7;
+    d->dw_coeff[0] = 2267.18; d->dw_coeff[1] = 0.16; d->dw_coeff[2] = -0.11;
+    const double pp[4][3] = {{0.028, 0.028, 0}, {-0.028, 0.028, 0}, {-0.028, -0.028, 0}, {0.028, -0.028, 0}};
+    memcpy(d->prop_pos, pp, sizeof pp);
+}
+
+void orc_default_config(int task, adrp_config* c) {
+    memset(c, 0, sizeof *c);
+    c->struct_size = sizeof(adrp_config);
+    c->task = task;
+    c->physics = ADRP_PHYS_PYB;
+    c->num_envs = 1;
+    c->autoreset = 1;
+    c->gravity = 9.8;
+    c->link_frame_lag = 1;
+    cf2x_iros(&c->drone);
+    if (task == ADRP_TASK_HOVER) {
+        c->act_type = ADRP_ACT_RPM;
+        c->num_drones = 1;
+        c->pyb_freq = 240; c->ctrl_freq = 30;
+        c->action_buffer_size = 15;
+        c->init_xyz[0][2] = c->drone.collision_h / 2 - c->drone.collision_z_offset + 0.1;
+        c->target_pos[2] = 1.0;
+        c->episode_len_sec = 8.0;
+    } else {
+        c->act_type = ADRP_ACT_FULLSTATE;
+        c->num_drones = 2;
+        c->pyb_freq = 500; c->ctrl_freq = 25;
+        adrp_track* t = &c->track;  /* config/level0.yaml */
+        const double gates[4][7] = {{0.45, -1.0, 0.525, 0, 0, 2.35, 1}, {1.0, -1.55, 1.0, 0, 0, -0.78, 0},
+                                    {0.0, 0.5, 0.525, 0, 0, 0, 1}, {-0.5, -0.5, 1.0, 0, 0, 3.14, 0}};
+        const double obst[4][6] = {{1.0, -0.5, 0.525, 0, 0, 0}, {0.5, -1.5, 0.525, 0, 0, 0},
+                                   {-0.5, 0, 0.525, 0, 0, 0}, {0, 1.0, 0.525, 0, 0, 0}};
+        t->num_gates = 4; t->num_obstacles = 4;
+        memcpy(t->gates, gates, sizeof gates);
+        memcpy(t->obstacles, obst, sizeof obst);
+        t->bounds_hi[0] = 3; t->bounds_hi[1] = 3; t->bounds_hi[2] = 2;
+        t->episode_len_sec = 33;
+        t->random_drone_state = 1;
+        t->pos_offset_range[0][0] = -0.1; t->pos_offset_range[0][1] = 0.1;
+        t->pos_offset_range[1][0] = -0.1; t->pos_offset_range[1][1] = 0.1;
+        t->pos_offset_range[2][0] = 0.0;  t->pos_offset_range[2][1] = 0.02;
+        for (int k = 0; k < 3; ++k) { t->rot_offset_range[k][0] = -0.1; t->rot_offset_range[k][1] = 0.1; }
+        t->init_pos[0][0] = 0.9; t->init_pos[0][1] = 0.9; t->init_pos[0][2] = 0.05;
+        t->init_pos[1][0] = 1.1; t->init_pos[1][1] = 1.1; t->init_pos[1][2] = 0.05;
+        /* build-side extension for N > 2 */
+        t->init_pos[2][0] = 0.7; t->init_pos[2][1] = 0.9; t->init_pos[2][2] = 0.05;
+        t->init_pos[3][0] = 1.3; t->init_pos[3][1] = 1.1; t->init_pos[3][2] = 0.05;
+        t->race_mass = 0.027;                  /* assets/cf2x.urdf:11 */
+        t->race_inertia[0] = 1.4e-5; t->race_inertia[1] = 1.4e-5; t->race_inertia[2] = 2.17e-5;
+    }
+}
+
+/* HOVER_RPM, MAX_RPM, MAX_THRUST, GND_EFF_H_CLIP, MAX_XY_TORQUE, MAX_Z_TORQUE
+ * (BaseAviary.py:117-128) */
+void orc_derived_constants(const adrp_config* c, double out[6]) {
+    const adrp_drone_params* d = &c->drone;
+    double gravity = c->gravity * d->m;
+    double hover = sqrt(gravity / (4 * d->kf));
+    double maxr = sqrt((d->thrust2weight * gravity) / (4 * d->kf));
+    double maxt = 4 * d->kf * maxr * maxr;
+    out[0] = hover;
+    out[1] = maxr;
+    out[2] = maxt;
+    out[3] = 0.25 * d->prop_radius * sqrt((15 * maxr * maxr * d->kf * d->gnd_eff_coeff) / maxt);
+    out[4] = (2 * d->l * d->kf * maxr * maxr) / sqrt(2.0);
+    out[5] = 2 * d->km * maxr * maxr;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* simulation state                                                                      */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    v3 pos;
+    qt q_wtb;        /* Bullet m_baseQuat: world-to-base (pybullet reports its inverse) */
+    v3 vel, omega;   /* world frame (btMultiBody m_realBuf) */
+    v3 rpy_rates;    /* Physics.DYN body rates (BaseAviary.py:481, 842, 881) */
+    v3 ang_v;        /* Physics.DYN: world angular velocity stored by resetBaseVelocity */
+    double last_rpm[4];
+    qt link_q_wtb;   /* links' m_cachedWorldTransform (world-to-base form) and origin, as */
+    v3 link_pos;     /* of the last btMultiBody::forwardKinematics (all links share the base basis) */
+} body_t;
+
+struct orc_handle {
+    adrp_config cfg;
+    int E, N, A, D, S;
+    double dt, hover_rpm, max_rpm, gnd_clip;
+    body_t* b;          /* [E*N] */
+    int32_t* step_counter;  /* [E] */
+    int32_t* episode;       /* [E] */
+    int32_t* ring_head;     /* [E] */
+    float* ring;            /* [E][buf][A] */
+    uint8_t* contact;       /* [E] ground-model flag of the last step */
+    int64_t contacts;
+};
+
+int orc_obs_dim(const orc_t* o) { return o->D; }
+int orc_act_dim(const orc_t* o) { return o->A; }
+int64_t orc_contact_count(const orc_t* o) { return o->contacts; }
+uint8_t orc_env_contact(const orc_t* o, int e) { return o->contact[e]; }
+
+int orc_create(const adrp_config* cfg, orc_t** out) {
+    if (!cfg || cfg->struct_size != sizeof(adrp_config)) return fail("struct_size mismatch");
+    if (cfg->task != ADRP_TASK_HOVER) return fail("oracle: only ADRP_TASK_HOVER is implemented");
+    if (cfg->num_envs <= 0 || cfg->num_drones != 1) return fail("hover: num_envs > 0, num_drones == 1");
+    if (cfg->ctrl_freq <= 0 || cfg->pyb_freq % cfg->ctrl_freq != 0)
+        return fail("pyb_freq is not divisible by env_freq");
+    if (cfg->act_type != ADRP_ACT_RPM && cfg->act_type != ADRP_ACT_ONE_D_RPM) return fail("hover act_type");
+    if (cfg->physics < 0 || cfg->physics > ADRP_PHYS_PYB_GND_DRAG_DW) return fail("physics");
+    if (cfg->action_buffer_size <= 0) return fail("action_buffer_size");
+    orc_t* o = (orc_t*)calloc(1, sizeof *o);
+    o->cfg = *cfg;
+    o->E = cfg->num_envs; o->N = cfg->num_drones;
+    o->A = cfg->act_type == ADRP_ACT_ONE_D_RPM ? 1 : 4;
+    o->D = 12 + cfg->action_buffer_size * o->A;
+    o->S = cfg->pyb_freq / cfg->ctrl_freq;
+    o->dt = 1.0 / cfg->pyb_freq;
+    double dc[6];
+    orc_derived_constants(cfg, dc);
+    o->hover_rpm = dc[0]; o->max_rpm = dc[1]; o->gnd_clip = dc[3];
+    o->b = (body_t*)calloc((size_t)o->E * o->N, sizeof(body_t));
+    o->step_counter = (int32_t*)calloc(o->E, 4);
+    o->episode = (int32_t*)calloc(o->E, 4);
+    o->ring_head = (int32_t*)calloc(o->E, 4);
+    o->ring = (float*)calloc((size_t)o->E * cfg->action_buffer_size * o->A, 4);
+    o->contact = (uint8_t*)calloc(o->E, 1);
+    *out = o;
+    return ADRP_OK;
+}
+
+void orc_destroy(orc_t* o) {
+    if (!o) return;
+    free(o->b); free(o->step_counter); free(o->episode); free(o->ring_head); free(o->ring);
+    free(o->contact); free(o);
+}
+
+/* ---- per-link external force accumulators (what p.applyExternalForce/Torque build) ---- */
+typedef struct {
+    v3 f_world[5], t_world[5];   /* links 0..4 (props 0-3, center_of_mass_link 4) */
+    v3 base_f_world;             /* gravity (btMultiBodyDynamicsWorld::applyGravity) */
+} forces_t;
+
+static v3 link_com_body(const orc_t* o, int link) {
+    if (link < 4) return V(o->cfg.drone.prop_pos[link][0], o->cfg.drone.prop_pos[link][1], o->cfg.drone.prop_pos[link][2]);
+    return V(0, 0, 0);
+}
+/* p.applyExternalForce(body, link, forceObj, posObj=[0,0,0], LINK_FRAME) */
+static void apply_force_link_frame(forces_t* F, m33 R_btw, int link, v3 f_local) {
+    F->f_world[link] = vadd(F->f_world[link], mv(R_btw, f_local));
+}
+static void apply_torque_link_frame(forces_t* F, m33 R_btw, int link, v3 t_local) {
+    F->t_world[link] = vadd(F->t_world[link], mv(R_btw, t_local));
+}
+
+static void body_rpy(const body_t* b, double rpy[3]) {
+    qt q = qconj(b->q_wtb);
+    double qq[4] = {q.x, q.y, q.z, q.w};
+    orc_euler_from_quat(qq, rpy);
+}
+
+/* BaseAviary._physics (BaseAviary.py:683-718) */
+static void ref_physics(const orc_t* o, forces_t* F, m33 R, const double rpm[4]) {
+    const adrp_drone_params* d = &o->cfg.drone;
+    double f[4], t[4];
+    for (int i = 0; i < 4; ++i) { f[i] = rpm[i] * rpm[i] * d->kf; t[i] = rpm[i] * rpm[i] * d->km; }
+    double z_torque = t[0] - t[1] + t[2] - t[3];   /* cf2x_IROS sign (BaseAviary.py:703) */
+    for (int i = 0; i < 4; ++i) apply_force_link_frame(F, R, i, V(0, 0, f[i]));
+    apply_torque_link_frame(F, R, 4, V(0, 0, z_torque));
+}
+/* BaseAviary._groundEffect (BaseAviary.py:722-757) */
+static void ref_ground_effect(const orc_t* o, forces_t* F, const body_t* b, m33 R, const double rpm[4]) {
+    const adrp_drone_params* d = &o->cfg.drone;
+    double h[4], g[4], rpy[3];
+    m33 Rc = mat_from_quat(qconj(b->q_wtb));
+    for (int i = 0; i < 4; ++i) {  /* getLinkStates(...)[i][0][2]: link COM world z (fresh FK) */
+        v3 w = vadd(b->pos, mv(Rc, link_com_body(o, i)));
+        h[i] = w.z < o->gnd_clip ? o->gnd_clip : w.z;
+        double k = d->prop_radius / (4 * h[i]);
+        g[i] = rpm[i] * rpm[i] * d->kf * d->gnd_eff_coeff * k * k;
+    }
+    body_rpy(b, rpy);  /* self.rpy: kinematic cache, current in the KIN physics modes */
+    if (fabs(rpy[0]) < PI / 2 && fabs(rpy[1]) < PI / 2)
+        for (int i = 0; i < 4; ++i) apply_force_link_frame(F, R, i, V(0, 0, g[i]));
+}
+/* BaseAviary._drag (BaseAviary.py:761-788) */
+static void ref_drag(const orc_t* o, forces_t* F, const body_t* b, m33 R, const double rpm[4]) {
+    const adrp_drone_params* d = &o->cfg.drone;
+    double s = 0;
+    for (int i = 0; i < 4; ++i) s += 2 * PI * rpm[i] / 60;
+    v3 fac = V(-d->drag_coeff[0] * s, -d->drag_coeff[1] * s, -d->drag_coeff[2] * s);
+    m33 base_rot = mat_from_quat(qconj(b->q_wtb));      /* p.getMatrixFromQuaternion(self.quat) */
+    v3 drag_link = mtv(base_rot, vmul(fac, b->vel));    /* np.dot(base_rot.T, ...) */
+    apply_force_link_frame(F, R, 4, drag_link);
+}
+/* BaseAviary._downwash (BaseAviary.py:792-818), over the drones of one env */
+static void ref_downwash(const orc_t* o, forces_t* F, const body_t* env_bodies, int n, m33 R) {
+    const adrp_drone_params* d = &o->cfg.drone;
+    for (int i = 0; i < o->N; ++i) {
+        double dz = env_bodies[i].pos.z - env_bodies[n].pos.z;
+        double dx = env_bodies[i].pos.x - env_bodies[n].pos.x, dy = env_bodies[i].pos.y - env_bodies[n].pos.y;
+        double dxy = sqrt(dx * dx + dy * dy);
+        if (dz > 0 && dxy < 10) {
+            double k = d->prop_radius / (4 * dz);
+            double alpha = d->dw_coeff[0] * k * k;
+            double beta = d->dw_coeff[1] * dz + d->dw_coeff[2];
+            apply_force_link_frame(F, R, 4, V(0, 0, -alpha * exp(-0.5 * (dxy / beta) * (dxy / beta))));
+        }
+    }
+}
+
+/* btMultiBody::forwardKinematics: refresh the cached link transforms to the current pose */
+static void forward_kinematics(body_t* b) {
+    b->link_q_wtb = b->q_wtb;
+    b->link_pos = b->pos;
+}
+/* basis pybullet rotates LINK_FRAME link forces with (m_cachedWorldTransform) */
+static m33 link_basis(const orc_t* o, const body_t* b) {
+    return mat_from_quat(qconj(o->cfg.link_frame_lag ? b->link_q_wtb : b->q_wtb));
+}
+
+/* The per-drone force calls of one sub-step, in the reference's order
+   (BaseAviary.py:353-371, MultiRaceAviary.py:512-530). */
+static void assemble_forces(const orc_t* o, forces_t* F, body_t* env_bodies, int n,
+                            const double rpm[4], const double prev_rpm[4]) {
+    memset(F, 0, sizeof *F);
+    body_t* b = &env_bodies[n];
+    int ph = o->cfg.physics;
+    ref_physics(o, F, link_basis(o, b), rpm);
+    if (ph == ADRP_PHYS_PYB_GND || ph == ADRP_PHYS_PYB_GND_DRAG_DW) {
+        forward_kinematics(b);  /* p.getLinkStates(..., computeForwardKinematics=1) */
+        ref_ground_effect(o, F, b, link_basis(o, b), rpm);
+    }
+    if (ph == ADRP_PHYS_PYB_DRAG || ph == ADRP_PHYS_PYB_GND_DRAG_DW) ref_drag(o, F, b, link_basis(o, b), prev_rpm);
+    if (ph == ADRP_PHYS_PYB_DW || ph == ADRP_PHYS_PYB_GND_DRAG_DW) ref_downwash(o, F, env_bodies, n, link_basis(o, b));
+}
+
+int orc_force_assembly(const adrp_config* cfg, int N, const double* states, int n, const double rpm[4],
+                       const double prev_rpm[4], double link_force[5][3], double link_torque[5][3]) {
+    if (N < 1 || N > ADRP_MAX_DRONES || n < 0 || n >= N) return fail("drone index");
+    orc_t o;
+    memset(&o, 0, sizeof o);
+    o.cfg = *cfg;
+    o.N = N;
+    double dc[6];
+    orc_derived_constants(cfg, dc);
+    o.gnd_clip = dc[3];
+    body_t b[ADRP_MAX_DRONES];
+    memset(b, 0, sizeof b);
+    for (int i = 0; i < N; ++i) {   /* state row: pos3, quat4 (x,y,z,w), vel3, omega3 */
+        const double* r = states + 13 * i;
+        b[i].pos = V(r[0], r[1], r[2]);
+        qt q = {r[3], r[4], r[5], r[6]};
+        b[i].q_wtb = qconj(q);
+        b[i].vel = V(r[7], r[8], r[9]);
+        b[i].omega = V(r[10], r[11], r[12]);
+        forward_kinematics(&b[i]);
+    }
+    forces_t F;
+    assemble_forces(&o, &F, b, n, rpm, prev_rpm);
+    m33 R = mat_from_quat(qconj(b[n].q_wtb));
+    for (int l = 0; l < 5; ++l) {  /* back to the LINK frame (links share the base basis) */
+        v3 f = mtv(R, F.f_world[l]), t = mtv(R, F.t_world[l]);
+        link_force[l][0] = f.x; link_force[l][1] = f.y; link_force[l][2] = f.z;
+        link_torque[l][0] = t.x; link_torque[l][1] = t.y; link_torque[l][2] = t.z;
+    }
+    return ADRP_OK;
+}
+
+/* BaseRLAviary._preprocessAction RPM / ONE_D_RPM branches (BaseRLAviary.py:192, 225):
+   float32 action -> float32 (1+0.05a) (NumPy 2 / NEP 50 promotion) -> * float64 HOVER_RPM */
+void orc_hover_rpm(const adrp_config* cfg, const float* act, double rpm[4]) {
+    double dc[6];
+    orc_derived_constants(cfg, dc);
+    int one_d = cfg->act_type == ADRP_ACT_ONE_D_RPM;
+    for (int j = 0; j < 4; ++j) {
+        float a = act[one_d ? 0 : j];
+        float g = 1.0f + 0.05f * a;
+        rpm[j] = dc[0] * (double)g;
+    }
+}
+
+/* ---- Bullet 3.x btMultiBody floating-base step, restated ---------------------------- */
+#define BT_DAMPING 0.04          /* btMultiBody m_linearDamping / m_angularDamping defaults */
+#define BT_MAX_COORD_VEL 100.0   /* btMultiBody m_maxCoordinateVelocity */
+#define BT_ANGULAR_MOTION_THRESHOLD (0.5 * (PI / 2))
+
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+/* returns 1 if the documented ground model acted */
+static int bullet_step(const orc_t* o, body_t* b, const forces_t* F, double mass, v3 inertia) {
+    const double dt = o->dt;
+    forward_kinematics(b);   /* btMultiBodyDynamicsWorld::solveExternalForces starts with it */
+    /* rot_from_parent[0] = world->base */
+    m33 R_wtb = mat_from_quat(b->q_wtb);
+    /* spatial velocity of the base in the base frame */
+    v3 w_b = mv(R_wtb, b->omega), v_b = mv(R_wtb, b->vel);
+    /* external spatial force on the base, base frame: base accumulator + fixed massless links */
+    v3 f_b = mv(R_wtb, F->base_f_world), n_b = V(0, 0, 0);
+    for (int l = 0; l < 5; ++l) {
+        v3 fl = mv(R_wtb, F->f_world[l]), tl = mv(R_wtb, F->t_world[l]);
+        f_b = vadd(f_b, fl);
+        n_b = vadd(n_b, vadd(tl, vcross(link_com_body(o, l), fl)));  /* fixed-joint transfer */
+    }
+    /* zeroAccSpatFrc[0] = -(torque, force) + damping + gyroscopic + m w x v */
+    v3 Iw = vmul(inertia, w_b);
+    v3 z_ang = vadd(vadd(vscale(n_b, -1.0), vscale(Iw, BT_DAMPING + BT_DAMPING * vnorm(w_b))), vcross(w_b, Iw));
+    v3 z_lin = vadd(vadd(vscale(f_b, -1.0), vscale(v_b, mass * (BT_DAMPING + BT_DAMPING * vnorm(v_b)))),
+                    vscale(vcross(w_b, v_b), mass));
+    /* spatAcc[0] = -I^-1 zeroAccSpatFrc[0]  (articulated inertia of the base = its own) */
+    v3 acc_ang = V(-z_ang.x / inertia.x, -z_ang.y / inertia.y, -z_ang.z / inertia.z);
+    v3 acc_lin = vscale(z_lin, -1.0 / mass);
+    /* back to world; spatial -> classical linear acceleration */
+    v3 wdot = mtv(R_wtb, acc_ang);
+    v3 vdot = mtv(R_wtb, vadd(acc_lin, vcross(w_b, v_b)));
+    /* applyDeltaVeeMultiDof(output, dt) with the coordinate-velocity clamp */
+    double buf[6] = {b->omega.x, b->omega.y, b->omega.z, b->vel.x, b->vel.y, b->vel.z};
+    double dv[6] = {wdot.x, wdot.y, wdot.z, vdot.x, vdot.y, vdot.z};
+    for (int k = 0; k < 6; ++k) buf[k] = clampd(buf[k] + dv[k] * dt, -BT_MAX_COORD_VEL, BT_MAX_COORD_VEL);
+    b->omega = V(buf[0], buf[1], buf[2]);
+    b->vel = V(buf[3], buf[4], buf[5]);
+    /* stepPositionsMultiDof: position with the new velocity, exp-map on world omega */
+    b->pos = vadd(b->pos, vscale(b->vel, dt));
+    double ang = vnorm(b->omega);
+    if (ang * dt > BT_ANGULAR_MOTION_THRESHOLD) ang = BT_ANGULAR_MOTION_THRESHOLD / dt;
+    v3 axis;
+    if (ang < 0.001)
+        axis = vscale(b->omega, 0.5 * dt - (dt * dt * dt) * 0.020833333333 * ang * ang);
+    else
+        axis = vscale(b->omega, sin(0.5 * ang * dt) / ang);
+    qt dq = {-axis.x, -axis.y, -axis.z, cos(0.5 * ang * dt)};
+    b->q_wtb = qnormalize(qmul(b->q_wtb, dq));
+    /* ground model (plane z = 0 vs the URDF collision cylinder): non-penetration +
+       zero inward normal velocity.  Not Bullet's contact solver: excluded from parity. */
+    m33 R = mat_from_quat(qconj(b->q_wtb));
+    double r33 = R.m[2][2];
+    double s = 1.0 - r33 * r33; if (s < 0) s = 0;
+    double low = b->pos.z + o->cfg.drone.collision_z_offset - 0.5 * o->cfg.drone.collision_h * fabs(r33)
+                 - o->cfg.drone.collision_r * sqrt(s);
+    if (low < 0.0) {
+        b->pos.z -= low;
+        if (b->vel.z < 0) b->vel.z = 0;
+        return 1;
+    }
+    return 0;
+}
+
+/* ---- Physics.DYN (BaseAviary.py:822-896) ------------------------------------------- */
+static void dyn_step(const orc_t* o, body_t* b, const double rpm[4]) {
+    const adrp_drone_params* d = &o->cfg.drone;
+    const double dt = o->dt;
+    qt q = qconj(b->q_wtb);            /* quat as pybullet reports it (x,y,z,w) */
+    m33 R = mat_from_quat(q);           /* p.getMatrixFromQuaternion */
+    double f[4], zt[4], sum = 0;
+    for (int i = 0; i < 4; ++i) { f[i] = rpm[i] * rpm[i] * d->kf; zt[i] = rpm[i] * rpm[i] * d->km; sum += f[i]; }
+    v3 thrust_w = mv(R, V(0, 0, sum));
+    v3 force_w = vsub(thrust_w, V(0, 0, o->cfg.gravity * d->m));
+    double z_torque = -zt[0] + zt[1] - zt[2] + zt[3];
+    double arm = d->l / sqrt(2.0);
+    double x_torque = (f[0] + f[1] - f[2] - f[3]) * arm;
+    double y_torque = (-f[0] + f[1] + f[2] - f[3]) * arm;
+    v3 J = V(d->ixx, d->iyy, d->izz);
+    v3 tq = vsub(V(x_torque, y_torque, z_torque), vcross(b->rpy_rates, vmul(J, b->rpy_rates)));
+    v3 rdd = V(tq.x / J.x, tq.y / J.y, tq.z / J.z);
+    v3 acc = vscale(force_w, 1.0 / d->m);
+    b->vel = vadd(b->vel, vscale(acc, dt));
+    b->rpy_rates = vadd(b->rpy_rates, vscale(rdd, dt));
+    b->pos = vadd(b->pos, vscale(b->vel, dt));
+    /* _integrateQ (BaseAviary.py:883-896) */
+    v3 w = b->rpy_rates;
+    double wn = vnorm(w);
+    if (!(fabs(wn) <= 1e-8)) {      /* np.isclose(omega_norm, 0): |x| <= atol + rtol*0 */
+        double th = wn * dt / 2, c = cos(th), s = sin(th) * 2 / wn;
+        double p = w.x, qq = w.y, r = w.z;
+        double L[4][4] = {{0, r, -qq, p}, {-r, 0, p, qq}, {qq, -p, 0, r}, {-p, -qq, -r, 0}};
+        double in[4] = {q.x, q.y, q.z, q.w}, outq[4];
+        for (int i = 0; i < 4; ++i) {
+            outq[i] = c * in[i];
+            for (int j = 0; j < 4; ++j) outq[i] += s * 0.5 * L[i][j] * in[j];
+        }
+        q.x = outq[0]; q.y = outq[1]; q.z = outq[2]; q.w = outq[3];
+    }
+    b->q_wtb = qconj(q);                        /* resetBasePositionAndOrientation (unnormalised) */
+    b->ang_v = mv(R, b->rpy_rates);             /* resetBaseVelocity(vel, rotation @ rpy_rates) */
+    b->omega = b->ang_v;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* HoverAviary task                                                                       */
+/* ------------------------------------------------------------------------------------ */
+static void hover_obs(const orc_t* o, int e, float* obs_row) {
+    const body_t* b = &o->b[e];
+    double rpy[3];
+    body_rpy(b, rpy);
+    v3 w = o->cfg.physics == ADRP_PHYS_DYN ? b->ang_v : b->omega;
+    double k12[12] = {b->pos.x, b->pos.y, b->pos.z, rpy[0], rpy[1], rpy[2],
+                      b->vel.x, b->vel.y, b->vel.z, w.x, w.y, w.z};
+    for (int i = 0; i < 12; ++i) obs_row[i] = (float)k12[i];   /* .astype('float32') */
+    const int B = o->cfg.action_buffer_size, A = o->A;
+    const float* ring = o->ring + (size_t)e * B * A;
+    /* deque order: oldest first; ring_head = slot the next append writes */
+    for (int k = 0; k < B; ++k) {
+        int slot = (o->ring_head[e] + k) % B;
+        for (int j = 0; j < A; ++j) obs_row[12 + k * A + j] = ring[slot * A + j];
+    }
+}
+
+static void hover_reset_env(orc_t* o, int e) {
+    body_t* b = &o->b[e];
+    const adrp_config* c = &o->cfg;
+    double u[4], u2[4], u3[4];
+    uint64_t gid = (uint64_t)(c->env_offset + e);
+    draw4(c->seed, gid, (uint32_t)o->episode[e], TAG_HOVER_RESET, 0, u);
+    draw4(c->seed, gid, (uint32_t)o->episode[e], TAG_HOVER_RESET, 1, u2);
+    draw4(c->seed, gid, (uint32_t)o->episode[e], TAG_HOVER_RESET, 2, u3);
+    double pos[3], rpy[3], vel[3], om[3];
+    for (int k = 0; k < 3; ++k) {
+        pos[k] = c->init_xyz[0][k] + c->init_xyz_noise[k] * (2 * u[k] - 1);
+        rpy[k] = c->init_rpy[0][k] + c->init_rpy_noise[k] * (2 * u2[k] - 1);
+        vel[k] = c->init_vel_noise[k] * (2 * u3[k] - 1);
+    }
+    om[0] = c->init_omega_noise[0] * (2 * u[3] - 1);
+    om[1] = c->init_omega_noise[1] * (2 * u2[3] - 1);
+    om[2] = c->init_omega_noise[2] * (2 * u3[3] - 1);
+    double q[4];
+    orc_quat_from_euler(rpy, q);
+    memset(b, 0, sizeof *b);
+    b->pos = V(pos[0], pos[1], pos[2]);
+    qt qq = {q[0], q[1], q[2], q[3]};
+    b->q_wtb = qconj(qq);
+    b->vel = V(vel[0], vel[1], vel[2]);
+    b->omega = V(om[0], om[1], om[2]);
+    if (c->physics == ADRP_PHYS_DYN) {   /* rpy_rates zeroed by _housekeeping; world w kept */
+        b->ang_v = b->omega;
+        m33 R = mat_from_quat(qq);
+        b->rpy_rates = mtv(R, b->omega);
+    }
+    forward_kinematics(b);   /* loadURDF / resetBasePositionAndOrientation */
+    o->step_counter[e] = 0;
+    o->episode[e] += 1;
+}
+
+int orc_reset(orc_t* o, const uint8_t* mask, float* obs) {
+    for (int e = 0; e < o->E; ++e) {
+        if (mask && !mask[e]) continue;
+        hover_reset_env(o, e);
+        if (obs) hover_obs(o, e, obs + (size_t)e * o->D);
+    }
+    return ADRP_OK;
+}
+
+static void hover_task(const orc_t* o, int e, float* rew, uint8_t* term, uint8_t* trunc) {
+    const adrp_config* c = &o->cfg;
+    const body_t* b = &o->b[e];
+    double dx = c->target_pos[0] - b->pos.x, dy = c->target_pos[1] - b->pos.y, dz = c->target_pos[2] - b->pos.z;
+    double dist = sqrt(dx * dx + dy * dy + dz * dz);
+    double r = 2 - dist * dist * dist * dist;       /* HoverAviary.py:68-79 */
+    *rew = (float)(r > 0 ? r : 0);
+    *term = dist < 0.0001;                         /* HoverAviary.py:83-96 */
+    double rpy[3];
+    body_rpy(b, rpy);
+    int tr = fabs(b->pos.x) > 1.5 || fabs(b->pos.y) > 1.5 || b->pos.z > 2.0 || fabs(rpy[0]) > 0.4 ||
+             fabs(rpy[1]) > 0.4;                   /* HoverAviary.py:100-117 */
+    if ((double)o->step_counter[e] / c->pyb_freq > c->episode_len_sec) tr = 1;
+    *trunc = (uint8_t)tr;
+}
+
+static void hover_step_env(orc_t* o, int e, const float* act, float* obs_row, float* rew,
+                           uint8_t* term, uint8_t* trunc, float* terminal_row) {
+    const adrp_config* c = &o->cfg;
+    const int B = c->action_buffer_size, A = o->A;
+    body_t* b = &o->b[e];
+    /* _preprocessAction (BaseRLAviary.py:160-239): action_buffer.append, RPM map in
+       float32 (NEP 50: 1+0.05*a on a float32 action), times float64 HOVER_RPM */
+    float* ring = o->ring + (size_t)e * B * A;
+    for (int j = 0; j < A; ++j) ring[o->ring_head[e] * A + j] = act[j];
+    o->ring_head[e] = (o->ring_head[e] + 1) % B;
+    double rpm[4];
+    orc_hover_rpm(c, act, rpm);
+    uint8_t touched = 0;
+    for (int s = 0; s < o->S; ++s) {
+        if (c->physics == ADRP_PHYS_DYN) {
+            dyn_step(o, b, rpm);
+        } else {
+            forces_t F;
+            assemble_forces(o, &F, b, 0, rpm, b->last_rpm);
+            F.base_f_world = V(0, 0, -c->gravity * c->drone.m);
+            touched |= (uint8_t)bullet_step(o, b, &F, c->drone.m, V(c->drone.ixx, c->drone.iyy, c->drone.izz));
+        }
+        memcpy(b->last_rpm, rpm, sizeof rpm);   /* self.last_clipped_action = clipped_action */
+    }
+    o->contact[e] = touched;
+    o->contacts += touched;
+    hover_obs(o, e, obs_row);
+    hover_task(o, e, rew, term, trunc);
+    o->step_counter[e] += o->S;                    /* BaseAviary.py:386 */
+    if (c->autoreset && (*term || *trunc)) {
+        if (terminal_row) memcpy(terminal_row, obs_row, sizeof(float) * o->D);
+        hover_reset_env(o, e);
+        hover_obs(o, e, obs_row);
+    }
+}
+
+int orc_hover_eval(const orc_t* o, float* obs, float* rew, uint8_t* term, uint8_t* trunc) {
+    for (int e = 0; e < o->E; ++e) {
+        hover_obs(o, e, obs + (size_t)e * o->D);
+        hover_task(o, e, rew + e, term + e, trunc + e);
+    }
+    return ADRP_OK;
+}
+
+int orc_step(orc_t* o, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
+             float* terminal_obs) {
+    o->contacts = 0;
+    for (int e = 0; e < o->E; ++e)
+        hover_step_env(o, e, act + (size_t)e * o->A, obs + (size_t)e * o->D, rew + e, term + e, trunc + e,
+                       terminal_obs ? terminal_obs + (size_t)e * o->D : NULL);
+    return ADRP_OK;
+}
+
+/* ---- state snapshot (same field names/order as libadrp) ---------------------------- */
+static const char* k_hover_f[] = {"pos_x", "pos_y", "pos_z", "quat_x", "quat_y", "quat_z", "quat_w",
+                                  "vel_x", "vel_y", "vel_z", "omega_x", "omega_y", "omega_z",
+                                  "last_rpm_0", "last_rpm_1", "last_rpm_2", "last_rpm_3",
+                                  "angv_x", "angv_y", "angv_z",
+                                  "link_quat_x", "link_quat_y", "link_quat_z", "link_quat_w",
+                                  "link_pos_x", "link_pos_y", "link_pos_z"};
+static const char* k_hover_i[] = {"step_counter", "episode", "ring_head"};
+#define HOVER_NF_BASE 27
+
+int orc_state_layout(const orc_t* o, int* nf, int* ni) {
+    *nf = HOVER_NF_BASE + o->cfg.action_buffer_size * o->A;
+    *ni = 3;
+    return ADRP_OK;
+}
+const char* orc_state_field(const orc_t* o, int is_int, int index) {
+    static char buf[32];
+    if (is_int) return (index >= 0 && index < 3) ? k_hover_i[index] : NULL;
+    if (index < 0) return NULL;
+    if (index < HOVER_NF_BASE) return k_hover_f[index];
+    int k = index - HOVER_NF_BASE;
+    if (k >= o->cfg.action_buffer_size * o->A) return NULL;
+    snprintf(buf, sizeof buf, "ring_%d_%d", k / o->A, k % o->A);
+    return buf;
+}
+
+int orc_get_state(const orc_t* o, double* f, int32_t* ii) {
+    int nf, ni;
+    orc_state_layout(o, &nf, &ni);
+    const int E = o->E, B = o->cfg.action_buffer_size, A = o->A;
+    for (int e = 0; e < E; ++e) {
+        const body_t* b = &o->b[e];
+        qt q = qconj(b->q_wtb);
+        v3 w = o->cfg.physics == ADRP_PHYS_DYN ? b->rpy_rates : b->omega;
+        qt lq = qconj(b->link_q_wtb);
+        double v[HOVER_NF_BASE] = {b->pos.x, b->pos.y, b->pos.z, q.x, q.y, q.z, q.w, b->vel.x, b->vel.y, b->vel.z,
+                                   w.x, w.y, w.z, b->last_rpm[0], b->last_rpm[1], b->last_rpm[2], b->last_rpm[3],
+                                   b->ang_v.x, b->ang_v.y, b->ang_v.z, lq.x, lq.y, lq.z, lq.w,
+                                   b->link_pos.x, b->link_pos.y, b->link_pos.z};
+        for (int k = 0; k < HOVER_NF_BASE; ++k) f[(size_t)k * E + e] = v[k];
+        for (int k = 0; k < B * A; ++k) f[(size_t)(HOVER_NF_BASE + k) * E + e] = o->ring[(size_t)e * B * A + k];
+        ii[e] = o->step_counter[e];
+        ii[E + e] = o->episode[e];
+        ii[2 * E + e] = o->ring_head[e];
+    }
+    return ADRP_OK;
+}
+
+int orc_set_state(orc_t* o, const double* f, const int32_t* ii) {
+    const int E = o->E, B = o->cfg.action_buffer_size, A = o->A;
+    for (int e = 0; e < E; ++e) {
+        body_t* b = &o->b[e];
+#define F_(k) f[(size_t)(k) * E + e]
+        b->pos = V(F_(0), F_(1), F_(2));
+        qt q = {F_(3), F_(4), F_(5), F_(6)};
+        b->q_wtb = qconj(q);
+        b->vel = V(F_(7), F_(8), F_(9));
+        if (o->cfg.physics == ADRP_PHYS_DYN) {
+            b->rpy_rates = V(F_(10), F_(11), F_(12));
+            b->ang_v = V(F_(17), F_(18), F_(19));
+            b->omega = b->ang_v;
+        } else {
+            b->omega = V(F_(10), F_(11), F_(12));
+            b->ang_v = V(F_(17), F_(18), F_(19));
+        }
+        for (int k = 0; k < 4; ++k) b->last_rpm[k] = F_(13 + k);
+        qt lq = {F_(20), F_(21), F_(22), F_(23)};
+        b->link_q_wtb = qconj(lq);
+        b->link_pos = V(F_(24), F_(25), F_(26));
+        for (int k = 0; k < B * A; ++k) o->ring[(size_t)e * B * A + k] = (float)F_(HOVER_NF_BASE + k);
+#undef F_
+        o->step_counter[e] = ii[e];
+        o->episode[e] = ii[E + e];
+        o->ring_head[e] = ii[2 * E + e];
+    }
+    return ADRP_OK;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Mellinger wrapper arithmetic (control/MellingerControl.py)                             */
+/* ------------------------------------------------------------------------------------ */
+#define MIN_PWM 20000.0
+#define MAX_PWM 65535.0
+#define PWM2RPM_SCALE 0.2685
+#define PWM2RPM_CONST 4070.3
+#define SUPPLY_VOLTAGE 3.0
+#define MEL_KF 3.16e-10   /* MellingerControl.py:270 */
+
+/* _compute_pwms (MellingerControl.py:423-442); control = roll, pitch, yaw, thrust */
+void orc_compute_pwms(const double control[4], double pwm[4]) {
+    double r = control[0] / 2, p = control[1] / 2, y = control[2], t = control[3];
+    double th[4] = {t - r + p + y, t - r - p - y, t + r - p + y, t + r + p - y};
+    for (int i = 0; i < 4; ++i) {
+        double x = clampd(th[i], 0, MAX_PWM) / MAX_PWM * 60;
+        double volts = -0.0006239 * x * x + 0.088 * x;
+        double pct = volts / SUPPLY_VOLTAGE;
+        if (pct > 1) pct = 1;
+        pwm[i] = pct * MAX_PWM;
+    }
+}
+/* MellingerControl.computeControl tail (:246-262) + _thr2pwm (:307-343) */
+void orc_pwms_to_rpms(const double pwm[4], const double noise[4], double rpm[4]) {
+    double thrust[4], tr[4];
+    for (int i = 0; i < 4; ++i) {
+        double c = clampd(pwm[i], MIN_PWM, MAX_PWM);
+        double r = PWM2RPM_SCALE * c + PWM2RPM_CONST;
+        thrust[i] = MEL_KF * r * r;
+    }
+    for (int i = 0; i < 4; ++i) tr[i] = thrust[3 - i] + noise[i];  /* reorder [3,2,1,0] + noise */
+    for (int i = 0; i < 4; ++i) {
+        double t = tr[i] < 0 ? 0 : tr[i];
+        double mp = (sqrt(t / 1 / MEL_KF) - PWM2RPM_CONST) / PWM2RPM_SCALE;
+        mp = clampd(mp, MIN_PWM, MAX_PWM);
+        rpm[i] = PWM2RPM_SCALE * mp + PWM2RPM_CONST;
+    }
+}
+/* _step_controller tick schedule (MellingerControl.py:393-411) in float64, no tumbling */
+int orc_tick_schedule(int n, uint8_t* ticks) {
+    double last_att = 0, last_pos = 0;
+    for (int tick = 0; tick < n; ++tick) {
+        double cur = tick / 500.0;
+        if ((cur - last_att > 0.002) && (cur - last_pos > 0.01)) {
+            ticks[tick] = 0; last_pos = cur; last_att = cur;
+        } else if (cur - last_att > 0.002) {
+            last_att = cur; ticks[tick] = 2;
+        } else {
+            ticks[tick] = 1;
+        }
+    }
+    return ADRP_OK;
+}
+
+uint32_t orc_config_size(void) { return (uint32_t)sizeof(adrp_config); }

@@ -1,0 +1,211 @@
+"""ctypes binding of the CPU oracle (oracle/oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.  The
+product package (gym_pybullet_adrp_amd) never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+def build(force=False):
+    src = os.path.join(HERE, "oracle.c")
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
+            os.path.getmtime(src), os.path.getmtime(os.path.join(HERE, "oracle.h")),
+            os.path.getmtime(os.path.join(HERE, "..", "include", "adrp.h"))):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB
+
+
+def _load():
+    build()
+    lib = ctypes.CDLL(LIB)
+    P, I, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    lib.orc_create.argtypes = [P, ctypes.POINTER(P)]
+    lib.orc_create.restype = I
+    lib.orc_destroy.argtypes = [P]
+    lib.orc_last_error.restype = ctypes.c_char_p
+    for f in ("orc_obs_dim", "orc_act_dim"):
+        getattr(lib, f).argtypes = [P]
+        getattr(lib, f).restype = I
+    lib.orc_reset.argtypes = [P, P, P]
+    lib.orc_step.argtypes = [P, P, P, P, P, P, P]
+    lib.orc_state_layout.argtypes = [P, ctypes.POINTER(I), ctypes.POINTER(I)]
+    lib.orc_state_field.argtypes = [P, I, I]
+    lib.orc_state_field.restype = ctypes.c_char_p
+    lib.orc_get_state.argtypes = [P, P, P]
+    lib.orc_set_state.argtypes = [P, P, P]
+    lib.orc_contact_count.argtypes = [P]
+    lib.orc_contact_count.restype = ctypes.c_int64
+    lib.orc_env_contact.argtypes = [P, I]
+    lib.orc_env_contact.restype = ctypes.c_uint8
+    lib.orc_default_config.argtypes = [I, P]
+    lib.orc_philox4x32_10.argtypes = [P, P, P]
+    lib.orc_euler_from_quat.argtypes = [P, P]
+    lib.orc_quat_from_euler.argtypes = [P, P]
+    lib.orc_derived_constants.argtypes = [P, P]
+    lib.orc_force_assembly.argtypes = [P, I, P, I, P, P, P, P]
+    lib.orc_hover_rpm.argtypes = [P, P, P]
+    lib.orc_hover_eval.argtypes = [P, P, P, P, P]
+    lib.orc_config_size.restype = ctypes.c_uint32
+    lib.orc_compute_pwms.argtypes = [P, P]
+    lib.orc_pwms_to_rpms.argtypes = [P, P, P]
+    lib.orc_tick_schedule.argtypes = [I, P]
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Oracle:
+    """Batched CPU restatement behind the same config struct as libadrp."""
+
+    def __init__(self, cfg):
+        from gym_pybullet_adrp_amd.utils.abi import AdrpConfig  # struct layout only
+        assert isinstance(cfg, AdrpConfig)
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        rc = lib().orc_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != 0:
+            raise ValueError(lib().orc_last_error().decode())
+        self.h = h
+        self.E, self.N = cfg.num_envs, cfg.num_drones
+        self.D = lib().orc_obs_dim(h)
+        self.A = lib().orc_act_dim(h)
+        nf, ni = ctypes.c_int(), ctypes.c_int()
+        lib().orc_state_layout(h, ctypes.byref(nf), ctypes.byref(ni))
+        self.nf, self.ni = nf.value, ni.value
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_destroy(self.h)
+            self.h = None
+
+    def field_names(self):
+        return ([lib().orc_state_field(self.h, 0, k).decode() for k in range(self.nf)],
+                [lib().orc_state_field(self.h, 1, k).decode() for k in range(self.ni)])
+
+    def reset(self, mask=None):
+        obs = np.zeros((self.E, self.N, self.D), np.float32)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        lib().orc_reset(self.h, _ptr(m), _ptr(obs))
+        return obs
+
+    def step(self, act):
+        act = np.ascontiguousarray(act, np.float32).reshape(self.E, self.N, self.A)
+        obs = np.zeros((self.E, self.N, self.D), np.float32)
+        tobs = np.zeros_like(obs)
+        rew = np.zeros(self.E, np.float32)
+        term = np.zeros(self.E, np.uint8)
+        trunc = np.zeros(self.E, np.uint8)
+        lib().orc_step(self.h, _ptr(act), _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(tobs))
+        return obs, rew, term.astype(bool), trunc.astype(bool), tobs
+
+    def get_state(self):
+        f = np.zeros((self.nf, self.E * self.N), np.float64)
+        i = np.zeros((self.ni, self.E * self.N), np.int32)
+        lib().orc_get_state(self.h, _ptr(f), _ptr(i))
+        return f, i
+
+    def set_state(self, f, i):
+        f = np.ascontiguousarray(f, np.float64)
+        i = np.ascontiguousarray(i, np.int32)
+        assert f.shape == (self.nf, self.E * self.N) and i.shape == (self.ni, self.E * self.N)
+        lib().orc_set_state(self.h, _ptr(f), _ptr(i))
+
+    def contact_count(self):
+        return lib().orc_contact_count(self.h)
+
+    def env_contact(self):
+        return np.array([lib().orc_env_contact(self.h, e) for e in range(self.E)], bool)
+
+    def hover_eval(self):
+        obs = np.zeros((self.E, self.N, self.D), np.float32)
+        rew = np.zeros(self.E, np.float32)
+        term = np.zeros(self.E, np.uint8)
+        trunc = np.zeros(self.E, np.uint8)
+        lib().orc_hover_eval(self.h, _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc))
+        return obs, rew, term.astype(bool), trunc.astype(bool)
+
+
+def force_assembly(cfg, states, n, rpm, prev):
+    """states: [N, 13] rows pos3, quat4 (xyzw), vel3, omega3 -> (link_force, link_torque) [5,3]."""
+    st = np.ascontiguousarray(states, float)
+    lf = np.zeros((5, 3)); lt = np.zeros((5, 3))
+    rc = lib().orc_force_assembly(ctypes.byref(cfg), st.shape[0], _ptr(st), n,
+                                  _ptr(np.ascontiguousarray(rpm, float)),
+                                  _ptr(np.ascontiguousarray(prev, float)), _ptr(lf), _ptr(lt))
+    assert rc == 0, lib().orc_last_error()
+    return lf, lt
+
+
+def hover_rpm(cfg, act):
+    a = np.ascontiguousarray(act, np.float32); o = np.zeros(4)
+    lib().orc_hover_rpm(ctypes.byref(cfg), _ptr(a), _ptr(o))
+    return o
+
+
+def philox(ctr, key):
+    c = np.ascontiguousarray(ctr, np.uint32); k = np.ascontiguousarray(key, np.uint32)
+    o = np.zeros(4, np.uint32)
+    lib().orc_philox4x32_10(_ptr(c), _ptr(k), _ptr(o))
+    return o
+
+
+def euler_from_quat(q):
+    q = np.ascontiguousarray(q, float); r = np.zeros(3)
+    lib().orc_euler_from_quat(_ptr(q), _ptr(r))
+    return r
+
+
+def quat_from_euler(e):
+    e = np.ascontiguousarray(e, float); q = np.zeros(4)
+    lib().orc_quat_from_euler(_ptr(e), _ptr(q))
+    return q
+
+
+def derived_constants(cfg):
+    out = np.zeros(6)
+    lib().orc_derived_constants(ctypes.byref(cfg), _ptr(out))
+    return out
+
+
+def default_config(task):
+    from gym_pybullet_adrp_amd.utils.abi import AdrpConfig
+    cfg = AdrpConfig()
+    lib().orc_default_config(task, ctypes.byref(cfg))
+    return cfg
+
+
+def compute_pwms(control):
+    c = np.ascontiguousarray(control, float); o = np.zeros(4)
+    lib().orc_compute_pwms(_ptr(c), _ptr(o))
+    return o
+
+
+def pwms_to_rpms(pwm, noise):
+    p = np.ascontiguousarray(pwm, float); n = np.ascontiguousarray(noise, float); o = np.zeros(4)
+    lib().orc_pwms_to_rpms(_ptr(p), _ptr(n), _ptr(o))
+    return o
+
+
+def tick_schedule(n):
+    o = np.zeros(n, np.uint8)
+    lib().orc_tick_schedule(n, _ptr(o))
+    return o

@@ -1,0 +1,507 @@
+"""Generate golden fixtures from the reference's own Python code (run HERE only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+
+The reference (FelixWaiblinger/gym-pybullet-adrp @ 2024-10-08) imports pybullet,
+gymnasium and munch, none of which exist in this image.  Its pure-numpy code paths are
+executed unchanged under minimal stand-ins installed into ``sys.modules``:
+
+* ``pybullet``: a kinematic pose store (loadURDF / resetBase* / getBase*), the three
+  math helpers (getQuaternionFromEuler / getEulerFromQuaternion / getMatrixFromQuaternion
+  via scipy's extrinsic 'xyz' convention, which is pybullet's away from gimbal lock),
+  getLinkStates by forward kinematics of the URDF prop offsets, and *recorders* for
+  applyExternalForce / applyExternalTorque.  Anything else raises.  stepSimulation is
+  not available, so the Bullet integration itself is NOT pinned by these fixtures.
+* ``gymnasium`` (Env, Wrapper, spaces.Box, envs.registration.register) and ``munch``.
+* ``gym_pybullet_adrp.envs`` / ``.control`` are registered as bare packages so that their
+  ``__init__`` files (which import Betaflight / pycffirmware code paths) are bypassed.
+* MellingerControl gets a fake ``firm`` object that records what the wrapper hands the
+  firmware and returns preset control outputs.
+
+Only data (inputs and the reference's outputs) is written, to tests/golden/*.npz.
+"""
+import importlib
+import math
+import os
+import sys
+import types
+
+import numpy as np
+from scipy.spatial.transform import Rotation
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+
+# --------------------------------------------------------------------------------------
+# stand-ins
+# --------------------------------------------------------------------------------------
+PROP_OFFSETS = {  # inertial origins of prop0..3 / center_of_mass links, cf2x_IROS.urdf:41-99
+    0: (0.028, 0.028, 0.0), 1: (-0.028, 0.028, 0.0), 2: (-0.028, -0.028, 0.0),
+    3: (0.028, -0.028, 0.0), 4: (0.0, 0.0, 0.0)}
+
+
+class _PB(types.ModuleType):
+    DIRECT, GUI = 1, 2
+    LINK_FRAME, WORLD_FRAME = 1, 2
+    URDF_USE_INERTIA_FROM_FILE = 8
+
+    def __init__(self):
+        super().__init__("pybullet")
+        self.reset_store()
+
+    def reset_store(self):
+        self.bodies = {}
+        self.next_id = 0
+        self.forces = []       # (body, link, force, pos, flags)
+        self.torques = []      # (body, link, torque, flags)
+        self.contacts = {}     # (bodyA, bodyB) -> bool
+        self.closest = {}      # (bodyA, bodyB) -> bool
+        self.rays = None
+
+    # --- client / world ---
+    def connect(self, *a, **k): return 0
+    def disconnect(self, *a, **k): pass
+    def resetSimulation(self, *a, **k):
+        self.bodies = {}
+        self.next_id = 0
+    def setGravity(self, *a, **k): pass
+    def setRealTimeSimulation(self, *a, **k): pass
+    def setTimeStep(self, *a, **k): pass
+    def setAdditionalSearchPath(self, *a, **k): pass
+    def changeDynamics(self, *a, **k): pass
+    def setCollisionFilterPair(self, *a, **k): pass
+
+    def loadURDF(self, name, basePosition=(0, 0, 0), baseOrientation=(0, 0, 0, 1), **k):
+        bid = self.next_id
+        self.next_id += 1
+        self.bodies[bid] = dict(name=str(name), pos=np.array(basePosition, float),
+                                quat=np.array(baseOrientation, float),
+                                vel=np.zeros(3), ang=np.zeros(3))
+        return bid
+
+    def resetBasePositionAndOrientation(self, bid, pos, quat, physicsClientId=0):
+        self.bodies[bid]["pos"] = np.array(pos, float)
+        self.bodies[bid]["quat"] = np.array(quat, float)
+
+    def resetBaseVelocity(self, bid, linearVelocity, angularVelocity=(0, 0, 0), physicsClientId=0):
+        self.bodies[bid]["vel"] = np.array(linearVelocity, float)
+        self.bodies[bid]["ang"] = np.array(angularVelocity, float)
+
+    def getBasePositionAndOrientation(self, bid, physicsClientId=0):
+        b = self.bodies[bid]
+        return tuple(b["pos"]), tuple(b["quat"])
+
+    def getBaseVelocity(self, bid, physicsClientId=0):
+        b = self.bodies[bid]
+        return tuple(b["vel"]), tuple(b["ang"])
+
+    # --- math helpers ---
+    def getQuaternionFromEuler(self, rpy):
+        r, p, y = rpy
+        cr, sr = math.cos(r / 2), math.sin(r / 2)
+        cp, sp = math.cos(p / 2), math.sin(p / 2)
+        cy, sy = math.cos(y / 2), math.sin(y / 2)
+        return (sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy,
+                cr * cp * sy - sr * sp * cy, cr * cp * cy + sr * sp * sy)
+
+    def getEulerFromQuaternion(self, q):
+        return tuple(Rotation.from_quat(np.asarray(q, float)).as_euler("xyz"))
+
+    def getMatrixFromQuaternion(self, q):
+        return tuple(Rotation.from_quat(np.asarray(q, float)).as_matrix().reshape(9))
+
+    def getLinkStates(self, bid, linkIndices, computeLinkVelocity=0, computeForwardKinematics=0,
+                      physicsClientId=0):
+        b = self.bodies[bid]
+        R = Rotation.from_quat(b["quat"]).as_matrix()
+        out = []
+        for i in linkIndices:
+            w = b["pos"] + R @ np.array(PROP_OFFSETS[i])
+            out.append((tuple(w), tuple(b["quat"])))
+        return out
+
+    # --- recorders / scripted queries ---
+    def applyExternalForce(self, bid, linkIndex, forceObj, posObj, flags, physicsClientId=0):
+        self.forces.append((bid, linkIndex, np.array(forceObj, float), np.array(posObj, float), flags))
+
+    def applyExternalTorque(self, bid, linkIndex, torqueObj, flags, physicsClientId=0):
+        self.torques.append((bid, linkIndex, np.array(torqueObj, float), flags))
+
+    def getContactPoints(self, bodyA=None, bodyB=None, physicsClientId=0):
+        return [1] if self.contacts.get((bodyA, bodyB), False) else []
+
+    def getClosestPoints(self, bodyA, bodyB, distance, physicsClientId=0):
+        return [1] if self.closest.get((bodyA, bodyB), False) else []
+
+    def rayTestBatch(self, rayFromPositions, rayToPositions, physicsClientId=0):
+        self.rays = (np.array(rayFromPositions), np.array(rayToPositions))
+        return self.ray_result
+
+    def stepSimulation(self, *a, **k):
+        raise RuntimeError("stepSimulation is not available: Bullet is not in this image")
+
+    def __getattr__(self, name):
+        raise AttributeError(f"pybullet stand-in has no {name}")
+
+
+def install_stubs():
+    pb = _PB()
+    sys.modules["pybullet"] = pb
+    pbd = types.ModuleType("pybullet_data")
+    pbd.getDataPath = lambda: "/nonexistent"
+    sys.modules["pybullet_data"] = pbd
+
+    gym = types.ModuleType("gymnasium")
+
+    class Env:
+        _np_random = None
+
+        @property
+        def np_random(self):
+            if self._np_random is None:
+                self._np_random = np.random.default_rng(0)
+            return self._np_random
+
+    class Wrapper(Env):
+        def __init__(self, env):
+            self.env = env
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.low = np.broadcast_to(np.asarray(low), shape) if shape else np.asarray(low)
+            self.high = np.broadcast_to(np.asarray(high), shape) if shape else np.asarray(high)
+            self.shape = self.low.shape
+            self.dtype = np.dtype(dtype)
+
+    spaces = types.ModuleType("gymnasium.spaces")
+    spaces.Box = Box
+    envs = types.ModuleType("gymnasium.envs")
+    reg = types.ModuleType("gymnasium.envs.registration")
+    reg.register = lambda **k: None
+    gym.Env, gym.Wrapper, gym.spaces = Env, Wrapper, spaces
+    sys.modules.update({"gymnasium": gym, "gymnasium.spaces": spaces, "gymnasium.envs": envs,
+                        "gymnasium.envs.registration": reg})
+
+    munch = types.ModuleType("munch")
+
+    class Munch(dict):
+        def __getattr__(self, k):
+            try:
+                return self[k]
+            except KeyError as e:
+                raise AttributeError(k) from e
+
+        def __setattr__(self, k, v):
+            self[k] = v
+
+    def munchify(x):
+        if isinstance(x, dict):
+            return Munch({k: munchify(v) for k, v in x.items()})
+        if isinstance(x, list):
+            return [munchify(v) for v in x]
+        return x
+
+    munch.Munch, munch.munchify = Munch, munchify
+    sys.modules["munch"] = munch
+    return pb
+
+
+def import_reference(pb):
+    sys.path.insert(0, REF)
+    import gym_pybullet_adrp  # noqa: F401  (registry, stubbed)
+    for sub in ("envs", "control"):
+        mod = types.ModuleType(f"gym_pybullet_adrp.{sub}")
+        mod.__path__ = [os.path.join(REF, "gym_pybullet_adrp", sub)]
+        sys.modules[f"gym_pybullet_adrp.{sub}"] = mod
+    ctrl = sys.modules["gym_pybullet_adrp.control"]
+    ctrl.BaseControl = importlib.import_module("gym_pybullet_adrp.control.BaseControl").BaseControl
+    ctrl.low_level_control = lambda *a, **k: None
+    m = types.SimpleNamespace()
+    m.enums = importlib.import_module("gym_pybullet_adrp.utils.enums")
+    m.utils = importlib.import_module("gym_pybullet_adrp.utils.utils")
+    m.BaseAviary = importlib.import_module("gym_pybullet_adrp.envs.BaseAviary")
+    m.Hover = importlib.import_module("gym_pybullet_adrp.envs.HoverAviary")
+    m.Mellinger = importlib.import_module("gym_pybullet_adrp.control.MellingerControl")
+    m.MultiRace = importlib.import_module("gym_pybullet_adrp.envs.MultiRaceAviary")
+    m.wrapper = importlib.import_module("gym_pybullet_adrp.utils.wrapper")
+    return m
+
+
+# --------------------------------------------------------------------------------------
+# fixtures
+# --------------------------------------------------------------------------------------
+def set_drone_state(pb, env, i, pos, quat, vel, ang):
+    did = env.DRONE_IDS[i]
+    pb.resetBasePositionAndOrientation(did, pos, quat)
+    pb.resetBaseVelocity(did, vel, ang)
+
+
+def random_state(rng, center=(0, 0, 1), tilt=0.3):
+    pos = np.asarray(center) + rng.uniform(-0.5, 0.5, 3)
+    rpy = rng.uniform(-tilt, tilt, 3) * np.array([1, 1, 3])
+    quat = np.array(sys.modules["pybullet"].getQuaternionFromEuler(rpy))
+    return pos, quat, rng.uniform(-1, 1, 3), rng.uniform(-2, 2, 3)
+
+
+def hover_fixtures(pb, m):
+    E = m.enums
+    out = {}
+    env = m.Hover.HoverAviary(physics=E.Physics.PYB, act=E.ActionType.RPM)
+    out["derived"] = np.array([env.HOVER_RPM, env.MAX_RPM, env.MAX_THRUST, env.GND_EFF_H_CLIP,
+                               env.MAX_XY_TORQUE, env.MAX_Z_TORQUE])
+    obs0, _ = env.reset()
+    out["reset_obs"] = np.asarray(obs0)
+    rng = np.random.default_rng(7)
+
+    # (1) preprocess + obs assembly + reward / terminated / truncated on sampled states
+    n = 200
+    acts = rng.uniform(-1, 1, (n, 1, 4)).astype(np.float32)
+    states = np.zeros((n, 13))
+    rpms = np.zeros((n, 4)); obs = np.zeros((n, 72)); rew = np.zeros(n)
+    term = np.zeros(n, bool); trunc = np.zeros(n, bool); counters = np.zeros(n, np.int64)
+    for k in range(n):
+        pos, quat, vel, ang = random_state(rng, tilt=0.3)
+        if k % 17 == 0:
+            pos = np.array([0.0, 0.0, 1.0]) + rng.uniform(-5e-5, 5e-5, 3)   # terminated case
+        if k % 23 == 0:
+            pos[0] = 1.5 + rng.uniform(-0.01, 0.01)                          # bound edge
+        counter = int(rng.choice([0, 8, 1920, 1928, 1936, int(rng.integers(0, 2000))]))
+        set_drone_state(pb, env, 0, pos, quat, vel, ang)
+        env.step_counter = counter
+        rpm = env._preprocessAction(acts[k])
+        env._updateAndStoreKinematicInformation()
+        states[k] = np.concatenate([pos, quat, vel, ang])
+        rpms[k] = rpm[0]
+        obs[k] = env._computeObs()[0]
+        rew[k] = env._computeReward()
+        term[k] = env._computeTerminated()
+        trunc[k] = env._computeTruncated()
+        counters[k] = counter
+    out.update(pp_act=acts, pp_rpm=rpms, task_state=states, task_obs=obs, task_rew=rew,
+               task_term=term, task_trunc=trunc, task_counter=counters)
+
+    # ONE_D_RPM preprocess
+    env1 = m.Hover.HoverAviary(physics=E.Physics.PYB, act=E.ActionType.ONE_D_RPM)
+    a1 = rng.uniform(-1, 1, (64, 1, 1)).astype(np.float32)
+    out["pp1_act"] = a1
+    out["pp1_rpm"] = np.array([env1._preprocessAction(a)[0] for a in a1])
+    return out
+
+
+def force_fixtures(pb, m):
+    """PYB force assembly: what _physics/_groundEffect/_drag/_downwash hand to pybullet."""
+    E = m.enums
+    rng = np.random.default_rng(11)
+    out = {}
+    for name, phys in (("pyb", E.Physics.PYB), ("gnd", E.Physics.PYB_GND), ("drag", E.Physics.PYB_DRAG),
+                       ("dw", E.Physics.PYB_DW), ("all", E.Physics.PYB_GND_DRAG_DW)):
+        nd = 3 if phys in (E.Physics.PYB_DW, E.Physics.PYB_GND_DRAG_DW) else 1
+        # HoverAviary is single-drone; use its base classes directly for N > 1
+        env = m.Hover.HoverAviary(physics=phys) if nd == 1 else _multi(m, phys, nd)
+        env.reset()
+        n = 64
+        S = np.zeros((n, nd, 13)); RPM = np.zeros((n, 4)); PREV = np.zeros((n, 4))
+        LF = np.zeros((n, 5, 3)); LT = np.zeros((n, 5, 3))
+        for k in range(n):
+            for i in range(nd):
+                low = 0.02 if (k % 5 == 0 and i == 0) else 0.3
+                pos, quat, vel, ang = random_state(rng, center=(0, 0, low + 0.4), tilt=0.4)
+                if i > 0:
+                    pos = S[k, 0, :3] + np.array([rng.uniform(-0.3, 0.3), rng.uniform(-0.3, 0.3),
+                                                  rng.uniform(0.02, 0.6)])
+                set_drone_state(pb, env, i, pos, quat, vel, ang)
+                S[k, i] = np.concatenate([pos, quat, vel, ang])
+            env._updateAndStoreKinematicInformation()
+            rpm = rng.uniform(0.5, 1.2, 4) * env.HOVER_RPM
+            prev = rng.uniform(0.5, 1.2, 4) * env.HOVER_RPM
+            pb.forces.clear(); pb.torques.clear()
+            env._physics(rpm, 0)
+            if phys in (E.Physics.PYB_GND, E.Physics.PYB_GND_DRAG_DW):
+                env._groundEffect(rpm, 0)
+            if phys in (E.Physics.PYB_DRAG, E.Physics.PYB_GND_DRAG_DW):
+                env._drag(prev, 0)
+            if phys in (E.Physics.PYB_DW, E.Physics.PYB_GND_DRAG_DW):
+                env._downwash(0)
+            for (bid, link, f, p, fl) in pb.forces:
+                assert bid == env.DRONE_IDS[0] and fl == pb.LINK_FRAME and not np.any(p)
+                LF[k, link] += f
+            for (bid, link, t, fl) in pb.torques:
+                assert fl == pb.LINK_FRAME
+                LT[k, link] += t
+            RPM[k], PREV[k] = rpm, prev
+        out.update({f"{name}_state": S, f"{name}_rpm": RPM, f"{name}_prev": PREV,
+                    f"{name}_link_force": LF, f"{name}_link_torque": LT})
+    return out
+
+
+def _multi(m, phys, nd):
+    """A BaseRLAviary with nd drones (MultiHoverAviary is out of scope; reuse Hover's
+    task hooks on drone 0 only, the force models are per-drone)."""
+    E = m.enums
+    BRL = importlib.import_module("gym_pybullet_adrp.envs.BaseRLAviary").BaseRLAviary
+
+    class _Multi(BRL):
+        def _computeReward(self): return 0
+        def _computeTerminated(self): return False
+        def _computeTruncated(self): return False
+        def _computeInfo(self): return {}
+
+    return _Multi(num_drones=nd, physics=phys, pyb_freq=240, ctrl_freq=30, act=E.ActionType.RPM)
+
+
+def dyn_fixtures(pb, m):
+    """Physics.DYN full episodes through HoverAviary.step (fully reference code)."""
+    E = m.enums
+    rng = np.random.default_rng(3)
+    env = m.Hover.HoverAviary(physics=E.Physics.DYN, act=E.ActionType.RPM)
+    n_ep, T = 12, 40
+    init = np.zeros((n_ep, 13)); acts = rng.uniform(-1, 1, (n_ep, T, 1, 4)).astype(np.float32)
+    obs = np.zeros((n_ep, T, 72)); rew = np.zeros((n_ep, T)); term = np.zeros((n_ep, T), bool)
+    trunc = np.zeros((n_ep, T), bool)
+    ring0 = np.zeros((n_ep, 15, 4), np.float32)
+    states = np.zeros((n_ep, T, 13))
+    for ep in range(n_ep):
+        env.reset()
+        pos, quat, vel, ang = random_state(rng, center=(0, 0, 1.0), tilt=0.1)
+        set_drone_state(pb, env, 0, pos, quat, vel, np.zeros(3))
+        init[ep] = np.concatenate([pos, quat, vel, np.zeros(3)])
+        ring0[ep] = np.array([np.asarray(a).reshape(4) for a in env.action_buffer])
+        for t in range(T):
+            o, r, te, tr, _ = env.step(acts[ep, t])
+            obs[ep, t] = o[0]; rew[ep, t] = r; term[ep, t] = te; trunc[ep, t] = tr
+            states[ep, t] = np.concatenate([env.pos[0], env.quat[0], env.vel[0], env.rpy_rates[0]])
+    return dict(dyn_init=init, dyn_ring0=ring0, dyn_act=acts, dyn_obs=obs, dyn_rew=rew,
+                dyn_term=term, dyn_trunc=trunc, dyn_state=states)
+
+
+class _FakeFirm:
+    """Records what MellingerControl hands the firmware; returns preset outputs."""
+
+    class _Obj:
+        def __init__(self, **kw):
+            self.__dict__.update(kw)
+
+    def __init__(self):
+        self.calls = []
+        self.preset = (0.0, 0.0, 0.0, 0.0)
+        self.modeAbs, self.modeDisable = 1, 0
+
+    def _vec(self):
+        return self._Obj(x=0.0, y=0.0, z=0.0, timestamp=0)
+
+    def lpf2pData(self): return self._Obj()
+    def lpf2pInit(self, d, fs, fc): d.fs, d.fc = fs, fc
+    def lpf2pApply(self, d, v): return v
+    def control_t(self): return self._Obj(roll=0, pitch=0, yaw=0, thrust=0.0)
+
+    def setpoint_t(self):
+        o = self._Obj()
+        o.position, o.velocity, o.acceleration = self._vec(), self._vec(), self._vec()
+        o.attitudeRate = self._Obj(roll=0.0, pitch=0.0, yaw=0.0)
+        o.attitudeQuaternion = self._Obj(x=0.0, y=0.0, z=0.0, w=1.0)
+        o.mode = self._Obj(x=0, y=0, z=0, quat=0, roll=0, pitch=0, yaw=0)
+        return o
+
+    def sensorData_t(self):
+        return self._Obj(acc=self._vec(), gyro=self._vec(), interruptTimestamp=0)
+
+    def state_t(self):
+        return self._Obj(attitude=self._Obj(roll=0.0, pitch=0.0, yaw=0.0, timestamp=0),
+                         attitudeQuaternion=self._Obj(x=0.0, y=0.0, z=0.0, w=1.0, timestamp=0),
+                         position=self._vec(), velocity=self._vec(), acc=self._vec())
+
+    def controllerMellingerInit(self): pass
+    def crtpCommanderHighLevelInit(self): pass
+    def crtpCommanderHighLevelTellState(self, s): pass
+    def crtpCommanderHighLevelStop(self): pass
+    def crtpCommanderHighLevelUpdateTime(self, t): pass
+
+    def controllerMellinger(self, control, setpoint, sensor, state, tick):
+        self.calls.append(dict(
+            tick=tick,
+            quat=[state.attitudeQuaternion.x, state.attitudeQuaternion.y, state.attitudeQuaternion.z,
+                  state.attitudeQuaternion.w],
+            att=[state.attitude.roll, state.attitude.pitch, state.attitude.yaw],
+            pos=[state.position.x, state.position.y, state.position.z],
+            vel=[state.velocity.x, state.velocity.y, state.velocity.z],
+            acc=[state.acc.x, state.acc.y, state.acc.z],
+            sacc=[sensor.acc.x, sensor.acc.y, sensor.acc.z],
+            sgyro=[sensor.gyro.x, sensor.gyro.y, sensor.gyro.z],
+            sp_pos=[setpoint.position.x, setpoint.position.y, setpoint.position.z],
+            sp_quat=[setpoint.attitudeQuaternion.x, setpoint.attitudeQuaternion.y,
+                     setpoint.attitudeQuaternion.z, setpoint.attitudeQuaternion.w]))
+        control.roll, control.pitch, control.yaw, control.thrust = self.preset
+
+
+def mellinger_fixtures(pb, m):
+    Mel = m.Mellinger
+    firm = _FakeFirm()
+    Mel.load_firmware = lambda *_: firm
+    ctrl = Mel.MellingerControl(0, m.enums.DroneModel.CF2X)
+    rng = np.random.default_rng(5)
+    out = {}
+    # _compute_pwms on int16-valued control outputs
+    n = 512
+    cin = np.stack([rng.integers(-32000, 32001, n), rng.integers(-32000, 32001, n),
+                    rng.integers(-32000, 32001, n), rng.uniform(-5000, 90000, n)], 1).astype(float)
+    cin[:8, :3] = 0
+    pw = np.array([ctrl._compute_pwms(types.SimpleNamespace(roll=int(c[0]), pitch=int(c[1]), yaw=int(c[2]),
+                                                           thrust=c[3])) for c in cin])
+    out.update(mel_control=cin, mel_pwms=pw)
+    # full computeControl chain with a scripted firmware: state/sensor packing + PWM->RPM
+    init_obs = np.zeros((1, 12)); init_obs[0, :3] = [0.9, 0.9, 0.05]
+    ctrl.reset(init_obs)
+    ctrl._sendFullStateCmd([0.5, -0.3, 1.0], np.zeros(3), np.zeros(3), 0.3, np.zeros(3), 0)
+    T = 120
+    ins = np.zeros((T, 12)); noise = rng.normal(0, 0.001, (T, 4)); presets = np.zeros((T, 4)); rpms = np.zeros((T, 4))
+    pos = np.array([0.9, 0.9, 0.05]); rpy = np.zeros(3); vel = np.zeros(3)
+    for t in range(T):
+        pos = pos + rng.uniform(-0.01, 0.01, 3); rpy = rpy + rng.uniform(-0.02, 0.02, 3)
+        vel = vel + rng.uniform(-0.05, 0.05, 3)
+        if t == 60:
+            rpy[2] = math.pi - 0.001   # yaw wrap spike in the finite-difference "gyro"
+        if t == 61:
+            rpy[2] = -math.pi + 0.001
+        presets[t] = [int(rng.integers(-3000, 3000)), int(rng.integers(-3000, 3000)),
+                      int(rng.integers(-3000, 3000)), rng.uniform(20000, 60000)]
+        firm.preset = tuple(presets[t])
+        ins[t] = np.concatenate([pos, rpy, vel, np.zeros(3)])
+        rpms[t] = ctrl.computeControl(t, pos.copy(), rpy.copy(), vel.copy(), np.zeros(3), noise[t])
+    keys = ("tick", "quat", "att", "pos", "vel", "acc", "sacc", "sgyro", "sp_pos", "sp_quat")
+    for k in keys:
+        out[f"melrec_{k}"] = np.array([c[k] for c in firm.calls], float)
+    out.update(mel_in=ins, mel_noise=noise, mel_preset=presets, mel_rpm=rpms)
+    # the float64 tick schedule the wrapper passes to controllerMellinger (33 s x 500 Hz)
+    firm.calls.clear()
+    ctrl.reset(init_obs)
+    for _ in range(16500):
+        ctrl.state.acc.z = 1.0
+        ctrl._step_controller()
+    out["tick_schedule"] = np.array([c["tick"] for c in firm.calls], np.uint8)
+    # get_quaternion_from_euler
+    e = rng.uniform(-math.pi, math.pi, (256, 3))
+    out["q_from_e_in"] = e
+    out["q_from_e_out"] = np.array([m.utils.get_quaternion_from_euler(*x) for x in e])
+    # LPF init arguments (swapped cut-offs)
+    out["lpf_acc"] = np.array([ctrl.acclpf[0].fs, ctrl.acclpf[0].fc], float)
+    out["lpf_gyro"] = np.array([ctrl.gyrolpf[0].fs, ctrl.gyrolpf[0].fc], float)
+    return out
+
+
+def main():
+    os.chdir(REF)   # MultiRaceAviary resolves URDF_DIR relative to the cwd (read only)
+    pb = install_stubs()
+    m = import_reference(pb)
+    fx = {}
+    fx.update(hover_fixtures(pb, m))
+    fx.update(force_fixtures(pb, m))
+    fx.update(dyn_fixtures(pb, m))
+    fx.update(mellinger_fixtures(pb, m))
+    path = os.path.join(HERE, "hover_golden.npz")
+    np.savez_compressed(path, **fx)
+    print("wrote", path, len(fx), "arrays")
+
+
+if __name__ == "__main__":
+    main()
