@@ -1,0 +1,196 @@
+"""Benchmark: HoverAviary env.step throughput (BASELINE.json configs[1]) on N MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one env.step() of every env on every GPU: per GPU one fused launch over
+4096 envs x 8 PYB sub-steps (240 Hz physics, 30 Hz control) incl. obs/reward/
+termination and auto-reset.  Envs are sharded across ranks (weak scaling, no collective
+on the step path).  Inputs are resident in HBM before the timed region: per-env random
+airborne initial states (device RNG) and a pre-generated buffer of U[-1,1] actions.
+
+Prints ONE JSON line on rank 0 with the roofline of the step kernel (per-launch HIP
+events on the launching stream) and a CPU baseline (the float64 oracle, one host core,
+bounded sample) timed in the same run.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ENVS_PER_GPU = 4096         # BASELINE.json configs[1]
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
+    p.add_argument("--physics", default="PYB")
+    p.add_argument("--precision", default="fp32")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--graph", type=int, default=1, help="also time HIP-graph replay of the step loop")
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, seconds):
+    """float64 oracle (oracle/oracle.c), single host thread, bounded sample of the same
+    workload: 4096 envs stepped until ~`seconds` of CPU time."""
+    from oracle import oracle as O
+    c = cfg.copy()
+    c.num_envs = ENVS_PER_GPU
+    c.env_offset = 0
+    orc = O.Oracle(c)
+    orc.reset()
+    rng = np.random.default_rng(1)
+    acts = rng.uniform(-1, 1, (8, c.num_envs, 1, 4)).astype(np.float32)
+    orc.step(acts[0])                     # warm
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.step(acts[steps % 8])
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": c.num_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{c.num_envs} envs x {steps} env.steps (float64 oracle, {dt:.1f} s, 1 thread, "
+                      f"{platform.processor() or platform.machine()})"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    from gym_pybullet_adrp_amd.envs.hover import HoverAviary
+    from gym_pybullet_adrp_amd.utils.enums import Physics
+
+    E = args.envs
+    env = HoverAviary(physics=Physics[args.physics], num_envs=E, device=local, precision=args.precision,
+                      seed=2024, env_offset=rank * E, initial_xyzs=[0, 0, 1.0],
+                      init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1})
+    dev = env.device
+    env.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + rank)
+    nbuf = 64
+    acts = (torch.rand((nbuf, E, 1, 4), generator=gen, device=dev) * 2 - 1).contiguous()
+    for k in range(args.warmup):
+        env.step(acts[k % nbuf])
+    torch.cuda.synchronize()
+
+    # ---- timed region: K env.steps, per-launch HIP events on the launching stream ----
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record()
+        env.step(acts[k % nbuf])
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    kern_ms = np.array([s.elapsed_time(e) for s, e in ev])
+    kern_avg_s = float(kern_ms.mean()) / 1e3
+
+    # ---- HIP-graph replay of the same step loop (launch-bound regime) ----
+    graph = None
+    if args.graph:
+        try:
+            G = 64
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for k in range(3):
+                    env.step(acts[k])
+            torch.cuda.current_stream(dev).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for k in range(G):
+                    env.step(acts[k % nbuf])
+            g.replay()
+            torch.cuda.synchronize()
+            reps = max(1, K // G)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            tg0 = time.perf_counter()
+            for _ in range(reps):
+                g.replay()
+            torch.cuda.synchronize()
+            tg = time.perf_counter() - tg0
+            graph = {"env_steps_per_s_per_gpu": E * G * reps / tg, "ms_per_step": tg / (G * reps) * 1e3,
+                     "steps_per_graph": G}
+        except Exception as exc:  # graph capture is an optimisation, not the measurement
+            graph = {"error": str(exc)[:200]}
+
+    bytes_per_launch = env.step_bytes()
+    achieved = bytes_per_launch / kern_avg_s / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            rec = json.load(fh)
+        key = f"{args.physics}_{args.precision}_{E}"
+        if key in rec:
+            traffic = rec[key]["hbm_bytes_per_launch"]
+    result = {
+        "metric": "env-steps/sec (N parallel drones) at 1/2/4/8 MI355X; % HBM roofline",
+        "value": E * world * K / elapsed,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if args.precision == "fp32" else "f64",
+        "data": "synthetic: device-RNG airborne initial states around (0,0,1), U[-1,1] RPM actions",
+        "config": {"workload": f"HoverAviary Physics.{args.physics} 240/30 Hz (8 sub-steps), {E} envs x 1 drone "
+                               f"per GPU, RPM actions, auto-reset", "envs_per_gpu": E, "global_envs": E * world,
+                   "drones_per_env": 1, "parallelism": f"env-sharded dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "bytes_per_launch": bytes_per_launch, "kernel_us": kern_avg_s * 1e6},
+        "graph_replay": graph,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(env.cfg, args.cpu_seconds)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    env.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+"""ctypes loader of libadrp.so (the C-ABI in include/adrp.h).
+
+torch is imported first on purpose: libadrp.so is linked against libamdhip64.so.7 and
+the dynamic loader then binds it to the HIP runtime torch already loaded, so torch's
+hipStream_t handles and device pointers are valid inside libadrp.
+
+There is no CPU fallback: if the library or a HIP device is missing, loading or
+creating a handle raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (binds the shared HIP runtime before libadrp loads)
+
+from .utils import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libadrp.so")
+
+_lib = None
+
+
+class AdrpError(RuntimeError):
+    pass
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise AdrpError(f"{LIB_PATH} is missing: build it with `make -C gym_pybullet_adrp_amd/csrc` "
+                        "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, I = ctypes.c_void_p, ctypes.c_int
+    lib.adrp_abi_version.restype = I
+    lib.adrp_default_config.argtypes = [I, P]
+    lib.adrp_default_config.restype = I
+    lib.adrp_create.argtypes = [P, I, ctypes.POINTER(P)]
+    lib.adrp_create.restype = I
+    lib.adrp_destroy.argtypes = [P]
+    lib.adrp_destroy.restype = None
+    lib.adrp_last_error.argtypes = [P]
+    lib.adrp_last_error.restype = ctypes.c_char_p
+    lib.adrp_obs_dim.argtypes = [P]
+    lib.adrp_act_dim.argtypes = [P]
+    lib.adrp_reset.argtypes = [P, P, P, P]
+    lib.adrp_reset.restype = I
+    lib.adrp_step.argtypes = [P, P, P, P, P, P, P, P]
+    lib.adrp_step.restype = I
+    lib.adrp_state_layout.argtypes = [P, ctypes.POINTER(I), ctypes.POINTER(I)]
+    lib.adrp_state_field.argtypes = [P, I, I]
+    lib.adrp_state_field.restype = ctypes.c_char_p
+    lib.adrp_get_state.argtypes = [P, P, P, P]
+    lib.adrp_set_state.argtypes = [P, P, P, P]
+    lib.adrp_step_bytes.argtypes = [P]
+    lib.adrp_step_bytes.restype = ctypes.c_int64
+    lib.adrp_debug_contact_count.argtypes = [P, I]
+    lib.adrp_debug_contact_count.restype = I
+    if lib.adrp_abi_version() != abi.ABI_VERSION:
+        raise AdrpError(f"libadrp ABI {lib.adrp_abi_version()} != python mirror {abi.ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def default_config(task):
+    cfg = abi.AdrpConfig()
+    rc = load().adrp_default_config(task, ctypes.byref(cfg))
+    if rc != 0:
+        raise AdrpError(load().adrp_last_error(None).decode())
+    return cfg
+
+
+def _p(t):
+    """device pointer of a tensor (or None)"""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class Handle:
+    """Owns one adrp_t: E envs x N drones resident in the HBM of one GPU."""
+
+    def __init__(self, cfg, device):
+        self.lib = load()
+        if not torch.cuda.is_available():
+            raise AdrpError("no HIP device visible: libadrp has no CPU fallback")
+        self.device = torch.device("cuda", device)
+        h = ctypes.c_void_p()
+        rc = self.lib.adrp_create(ctypes.byref(cfg), device, ctypes.byref(h))
+        if rc != 0:
+            msg = self.lib.adrp_last_error(None).decode()
+            raise (ValueError if rc == abi.ERR_INVALID else AdrpError)(f"adrp_create: {msg}")
+        self.h = h
+        self.cfg = cfg
+        self.E, self.N = cfg.num_envs, cfg.num_drones
+        self.D = self.lib.adrp_obs_dim(h)
+        self.A = self.lib.adrp_act_dim(h)
+        nf, ni = ctypes.c_int(), ctypes.c_int()
+        self.lib.adrp_state_layout(h, ctypes.byref(nf), ctypes.byref(ni))
+        self.nf, self.ni = nf.value, ni.value
+        self.real = torch.float64 if cfg.precision else torch.float32
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.adrp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise AdrpError(f"{what}: {self.lib.adrp_last_error(self.h).decode()}")
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def field_names(self):
+        return ([self.lib.adrp_state_field(self.h, 0, k).decode() for k in range(self.nf)],
+                [self.lib.adrp_state_field(self.h, 1, k).decode() for k in range(self.ni)])
+
+    def reset(self, obs, mask=None):
+        self._check(self.lib.adrp_reset(self.h, _p(mask), _p(obs), self._stream()), "adrp_reset")
+
+    def step(self, act, obs, rew, term, trunc, tobs=None):
+        self._check(self.lib.adrp_step(self.h, _p(act), _p(obs), _p(rew), _p(term), _p(trunc), _p(tobs),
+                                       self._stream()), "adrp_step")
+
+    def get_state(self):
+        f = torch.empty((self.nf, self.E * self.N), dtype=self.real, device=self.device)
+        i = torch.empty((self.ni, self.E * self.N), dtype=torch.int32, device=self.device)
+        self._check(self.lib.adrp_get_state(self.h, _p(f), _p(i), self._stream()), "adrp_get_state")
+        return f, i
+
+    def set_state(self, f, i):
+        f = f.to(device=self.device, dtype=self.real).contiguous()
+        i = i.to(device=self.device, dtype=torch.int32).contiguous()
+        assert f.shape == (self.nf, self.E * self.N) and i.shape == (self.ni, self.E * self.N)
+        self._check(self.lib.adrp_set_state(self.h, _p(f), _p(i), self._stream()), "adrp_set_state")
+
+    def step_bytes(self):
+        return self.lib.adrp_step_bytes(self.h)
+
+    def contact_count(self, reset=True):
+        return self.lib.adrp_debug_contact_count(self.h, 1 if reset else 0)

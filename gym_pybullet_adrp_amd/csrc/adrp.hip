@@ -1,0 +1,387 @@
+// adrp.hip — libadrp.so: the C-ABI of include/adrp.h over the fused HIP kernels.
+//
+// Build (gfx950 only):  see gym_pybullet_adrp_amd/csrc/Makefile
+// No CPU fallback: every entry point that computes needs a HIP device and fails with
+// ADRP_ERR_DEVICE otherwise.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/adrp.h"
+#include "hover_kernel.h"
+
+using namespace adrp;
+
+struct adrp_handle {
+    adrp_config cfg;
+    int device = 0;
+    int E = 0, N = 0, A = 0, D = 0, S = 0, B = 0;
+    int nf_base = 0, ni = 0;
+    size_t real_size = 4;
+    void* f = nullptr;        // Real [nf_base][E*N]
+    float* ring = nullptr;    // [B*A][E]
+    int32_t* ist = nullptr;   // [ni][E*N]
+    int32_t* counters = nullptr;  // device diagnostics (ground-model hits)
+    std::string err;
+};
+
+static thread_local std::string g_err;
+
+static int seterr(adrp_t* h, int code, const std::string& msg) {
+    if (h) h->err = msg;
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(h, x)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess)                                                                   \
+            return seterr(h, ADRP_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));  \
+    } while (0)
+
+extern "C" int adrp_abi_version(void) { return ADRP_ABI_VERSION; }
+
+extern "C" const char* adrp_last_error(const adrp_t* h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+// ---------------------------------------------------------------------------------------------
+// defaults (reference constructors; cf2x_IROS.urdf constants; level0.yaml track)
+// ---------------------------------------------------------------------------------------------
+extern "C" int adrp_default_config(int task, adrp_config* c) {
+    if (!c || (task != ADRP_TASK_HOVER && task != ADRP_TASK_RACE)) return seterr(nullptr, ADRP_ERR_INVALID, "task");
+    memset(c, 0, sizeof *c);
+    c->struct_size = sizeof(adrp_config);
+    c->task = task;
+    c->physics = ADRP_PHYS_PYB;
+    c->num_envs = 1;
+    c->autoreset = 1;
+    c->link_frame_lag = 1;
+    c->gravity = 9.8;                                        // BaseAviary.py:74
+    adrp_drone_params& d = c->drone;                         // assets/cf2x_IROS.urdf
+    d.m = 0.03454; d.l = 0.0397; d.thrust2weight = 2.25;
+    d.ixx = 1.4e-5; d.iyy = 1.4e-5; d.izz = 2.17e-5;
+    d.kf = 3.16e-10; d.km = 7.94e-12;
+    d.collision_h = 0.025; d.collision_r = 0.06; d.collision_z_offset = 0.0;
+    d.max_speed_kmh = 30.0; d.gnd_eff_coeff = 11.36859; d.prop_radius = 2.31348e-2;
+    d.drag_coeff[0] = 9.1785e-7; d.drag_coeff[1] = 9.1785e-7; d.drag_coeff[2] = 10.311e-7;
+    d.dw_coeff[0] = 2267.18; d.dw_coeff[1] = 0.16; d.dw_coeff[2] = -0.11;
+    const double pp[4][2] = {{0.028, 0.028}, {-0.028, 0.028}, {-0.028, -0.028}, {0.028, -0.028}};
+    for (int i = 0; i < 4; ++i) { d.prop_pos[i][0] = pp[i][0]; d.prop_pos[i][1] = pp[i][1]; }
+    if (task == ADRP_TASK_HOVER) {
+        c->act_type = ADRP_ACT_RPM;
+        c->num_drones = 1;
+        c->pyb_freq = 240; c->ctrl_freq = 30;                // HoverAviary.py:18-19
+        c->action_buffer_size = 15;                          // ctrl_freq//2 (BaseRLAviary.py:66)
+        c->init_xyz[0][2] = d.collision_h / 2 - d.collision_z_offset + 0.1;  // BaseAviary.py:195-197
+        c->target_pos[2] = 1.0;
+        c->episode_len_sec = 8.0;
+    } else {
+        c->act_type = ADRP_ACT_FULLSTATE;
+        c->num_drones = 2;
+        c->pyb_freq = 500; c->ctrl_freq = 25;                // constants.py:29-31
+        adrp_track& t = c->track;
+        const double gates[4][7] = {{0.45, -1.0, 0.525, 0, 0, 2.35, 1}, {1.0, -1.55, 1.0, 0, 0, -0.78, 0},
+                                    {0.0, 0.5, 0.525, 0, 0, 0, 1}, {-0.5, -0.5, 1.0, 0, 0, 3.14, 0}};
+        const double obst[4][6] = {{1.0, -0.5, 0.525, 0, 0, 0}, {0.5, -1.5, 0.525, 0, 0, 0},
+                                   {-0.5, 0, 0.525, 0, 0, 0}, {0, 1.0, 0.525, 0, 0, 0}};
+        t.num_gates = 4; t.num_obstacles = 4;
+        memcpy(t.gates, gates, sizeof gates);
+        memcpy(t.obstacles, obst, sizeof obst);
+        t.bounds_hi[0] = 3; t.bounds_hi[1] = 3; t.bounds_hi[2] = 2;
+        t.episode_len_sec = 33;
+        t.random_drone_state = 1;
+        t.pos_offset_range[0][0] = -0.1; t.pos_offset_range[0][1] = 0.1;
+        t.pos_offset_range[1][0] = -0.1; t.pos_offset_range[1][1] = 0.1;
+        t.pos_offset_range[2][0] = 0.0;  t.pos_offset_range[2][1] = 0.02;
+        for (int k = 0; k < 3; ++k) { t.rot_offset_range[k][0] = -0.1; t.rot_offset_range[k][1] = 0.1; }
+        t.init_pos[0][0] = 0.9; t.init_pos[0][1] = 0.9; t.init_pos[0][2] = 0.05;
+        t.init_pos[1][0] = 1.1; t.init_pos[1][1] = 1.1; t.init_pos[1][2] = 0.05;
+        t.init_pos[2][0] = 0.7; t.init_pos[2][1] = 0.9; t.init_pos[2][2] = 0.05;   // N>2 extension
+        t.init_pos[3][0] = 1.3; t.init_pos[3][1] = 1.1; t.init_pos[3][2] = 0.05;
+        t.race_mass = 0.027;                                 // assets/cf2x.urdf:11
+        t.race_inertia[0] = 1.4e-5; t.race_inertia[1] = 1.4e-5; t.race_inertia[2] = 2.17e-5;
+    }
+    return ADRP_OK;
+}
+
+static void derived(const adrp_config& c, double* hover_rpm, double* gnd_clip) {
+    const adrp_drone_params& d = c.drone;
+    const double gravity = c.gravity * d.m;
+    *hover_rpm = sqrt(gravity / (4 * d.kf));
+    const double maxr = sqrt((d.thrust2weight * gravity) / (4 * d.kf));
+    const double maxt = 4 * d.kf * maxr * maxr;
+    *gnd_clip = 0.25 * d.prop_radius * sqrt((15 * maxr * maxr * d.kf * d.gnd_eff_coeff) / maxt);
+}
+
+template <typename Real>
+static HoverArgs<Real> hover_args(const adrp_t* h) {
+    const adrp_config& c = h->cfg;
+    const adrp_drone_params& d = c.drone;
+    HoverArgs<Real> a;
+    memset(&a, 0, sizeof a);
+    a.E = h->E; a.S = h->S; a.A = h->A; a.B = h->B; a.D = h->D;
+    a.physics = c.physics; a.autoreset = c.autoreset; a.link_lag = c.link_frame_lag ? 1 : 0;
+    // truncated when step_counter / PYB_FREQ > EPISODE_LEN_SEC in float64 (HoverAviary.py:114)
+    long long t = (long long)floor(c.episode_len_sec * c.pyb_freq) - 2;
+    if (t < 0) t = 0;
+    while (!((double)t / (double)c.pyb_freq > c.episode_len_sec)) ++t;
+    a.trunc_steps = (int)t;
+    a.dt = Real(1.0 / c.pyb_freq);
+    a.mass = Real(d.m); a.inv_mass = Real(1.0 / d.m); a.gravity = Real(c.gravity);
+    a.ixx = Real(d.ixx); a.iyy = Real(d.iyy); a.izz = Real(d.izz);
+    a.inv_ixx = Real(1.0 / d.ixx); a.inv_iyy = Real(1.0 / d.iyy); a.inv_izz = Real(1.0 / d.izz);
+    a.ang_max = Real(0.5 * (M_PI / 2) * c.pyb_freq);
+    a.kf = Real(d.kf); a.km = Real(d.km);
+    double hover_rpm, gnd_clip;
+    derived(c, &hover_rpm, &gnd_clip);
+    a.hover_rpm = Real(hover_rpm);
+    for (int i = 0; i < 4; ++i) {
+        a.px[i] = Real(d.prop_pos[i][0]); a.py[i] = Real(d.prop_pos[i][1]); a.pz[i] = Real(d.prop_pos[i][2]);
+    }
+    a.gnd_kf = Real(d.kf * d.gnd_eff_coeff);
+    a.prop_r4 = Real(d.prop_radius / 4);
+    a.gnd_clip = Real(gnd_clip);
+    for (int k = 0; k < 3; ++k) a.drag[k] = Real(d.drag_coeff[k]);
+    a.dyn_arm = Real(d.l / sqrt(2.0));
+    a.coll_hh = Real(0.5 * d.collision_h); a.coll_r = Real(d.collision_r); a.coll_zoff = Real(d.collision_z_offset);
+    for (int k = 0; k < 3; ++k) {
+        a.target[k] = Real(c.target_pos[k]);
+        a.init_xyz[k] = Real(c.init_xyz[0][k]); a.init_rpy[k] = Real(c.init_rpy[0][k]);
+        a.n_xyz[k] = Real(c.init_xyz_noise[k]); a.n_rpy[k] = Real(c.init_rpy_noise[k]);
+        a.n_vel[k] = Real(c.init_vel_noise[k]); a.n_om[k] = Real(c.init_omega_noise[k]);
+    }
+    a.seed = c.seed;
+    a.env_offset = c.env_offset;
+    a.f = (Real*)h->f;
+    a.ring = h->ring;
+    a.ist = h->ist;
+    a.contact_count = h->counters;
+    return a;
+}
+
+// ---------------------------------------------------------------------------------------------
+extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
+    if (!out) return seterr(nullptr, ADRP_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (!cfg || cfg->struct_size != sizeof(adrp_config))
+        return seterr(nullptr, ADRP_ERR_INVALID, "adrp_config.struct_size mismatch (ABI)");
+    const adrp_config& c = *cfg;
+    if (c.num_envs <= 0) return seterr(nullptr, ADRP_ERR_INVALID, "num_envs must be > 0");
+    if (c.ctrl_freq <= 0 || c.pyb_freq <= 0 || c.pyb_freq % c.ctrl_freq != 0)
+        return seterr(nullptr, ADRP_ERR_INVALID, "pyb_freq is not divisible by env_freq");  // BaseAviary.py:79-80
+    if (c.physics < ADRP_PHYS_PYB || c.physics > ADRP_PHYS_PYB_GND_DRAG_DW)
+        return seterr(nullptr, ADRP_ERR_INVALID, "unknown physics");
+    if (c.precision != 0 && c.precision != 1) return seterr(nullptr, ADRP_ERR_INVALID, "precision must be 0 or 1");
+    if (c.task == ADRP_TASK_HOVER) {
+        if (c.num_drones != 1) return seterr(nullptr, ADRP_ERR_INVALID, "HoverAviary has exactly one drone");
+        if (c.act_type != ADRP_ACT_RPM && c.act_type != ADRP_ACT_ONE_D_RPM)
+            return seterr(nullptr, ADRP_ERR_INVALID, "HoverAviary act_type must be RPM or ONE_D_RPM");
+        if (c.action_buffer_size <= 0 || c.action_buffer_size > 4096)
+            return seterr(nullptr, ADRP_ERR_INVALID, "action_buffer_size");
+    } else if (c.task == ADRP_TASK_RACE) {
+        return seterr(nullptr, ADRP_ERR_INVALID, "ADRP_TASK_RACE is not built yet in this library version");
+    } else {
+        return seterr(nullptr, ADRP_ERR_INVALID, "unknown task");
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return seterr(nullptr, ADRP_ERR_DEVICE, "no HIP device visible (libadrp has no CPU fallback)");
+    if (device < 0 || device >= ndev) return seterr(nullptr, ADRP_ERR_INVALID, "device index out of range");
+    adrp_t* h = new adrp_t();
+    h->cfg = c;
+    h->device = device;
+    h->E = c.num_envs; h->N = c.num_drones;
+    h->A = c.act_type == ADRP_ACT_ONE_D_RPM ? 1 : 4;
+    h->B = c.action_buffer_size;
+    h->D = 12 + h->B * h->A;
+    h->S = c.pyb_freq / c.ctrl_freq;
+    h->nf_base = HF_NBASE;
+    h->ni = HI_N;
+    h->real_size = c.precision ? 8 : 4;
+    const size_t EN = size_t(h->E) * h->N;
+    auto cleanup = [&](int rc) {
+        hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters);
+        g_err = h->err;
+        delete h;
+        return rc;
+    };
+    if (hipSetDevice(device) != hipSuccess) return cleanup(seterr(h, ADRP_ERR_DEVICE, "hipSetDevice failed"));
+    if (hipMalloc(&h->f, h->nf_base * EN * h->real_size) != hipSuccess ||
+        hipMalloc((void**)&h->ring, size_t(h->B) * h->A * h->E * sizeof(float)) != hipSuccess ||
+        hipMalloc((void**)&h->ist, h->ni * EN * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc((void**)&h->counters, 64 * sizeof(int32_t)) != hipSuccess)
+        return cleanup(seterr(h, ADRP_ERR_OOM, "hipMalloc failed"));
+    if (hipMemset(h->f, 0, h->nf_base * EN * h->real_size) != hipSuccess ||
+        hipMemset(h->ring, 0, size_t(h->B) * h->A * h->E * sizeof(float)) != hipSuccess ||
+        hipMemset(h->ist, 0, h->ni * EN * sizeof(int32_t)) != hipSuccess ||
+        hipMemset(h->counters, 0, 64 * sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return cleanup(seterr(h, ADRP_ERR_DEVICE, "initialisation failed"));
+    *out = h;
+    return ADRP_OK;
+}
+
+extern "C" void adrp_destroy(adrp_t* h) {
+    if (!h) return;
+    hipSetDevice(h->device);
+    hipDeviceSynchronize();
+    hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters);
+    delete h;
+}
+
+extern "C" int adrp_obs_dim(const adrp_t* h) { return h ? h->D : ADRP_ERR_INVALID; }
+extern "C" int adrp_act_dim(const adrp_t* h) { return h ? h->A : ADRP_ERR_INVALID; }
+
+// ---------------------------------------------------------------------------------------------
+// launch dispatch
+// ---------------------------------------------------------------------------------------------
+constexpr int kBlock = 64;   // one wave per workgroup: E=4096 -> 64 CUs busy, no intra-block sync
+
+template <typename Real, int A, int B>
+static void launch_step_ph(const HoverArgs<Real>& a, int physics, dim3 grid, hipStream_t s) {
+    const dim3 blk(kBlock);
+    switch (physics) {
+        case ADRP_PHYS_PYB: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB, A, B>), grid, blk, 0, s, a); break;
+        case ADRP_PHYS_DYN: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_DYN, A, B>), grid, blk, 0, s, a); break;
+        case ADRP_PHYS_PYB_GND: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B>), grid, blk, 0, s, a); break;
+        case ADRP_PHYS_PYB_DRAG: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B>), grid, blk, 0, s, a); break;
+        case ADRP_PHYS_PYB_DW: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B>), grid, blk, 0, s, a); break;
+        default: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B>), grid, blk, 0, s, a); break;
+    }
+}
+
+template <typename Real>
+static int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                      float* tobs, hipStream_t s) {
+    HoverArgs<Real> a = hover_args<Real>(h);
+    a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
+    const dim3 grid((h->E + kBlock - 1) / kBlock);
+    const int ph = h->cfg.physics;
+    if (h->A == 1) {
+        if (h->B == 15) launch_step_ph<Real, 1, 15>(a, ph, grid, s);
+        else launch_step_ph<Real, 1, 0>(a, ph, grid, s);
+    } else {
+        if (h->B == 15) launch_step_ph<Real, 4, 15>(a, ph, grid, s);
+        else launch_step_ph<Real, 4, 0>(a, ph, grid, s);
+    }
+    HIPCHK(h, hipGetLastError());
+    return ADRP_OK;
+}
+
+template <typename Real>
+static int hover_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s) {
+    HoverArgs<Real> a = hover_args<Real>(h);
+    a.mask = mask; a.obs = obs;
+    const dim3 grid((h->E + kBlock - 1) / kBlock);
+    if (h->A == 1) hipLaunchKernelGGL((hover_reset_kernel<Real, 1>), grid, dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((hover_reset_kernel<Real, 4>), grid, dim3(kBlock), 0, s, a);
+    HIPCHK(h, hipGetLastError());
+    return ADRP_OK;
+}
+
+extern "C" int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev, void* stream) {
+    if (!h || !obs_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_reset: NULL argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    return h->real_size == 8 ? hover_reset<double>(h, env_mask_dev, obs_dev, s)
+                             : hover_reset<float>(h, env_mask_dev, obs_dev, s);
+}
+
+extern "C" int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* term_dev,
+                         uint8_t* trunc_dev, float* terminal_obs_dev, void* stream) {
+    if (!h || !act_dev || !obs_dev || !rew_dev || !term_dev || !trunc_dev)
+        return seterr(h, ADRP_ERR_INVALID, "adrp_step: NULL argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    return h->real_size == 8 ? hover_step<double>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s)
+                             : hover_step<float>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// state snapshot
+// ---------------------------------------------------------------------------------------------
+static const char* k_hover_f[HF_NBASE] = {
+    "pos_x", "pos_y", "pos_z", "quat_x", "quat_y", "quat_z", "quat_w", "vel_x", "vel_y", "vel_z",
+    "omega_x", "omega_y", "omega_z", "last_rpm_0", "last_rpm_1", "last_rpm_2", "last_rpm_3",
+    "angv_x", "angv_y", "angv_z", "link_quat_x", "link_quat_y", "link_quat_z", "link_quat_w"};
+static const char* k_hover_i[HI_N] = {"step_counter", "episode", "ring_head"};
+
+extern "C" int adrp_state_layout(const adrp_t* h, int* nf, int* ni) {
+    if (!h || !nf || !ni) return ADRP_ERR_INVALID;
+    *nf = h->nf_base + h->B * h->A;
+    *ni = h->ni;
+    return ADRP_OK;
+}
+
+extern "C" const char* adrp_state_field(const adrp_t* h, int is_int, int index) {
+    static thread_local char buf[32];
+    if (!h || index < 0) return nullptr;
+    if (is_int) return index < h->ni ? k_hover_i[index] : nullptr;
+    if (index < h->nf_base) return k_hover_f[index];
+    const int k = index - h->nf_base;
+    if (k >= h->B * h->A) return nullptr;
+    snprintf(buf, sizeof buf, "ring_%d_%d", k / h->A, k % h->A);
+    return buf;
+}
+
+extern "C" int adrp_get_state(adrp_t* h, void* f_dev, int32_t* i_dev, void* stream) {
+    if (!h || !f_dev || !i_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_get_state: NULL argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    const size_t EN = size_t(h->E) * h->N, nb = h->nf_base * EN, nr = size_t(h->B) * h->A * h->E;
+    HIPCHK(h, hipMemcpyAsync(f_dev, h->f, nb * h->real_size, hipMemcpyDeviceToDevice, s));
+    void* ring_dst = (char*)f_dev + nb * h->real_size;
+    hipLaunchKernelGGL(ring_get_kernel, dim3((h->E + 255) / 256), dim3(256), 0, s, h->ring, ring_dst,
+                       int(h->real_size == 8), h->B, h->A, h->E);
+    HIPCHK(h, hipGetLastError());
+    (void)nr;
+    HIPCHK(h, hipMemcpyAsync(i_dev, h->ist, h->ni * EN * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return ADRP_OK;
+}
+
+extern "C" int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev, void* stream) {
+    if (!h || !f_dev || !i_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_set_state: NULL argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    const size_t EN = size_t(h->E) * h->N, nb = h->nf_base * EN, nr = size_t(h->B) * h->A * h->E;
+    HIPCHK(h, hipMemcpyAsync(h->f, f_dev, nb * h->real_size, hipMemcpyDeviceToDevice, s));
+    const void* ring_src = (const char*)f_dev + nb * h->real_size;
+    hipLaunchKernelGGL(ring_set_kernel, dim3((h->E + 255) / 256), dim3(256), 0, s, h->ring, ring_src,
+                       int(h->real_size == 8), h->B, h->A, h->E);
+    HIPCHK(h, hipGetLastError());
+    (void)nr;
+    HIPCHK(h, hipMemcpyAsync(h->ist, i_dev, h->ni * EN * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return ADRP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// roofline accounting: algorithmic HBM bytes of one adrp_step
+// ---------------------------------------------------------------------------------------------
+extern "C" int64_t adrp_step_bytes(const adrp_t* h) {
+    if (!h) return ADRP_ERR_INVALID;
+    const int ph = h->cfg.physics;
+    const bool dyn = ph == ADRP_PHYS_DYN;
+    const bool drag = ph == ADRP_PHYS_PYB_DRAG || ph == ADRP_PHYS_PYB_GND_DRAG_DW;
+    const bool lag = h->cfg.link_frame_lag && !dyn;
+    const int64_t fields = 13 + (lag ? 4 : 0) + (drag ? 4 : 0) + (dyn ? 3 : 0);
+    const int64_t per_env = 2 * fields * int64_t(h->real_size)   // state read + write
+                            + 2 * HI_N * 4                        // int state read + write
+                            + int64_t(h->A) * 4                   // action
+                            + int64_t(h->A) * 4                   // ring append
+                            + int64_t(h->B - 1) * h->A * 4        // ring read
+                            + int64_t(h->D) * 4                   // obs write
+                            + 4 + 2;                              // reward, terminated, truncated
+    return per_env * h->E;
+}
+
+// diagnostics for tests: number of envs whose last step touched the plane contact model
+extern "C" int adrp_debug_contact_count(adrp_t* h, int reset) {
+    if (!h) return ADRP_ERR_INVALID;
+    int32_t v = 0;
+    if (hipMemcpy(&v, h->counters, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return ADRP_ERR_DEVICE;
+    if (reset && hipMemset(h->counters, 0, sizeof(int32_t)) != hipSuccess) return ADRP_ERR_DEVICE;
+    return v;
+}

@@ -1,0 +1,508 @@
+// hover_kernel.h — fused HoverAviary env.step for gfx950: one lane per env, all
+// PYB_FREQ/CTRL_FREQ sub-steps in registers, then obs / reward / terminated /
+// truncated and (optionally) the VecEnv auto-reset, in ONE launch.
+//
+// Reference path (FelixWaiblinger/gym-pybullet-adrp @ 2024-10-08):
+//   BaseAviary.step            envs/BaseAviary.py:262-387 (sub-step loop 347-376)
+//   _preprocessAction          envs/BaseRLAviary.py:160-239 (RPM 192, ONE_D_RPM 225)
+//   _physics / _groundEffect / _drag / _downwash   envs/BaseAviary.py:683-818
+//   p.stepSimulation (Bullet btMultiBody floating base)        BaseAviary.py:373-374
+//   _dynamics / _integrateQ (Physics.DYN)          envs/BaseAviary.py:822-896
+//   _computeObs                envs/BaseRLAviary.py:284-319
+//   _computeReward / _computeTerminated / _computeTruncated    envs/HoverAviary.py:68-117
+//
+// Closed form used per Bullet sub-step (derivation in DESIGN.md §Kernel):
+//   thrust axis  zs = Rs·ẑ  (Rs = link basis cached at the last forwardKinematics)
+//   F_world      = Σf·zs + [Σg·R·ẑ] + B·f_link4 + m·g
+//   n_body       = P × (Rᵀzs) + τz·(Rᵀzs) + [G × ẑ]          P = Σ f_i p_i, G = Σ g_i p_i
+//   ω̇_b          = I⁻¹(n_b − k(1+|ω_b|) I∘ω_b − ω_b × I ω_b),   a_w = F_w/m − k(1+|v|) v
+//   v, ω += dt(·) (clamped ±100);  x += dt v;  q ← normalize((ω̂ sin, cos) ⊗ q)
+//
+// Latency design (E = 4096 is 64 waves on 256 CUs: the kernel is one wave's critical
+// path): no divides or IEEE sqrt in the sub-step chain (reciprocal constants, 1-ulp
+// hardware rcp/sqrt/rsq), small-angle sin/cos polynomial, the lagged link basis is the
+// previous sub-step's rotation matrix (carried, not recomputed), the action-ring loads
+// are issued at entry independent of the ring head, rows are written with 16-byte
+// per-lane stores straight from registers (no LDS, no barrier).
+#pragma once
+
+#include "adrp_device.h"
+
+namespace adrp {
+
+// float-field indices of the HoverAviary state snapshot ([field][E], SoA)
+enum HoverField {
+    HF_POS = 0, HF_QUAT = 3, HF_VEL = 7, HF_OMEGA = 10, HF_LAST_RPM = 13, HF_ANGV = 17,
+    HF_LINK_QUAT = 20, HF_NBASE = 24
+};
+enum HoverInt { HI_STEP = 0, HI_EPISODE = 1, HI_RING_HEAD = 2, HI_N = 3 };
+
+template <typename Real>
+struct HoverArgs {
+    int E, S, A, B, D;
+    int physics, autoreset, link_lag, trunc_steps;   // truncated once step_counter >= trunc_steps
+    Real dt, mass, inv_mass, gravity;
+    Real ixx, iyy, izz, inv_ixx, inv_iyy, inv_izz;
+    Real kf, km, hover_rpm;
+    Real px[4], py[4], pz[4];                // prop link COM offsets (body)
+    Real gnd_kf, prop_r4, gnd_clip;          // kf*GND_EFF_COEFF, PROP_RADIUS/4, GND_EFF_H_CLIP
+    Real drag[3];
+    Real dyn_arm;                            // L/sqrt(2) (Physics.DYN)
+    Real coll_hh, coll_r, coll_zoff;         // collision cylinder half-height, radius, z offset
+    Real ang_max;                            // ANGULAR_MOTION_THRESHOLD / dt
+    Real target[3];
+    Real init_xyz[3], init_rpy[3], n_xyz[3], n_rpy[3], n_vel[3], n_om[3];
+    uint64_t seed;
+    int64_t env_offset;
+    Real* f;           // [HF_NBASE][E]
+    float* ring;       // [B][E][A]  (slot-major, the A floats of one env contiguous)
+    int32_t* ist;      // [HI_N][E]
+    const float* act;  // [E][A]
+    float* obs;        // [E][D]
+    float* rew;
+    uint8_t* term;
+    uint8_t* trunc;
+    float* tobs;       // [E][D] or null
+    const uint8_t* mask;  // reset mask or null
+    int32_t* contact_count;  // device counter of ground-model hits (diagnostics)
+};
+
+template <typename Real>
+struct Body {
+    V3<Real> pos, vel, w;     // w: world ω (PYB) or body rpy_rates (DYN)
+    Q4<Real> q, ql;           // pose quaternion, cached link basis
+    V3<Real> angv;            // DYN: world ω reported by getBaseVelocity
+    Real prev_rpm[4];
+};
+
+template <typename Real>
+__device__ __forceinline__ Real clamp100(Real x) {
+    return x < Real(-100) ? Real(-100) : (x > Real(100) ? Real(100) : x);
+}
+
+// One Bullet stepSimulation of one drone after the reference's force calls.
+// R = rot(b.q) on entry; Rs = rotation of the cached link basis.  On exit R/Rs are the
+// matrices the next sub-step needs.  Returns true if the plane contact model acted.
+template <typename Real, int PH>
+__device__ __forceinline__ bool pyb_substep(const HoverArgs<Real>& a, Body<Real>& b, M3<Real>& R, M3<Real>& Rs,
+                                            const Real rpm[4], Real sum_f, V3<Real> P, Real tau_z) {
+    constexpr bool GND = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
+    constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
+    // _physics: 4 prop forces + z torque on link 4, LINK_FRAME, cached basis
+    const V3<Real> zs = col2(Rs);
+    V3<Real> Fw = v3(sum_f * zs.x, sum_f * zs.y, sum_f * zs.z - a.mass * a.gravity);
+    const V3<Real> m3 = mulT(R, zs);
+    V3<Real> nb = cross(P, m3) + tau_z * m3;
+    bool cur_basis = false;
+    if constexpr (GND) {
+        // getLinkStates(computeForwardKinematics=1) refreshes the cached basis first
+        cur_basis = true;
+        const Real sqx = b.q.x * b.q.x, sqy = b.q.y * b.q.y, sqz = b.q.z * b.q.z, squ = b.q.w * b.q.w;
+        const Real sarg = Real(-2) * (b.q.x * b.q.z - b.q.w * b.q.y);
+        const Real den = squ - sqx - sqy + sqz, num = Real(2) * (b.q.y * b.q.z + b.q.w * b.q.x);
+        // |roll| < pi/2 and |pitch| < pi/2 of getEulerFromQuaternion (BaseAviary.py:749)
+        const bool gate = fabs_(sarg) < Real(0.99999) && (den > Real(0) || (den == Real(0) && num == Real(0)));
+        if (gate) {
+            Real sg = 0;
+            V3<Real> G = v3(Real(0), Real(0), Real(0));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                Real h = b.pos.z + R.a20 * a.px[i] + R.a21 * a.py[i] + R.a22 * a.pz[i];
+                h = h < a.gnd_clip ? a.gnd_clip : h;
+                const Real k = a.prop_r4 * rcp_(h);
+                const Real g = a.gnd_kf * rpm[i] * rpm[i] * k * k;
+                sg += g;
+                G = G + v3(g * a.px[i], g * a.py[i], g * a.pz[i]);
+            }
+            Fw = Fw + sg * col2(R);
+            nb = nb + v3(G.y, -G.x, Real(0));
+        }
+    }
+    if constexpr (DRAG) {
+        Real s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s += b.prev_rpm[i];
+        s = s * Real(0.10471975511965977);  // sum(2*pi*rpm/60)
+        const V3<Real> dw = v3(-a.drag[0] * s * b.vel.x, -a.drag[1] * s * b.vel.y, -a.drag[2] * s * b.vel.z);
+        const V3<Real> dl = mulT(R, dw);    // np.dot(base_rot.T, drag_factors * vel)
+        Fw = Fw + (cur_basis ? dw : mul(Rs, dl));
+    }
+    // ---- Bullet: forwardKinematics, ABA of the floating base, semi-implicit Euler ----
+    const V3<Real> wb = mulT(R, b.w);
+    const V3<Real> Iw = v3(a.ixx * wb.x, a.iyy * wb.y, a.izz * wb.z);
+    const Real kw = Real(0.04) + Real(0.04) * hsqrt_(dot(wb, wb));
+    const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
+    const V3<Real> wdot = mul(R, v3(rhs.x * a.inv_ixx, rhs.y * a.inv_iyy, rhs.z * a.inv_izz));
+    const Real kv = Real(0.04) + Real(0.04) * hsqrt_(dot(b.vel, b.vel));
+    const V3<Real> acc = a.inv_mass * Fw - kv * b.vel;
+    b.w = v3(clamp100(b.w.x + a.dt * wdot.x), clamp100(b.w.y + a.dt * wdot.y), clamp100(b.w.z + a.dt * wdot.z));
+    b.vel = v3(clamp100(b.vel.x + a.dt * acc.x), clamp100(b.vel.y + a.dt * acc.y), clamp100(b.vel.z + a.dt * acc.z));
+    b.pos = b.pos + a.dt * b.vel;
+    // exp-map quaternion update (btMultiBody::stepPositionsMultiDof)
+    Real ang = hsqrt_(dot(b.w, b.w));
+    if (ang > a.ang_max) ang = a.ang_max;          // |w| dt > ANGULAR_MOTION_THRESHOLD
+    Real sh, ch;
+    small_sincos(Real(0.5) * ang * a.dt, &sh, &ch);
+    const Real sc = ang < Real(0.001) ? Real(0.5) * a.dt - (a.dt * a.dt * a.dt) * Real(0.020833333333) * ang * ang
+                                      : sh * rcp_(ang);
+    const V3<Real> ax = sc * b.w;
+    const Q4<Real> q0 = b.q;
+    const Q4<Real> q1 = {ch * q0.x + ax.x * q0.w + ax.y * q0.z - ax.z * q0.y,
+                         ch * q0.y + ax.y * q0.w + ax.z * q0.x - ax.x * q0.z,
+                         ch * q0.z + ax.z * q0.w + ax.x * q0.y - ax.y * q0.x,
+                         ch * q0.w - ax.x * q0.x - ax.y * q0.y - ax.z * q0.z};
+    const Real inv = hrsqrt_(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
+    // the basis cached by this step's forwardKinematics is the pre-integration pose
+    if (a.link_lag) {
+        b.ql = b.q;
+        Rs = R;
+    }
+    b.q = {q1.x * inv, q1.y * inv, q1.z * inv, q1.w * inv};
+    R = rot(b.q);
+    if (!a.link_lag) Rs = R;
+    // plane contact model: non-penetration, no inward velocity
+    const Real r22 = R.a22;
+    Real s2 = Real(1) - r22 * r22;
+    s2 = s2 < Real(0) ? Real(0) : s2;
+    const Real low = b.pos.z + a.coll_zoff - a.coll_hh * fabs_(r22) - a.coll_r * hsqrt_(s2);
+    if (low < Real(0)) {
+        b.pos.z -= low;
+        if (b.vel.z < Real(0)) b.vel.z = Real(0);
+        return true;
+    }
+    return false;
+}
+
+// Physics.DYN (BaseAviary.py:822-896): explicit model, forward Euler, _integrateQ
+template <typename Real>
+__device__ __forceinline__ void dyn_substep(const HoverArgs<Real>& a, Body<Real>& b, const Real rpm[4]) {
+    const M3<Real> R = rot(b.q);
+    Real f[4], zt[4], sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[i] = rpm[i] * rpm[i] * a.kf;
+        zt[i] = rpm[i] * rpm[i] * a.km;
+        sum += f[i];
+    }
+    const V3<Real> zb = col2(R);
+    const V3<Real> force_w = v3(sum * zb.x, sum * zb.y, sum * zb.z - a.gravity * a.mass);
+    const Real tz = -zt[0] + zt[1] - zt[2] + zt[3];
+    const Real tx = (f[0] + f[1] - f[2] - f[3]) * a.dyn_arm;
+    const Real ty = (-f[0] + f[1] + f[2] - f[3]) * a.dyn_arm;
+    const V3<Real> rr = b.w;
+    const V3<Real> tq = v3(tx, ty, tz) - cross(rr, v3(a.ixx * rr.x, a.iyy * rr.y, a.izz * rr.z));
+    const V3<Real> rdd = v3(tq.x * a.inv_ixx, tq.y * a.inv_iyy, tq.z * a.inv_izz);
+    b.vel = b.vel + a.dt * (a.inv_mass * force_w);
+    b.w = rr + a.dt * rdd;
+    b.pos = b.pos + a.dt * b.vel;
+    const V3<Real> w = b.w;
+    const Real wn = hsqrt_(dot(w, w));
+    if (!(wn <= Real(1e-8))) {  // np.isclose(omega_norm, 0)
+        const Real th = wn * a.dt * Real(0.5);
+        Real s, c;
+        if (th <= Real(0.39269908169872414)) small_sincos(th, &s, &c);
+        else sincos_(th, &s, &c);
+        const Real k = s * rcp_(wn);
+        const Q4<Real> q = b.q;
+        b.q = {c * q.x + k * (w.z * q.y - w.y * q.z + w.x * q.w),
+               c * q.y + k * (-w.z * q.x + w.x * q.z + w.y * q.w),
+               c * q.z + k * (w.y * q.x - w.x * q.y + w.z * q.w),
+               c * q.w + k * (-w.x * q.x - w.y * q.y - w.z * q.z)};
+    }
+    b.angv = mul(R, b.w);   // resetBaseVelocity(vel, rotation @ rpy_rates)
+}
+
+template <typename Real>
+__device__ __forceinline__ Real u01r(uint32_t x) {
+    return Real(x >> 8) * Real(1.0 / 16777216.0);
+}
+
+// BaseAviary.reset -> _housekeeping (+ the optional init_noise extension), Real precision
+template <typename Real>
+__device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& a, int e, Body<Real>& b,
+                                                  int32_t& sc, int32_t& ep) {
+    const uint64_t gid = uint64_t(a.env_offset + e);
+    const U4 r0 = draw(a.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 0);
+    const U4 r1 = draw(a.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 1);
+    const U4 r2 = draw(a.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 2);
+    const uint32_t w0[4] = {r0.a, r0.b, r0.c, r0.d}, w1[4] = {r1.a, r1.b, r1.c, r1.d},
+                   w2[4] = {r2.a, r2.b, r2.c, r2.d};
+    Real p[3], e_[3], v[3], om[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        p[k] = a.init_xyz[k] + a.n_xyz[k] * (Real(2) * u01r<Real>(w0[k]) - Real(1));
+        e_[k] = a.init_rpy[k] + a.n_rpy[k] * (Real(2) * u01r<Real>(w1[k]) - Real(1));
+        v[k] = a.n_vel[k] * (Real(2) * u01r<Real>(w2[k]) - Real(1));
+    }
+    om[0] = a.n_om[0] * (Real(2) * u01r<Real>(w0[3]) - Real(1));
+    om[1] = a.n_om[1] * (Real(2) * u01r<Real>(w1[3]) - Real(1));
+    om[2] = a.n_om[2] * (Real(2) * u01r<Real>(w2[3]) - Real(1));
+    b.q = quat_from_euler<Real>(e_[0], e_[1], e_[2]);
+    b.pos = v3(p[0], p[1], p[2]);
+    b.ql = b.q;
+    b.vel = v3(v[0], v[1], v[2]);
+    if (a.physics == ADRP_PHYS_DYN) {
+        b.w = mulT(rot(b.q), v3(om[0], om[1], om[2]));
+        b.angv = v3(om[0], om[1], om[2]);
+    } else {
+        b.w = v3(om[0], om[1], om[2]);
+        b.angv = v3(Real(0), Real(0), Real(0));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b.prev_rpm[i] = Real(0);
+    sc = 0;
+    ep += 1;
+}
+
+template <typename Real>
+__device__ __forceinline__ V3<Real> hover_obs12(const HoverArgs<Real>& a, const Body<Real>& b, float o[12]) {
+    const V3<Real> rpy = euler_xyz(b.q);
+    const V3<Real> w = a.physics == ADRP_PHYS_DYN ? b.angv : b.w;
+    o[0] = float(b.pos.x); o[1] = float(b.pos.y); o[2] = float(b.pos.z);
+    o[3] = float(rpy.x);   o[4] = float(rpy.y);   o[5] = float(rpy.z);
+    o[6] = float(b.vel.x); o[7] = float(b.vel.y); o[8] = float(b.vel.z);
+    o[9] = float(w.x);     o[10] = float(w.y);    o[11] = float(w.z);
+    return rpy;
+}
+
+// one obs row [12 kinematic | B x A action ring, oldest first] from registers
+template <int A, int B>
+__device__ __forceinline__ void write_row(float* row, const float o12[12], const float (&ring)[B][A], int head1) {
+    if constexpr (A == 4) {
+        float4* r4 = reinterpret_cast<float4*>(row);
+        r4[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
+        r4[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
+        r4[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
+#pragma unroll
+        for (int p = 0; p < B; ++p) {          // physical slot p -> logical position k
+            int k = p - head1;
+            k += k < 0 ? B : 0;
+            r4[3 + k] = make_float4(ring[p][0], ring[p][1], ring[p][2], ring[p][3]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) row[k] = o12[k];
+#pragma unroll
+        for (int p = 0; p < B; ++p) {
+            int k = p - head1;
+            k += k < 0 ? B : 0;
+#pragma unroll
+            for (int j = 0; j < A; ++j) row[12 + k * A + j] = ring[p][j];
+        }
+    }
+}
+
+// generic-B variant: the ring part is copied from HBM in logical order (slot head1 = oldest);
+// the newest entry (logical B-1) is this step's action
+template <int A>
+__device__ __forceinline__ void write_row_generic(float* row, const float o12[12], const float* ring, int B, int E,
+                                                  int e, int head1, const float act[A], bool act_is_newest) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) row[k] = o12[k];
+    int slot = head1;
+    for (int k = 0; k < B; ++k) {
+#pragma unroll
+        for (int j = 0; j < A; ++j)
+            row[12 + k * A + j] = (act_is_newest && k == B - 1) ? act[j] : ring[(size_t(slot) * E + e) * A + j];
+        slot = slot + 1 == B ? 0 : slot + 1;
+    }
+}
+
+template <typename Real>
+__device__ __forceinline__ void load_body(const HoverArgs<Real>& a, int e, Body<Real>& b, bool lag, bool drag,
+                                          bool dyn) {
+    const int E = a.E;
+    const Real* f = a.f;
+    b.pos = v3(f[(HF_POS + 0) * E + e], f[(HF_POS + 1) * E + e], f[(HF_POS + 2) * E + e]);
+    b.q = {f[(HF_QUAT + 0) * E + e], f[(HF_QUAT + 1) * E + e], f[(HF_QUAT + 2) * E + e], f[(HF_QUAT + 3) * E + e]};
+    b.vel = v3(f[(HF_VEL + 0) * E + e], f[(HF_VEL + 1) * E + e], f[(HF_VEL + 2) * E + e]);
+    b.w = v3(f[(HF_OMEGA + 0) * E + e], f[(HF_OMEGA + 1) * E + e], f[(HF_OMEGA + 2) * E + e]);
+    if (lag) b.ql = {f[(HF_LINK_QUAT + 0) * E + e], f[(HF_LINK_QUAT + 1) * E + e], f[(HF_LINK_QUAT + 2) * E + e],
+                     f[(HF_LINK_QUAT + 3) * E + e]};
+    else b.ql = b.q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b.prev_rpm[i] = drag ? f[(HF_LAST_RPM + i) * E + e] : Real(0);
+    if (dyn) b.angv = v3(f[(HF_ANGV + 0) * E + e], f[(HF_ANGV + 1) * E + e], f[(HF_ANGV + 2) * E + e]);
+    else b.angv = v3(Real(0), Real(0), Real(0));
+}
+
+template <typename Real>
+__device__ __forceinline__ void store_body(const HoverArgs<Real>& a, int e, const Body<Real>& b, bool lag,
+                                           bool drag, bool dyn) {
+    const int E = a.E;
+    Real* f = a.f;
+    f[(HF_POS + 0) * E + e] = b.pos.x; f[(HF_POS + 1) * E + e] = b.pos.y; f[(HF_POS + 2) * E + e] = b.pos.z;
+    f[(HF_QUAT + 0) * E + e] = b.q.x; f[(HF_QUAT + 1) * E + e] = b.q.y;
+    f[(HF_QUAT + 2) * E + e] = b.q.z; f[(HF_QUAT + 3) * E + e] = b.q.w;
+    f[(HF_VEL + 0) * E + e] = b.vel.x; f[(HF_VEL + 1) * E + e] = b.vel.y; f[(HF_VEL + 2) * E + e] = b.vel.z;
+    f[(HF_OMEGA + 0) * E + e] = b.w.x; f[(HF_OMEGA + 1) * E + e] = b.w.y; f[(HF_OMEGA + 2) * E + e] = b.w.z;
+    if (lag) {
+        f[(HF_LINK_QUAT + 0) * E + e] = b.ql.x; f[(HF_LINK_QUAT + 1) * E + e] = b.ql.y;
+        f[(HF_LINK_QUAT + 2) * E + e] = b.ql.z; f[(HF_LINK_QUAT + 3) * E + e] = b.ql.w;
+    }
+    if (drag) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[(HF_LAST_RPM + i) * E + e] = b.prev_rpm[i];
+    }
+    if (dyn) {
+        f[(HF_ANGV + 0) * E + e] = b.angv.x; f[(HF_ANGV + 1) * E + e] = b.angv.y; f[(HF_ANGV + 2) * E + e] = b.angv.z;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// env.step kernel: lane = env; B (ring length) is a template parameter so the ring lives
+// in registers
+// ------------------------------------------------------------------------------------------
+template <typename Real, int PH, int A, int B>   // B == 0: runtime ring length a.B
+__global__ void __launch_bounds__(256) hover_step_kernel(HoverArgs<Real> a) {
+    constexpr int BR = B > 0 ? B : 1;
+    constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
+    constexpr bool DYN = (PH == ADRP_PHYS_DYN);
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int E = a.E, D = a.D;
+    if (e >= E) return;
+    // ---- issue every load up front: action, the whole ring, ints, state ----
+    float act[A];
+    if constexpr (A == 4) {
+        const float4 v = reinterpret_cast<const float4*>(a.act)[e];
+        act[0] = v.x; act[1] = v.y; act[2] = v.z; act[3] = v.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < A; ++j) act[j] = a.act[e * A + j];
+    }
+    float ring[BR][A];
+#pragma unroll
+    for (int p = 0; p < B; ++p) {   // (no-op for B == 0)
+        if constexpr (A == 4) {
+            const float4 v = reinterpret_cast<const float4*>(a.ring)[size_t(p) * E + e];
+            ring[p][0] = v.x; ring[p][1] = v.y; ring[p][2] = v.z; ring[p][3] = v.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < A; ++j) ring[p][j] = a.ring[(size_t(p) * E + e) * A + j];
+        }
+    }
+    int32_t sc = a.ist[HI_STEP * E + e], ep = a.ist[HI_EPISODE * E + e];
+    const int32_t head = a.ist[HI_RING_HEAD * E + e];
+    const bool lag = a.link_lag && !DYN;
+    Body<Real> b;
+    load_body(a, e, b, lag, DRAG, DYN);
+    // ---- _preprocessAction: RPM = HOVER_RPM * (1 + 0.05 a), the gain in float32 (NEP 50) ----
+    Real rpm[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float g = __fadd_rn(1.0f, __fmul_rn(0.05f, act[A == 1 ? 0 : i]));
+        rpm[i] = a.hover_rpm * Real(g);
+    }
+    // ---- sub-step loop (BaseAviary.py:347-376) ----
+    bool touched = false;
+    if constexpr (DYN) {
+        for (int s = 0; s < a.S; ++s) dyn_substep(a, b, rpm);
+    } else {
+        Real sum_f = 0, t2 = 0;
+        V3<Real> P = v3(Real(0), Real(0), Real(0));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const Real r2 = rpm[i] * rpm[i];
+            const Real f = r2 * a.kf;
+            sum_f += f;
+            P = P + v3(f * a.px[i], f * a.py[i], f * a.pz[i]);
+            t2 += (i & 1) ? -r2 : r2;
+        }
+        const Real tau_z = t2 * a.km;    // KM*(rpm0^2 - rpm1^2 + rpm2^2 - rpm3^2), IROS sign
+        M3<Real> R = rot(b.q);
+        M3<Real> Rs = lag ? rot(b.ql) : R;
+        for (int s = 0; s < a.S; ++s) {
+            touched |= pyb_substep<Real, PH>(a, b, R, Rs, rpm, sum_f, P, tau_z);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b.prev_rpm[i] = rpm[i];  // last_clipped_action
+        }
+    }
+    if (touched && a.contact_count) atomicAdd(a.contact_count, 1);
+    // ---- action ring: append this action at `head` (deque.append, BaseRLAviary.py:187) ----
+#pragma unroll
+    for (int p = 0; p < B; ++p)
+        if (p == head) {
+#pragma unroll
+            for (int j = 0; j < A; ++j) ring[p][j] = act[j];
+        }
+    if constexpr (A == 4)
+        reinterpret_cast<float4*>(a.ring)[size_t(head) * E + e] = make_float4(act[0], act[1], act[2], act[3]);
+    else
+#pragma unroll
+        for (int j = 0; j < A; ++j) a.ring[(size_t(head) * E + e) * A + j] = act[j];
+    const int head1 = head + 1 == B ? 0 : head + 1;
+    // ---- obs / reward / terminated / truncated (HoverAviary.py:68-117) ----
+    float o12[12];
+    const V3<Real> rpy = hover_obs12(a, b, o12);
+    const Real dx = a.target[0] - b.pos.x, dy = a.target[1] - b.pos.y, dz = a.target[2] - b.pos.z;
+    const Real d2 = dx * dx + dy * dy + dz * dz;
+    const Real r = Real(2) - d2 * d2;
+    a.rew[e] = float(r > Real(0) ? r : Real(0));
+    const bool te = d2 < Real(1e-8);   // |target - pos| < 1e-4
+    const bool tr = fabs_(b.pos.x) > Real(1.5) || fabs_(b.pos.y) > Real(1.5) || b.pos.z > Real(2.0) ||
+                    fabs_(rpy.x) > Real(0.4) || fabs_(rpy.y) > Real(0.4) || sc >= a.trunc_steps;
+    a.term[e] = te;
+    a.trunc[e] = tr;
+    sc += a.S;
+    if (a.autoreset && (te || tr)) {
+        if (a.tobs) {
+            if constexpr (B > 0) write_row<A, B>(a.tobs + size_t(e) * D, o12, ring, head1);
+            else write_row_generic<A>(a.tobs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
+        }
+        hover_reset_state(a, e, b, sc, ep);
+        hover_obs12(a, b, o12);
+    }
+    if constexpr (B > 0) write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
+    else write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
+    store_body(a, e, b, lag, DRAG, DYN);
+    a.ist[HI_STEP * E + e] = sc;
+    a.ist[HI_EPISODE * E + e] = ep;
+    a.ist[HI_RING_HEAD * E + e] = head1;
+}
+
+// reset kernel (BaseAviary.reset -> _housekeeping -> _computeObs); ring is NOT cleared (Q21)
+template <typename Real, int A>
+__global__ void __launch_bounds__(256) hover_reset_kernel(HoverArgs<Real> a) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.E || (a.mask && !a.mask[e])) return;
+    const int E = a.E;
+    const bool dyn = a.physics == ADRP_PHYS_DYN;
+    const bool drag = a.physics == ADRP_PHYS_PYB_DRAG || a.physics == ADRP_PHYS_PYB_GND_DRAG_DW;
+    Body<Real> b;
+    int32_t sc = a.ist[HI_STEP * E + e], ep = a.ist[HI_EPISODE * E + e];
+    const int head = a.ist[HI_RING_HEAD * E + e];
+    hover_reset_state(a, e, b, sc, ep);
+    store_body(a, e, b, a.link_lag && !dyn, drag, dyn);
+    a.ist[HI_STEP * E + e] = sc;
+    a.ist[HI_EPISODE * E + e] = ep;
+    float o12[12];
+    hover_obs12(a, b, o12);
+    const float none[A] = {};
+    write_row_generic<A>(a.obs + size_t(e) * a.D, o12, a.ring, a.B, E, e, head, none, false);
+}
+
+// snapshot <-> internal ring: user fields ring_{s}_{j} = [B*A][E] (physical slot s, per-env
+// ring_head); internal [B][E][A].  Both keep the same physical slots and heads.
+__global__ void ring_get_kernel(const float* __restrict__ ring, void* dst, int is_double, int B, int A, int E) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    for (int s = 0; s < B; ++s)
+        for (int j = 0; j < A; ++j) {
+            const float v = ring[(size_t(s) * E + e) * A + j];
+            const size_t o = size_t(s * A + j) * E + e;
+            if (is_double) static_cast<double*>(dst)[o] = v;
+            else static_cast<float*>(dst)[o] = v;
+        }
+}
+__global__ void ring_set_kernel(float* __restrict__ ring, const void* src, int is_double, int B, int A, int E) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    for (int s = 0; s < B; ++s)
+        for (int j = 0; j < A; ++j) {
+            const size_t o = size_t(s * A + j) * E + e;
+            ring[(size_t(s) * E + e) * A + j] =
+                is_double ? float(static_cast<const double*>(src)[o]) : static_cast<const float*>(src)[o];
+        }
+}
+
+}  // namespace adrp

@@ -1,0 +1,135 @@
+"""HoverAviary on the GPU: E independent envs stepped by one fused HIP launch.
+
+Mirrors the reference surface (envs/HoverAviary.py:11-117, envs/BaseRLAviary.py,
+envs/BaseAviary.py): same constructor arguments and attributes, same per-env
+observation/action spaces, same obs layout [pos, rpy, vel, ang_v, 15 past actions],
+reward max(0, 2-|p-(0,0,1)|^4), terminated |p-target|<1e-4, truncated by bounds / tilt /
+8 s.  Batched extras: ``num_envs``, ``device``, ``precision``, ``seed``, ``autoreset``
+and ``init_noise`` (per-reset uniform perturbation of the initial state, 0 = reference).
+
+``step``/``reset`` take and return torch tensors that live on the GPU (no host copy):
+obs [E, 1, D] float32, reward [E] float32, terminated / truncated [E] bool.
+"""
+import numpy as np
+import torch
+
+from .. import _lib
+from ..utils import abi
+from ..utils.enums import ActionType, DroneModel, ObservationType, Physics, PHYSICS_CODE
+from ..utils.spaces import Box
+
+
+class HoverAviary:
+    """Batched counterpart of gym_pybullet_adrp.envs.HoverAviary."""
+
+    def __init__(self, drone_model: DroneModel = DroneModel.CF2X, initial_xyzs=None, initial_rpys=None,
+                 physics: Physics = Physics.PYB, pyb_freq: int = 240, ctrl_freq: int = 30, gui=False,
+                 record=False, obs: ObservationType = ObservationType.KIN, act: ActionType = ActionType.RPM,
+                 *, num_envs: int = 1, device: int = 0, precision: str = "fp32", seed: int = 0,
+                 autoreset: bool = True, init_noise=None, env_offset: int = 0, link_frame_lag: bool = True):
+        if drone_model != DroneModel.CF2X:
+            raise ValueError("only DroneModel.CF2X (cf2x_IROS.urdf) is supported")
+        if gui or record:
+            raise ValueError("GUI / video recording are out of scope (DESIGN.md)")
+        if obs != ObservationType.KIN:
+            raise ValueError("only ObservationType.KIN is supported")
+        if act not in (ActionType.RPM, ActionType.ONE_D_RPM):
+            raise ValueError("supported action types: RPM, ONE_D_RPM")
+        if pyb_freq % ctrl_freq != 0:
+            raise ValueError("[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.")
+        cfg = _lib.default_config(abi.TASK_HOVER)
+        cfg.physics = PHYSICS_CODE[physics]
+        cfg.act_type = abi.ACT_ONE_D_RPM if act == ActionType.ONE_D_RPM else abi.ACT_RPM
+        cfg.num_envs = int(num_envs)
+        cfg.pyb_freq, cfg.ctrl_freq = int(pyb_freq), int(ctrl_freq)
+        cfg.action_buffer_size = int(ctrl_freq // 2)
+        cfg.autoreset = 1 if autoreset else 0
+        cfg.precision = {"fp32": 0, "fp64": 1}[precision]
+        cfg.link_frame_lag = 1 if link_frame_lag else 0
+        cfg.seed = int(seed) & (2 ** 64 - 1)
+        cfg.env_offset = int(env_offset)
+        if initial_xyzs is not None:
+            abi.set_vec(cfg.init_xyz[0], np.asarray(initial_xyzs, float).reshape(3))
+        if initial_rpys is not None:
+            abi.set_vec(cfg.init_rpy[0], np.asarray(initial_rpys, float).reshape(3))
+        for key, dst in (("xyz", cfg.init_xyz_noise), ("rpy", cfg.init_rpy_noise), ("vel", cfg.init_vel_noise),
+                         ("omega", cfg.init_omega_noise)):
+            if init_noise and key in init_noise:
+                abi.set_vec(dst, np.broadcast_to(np.asarray(init_noise[key], float), 3))
+        self.cfg = cfg
+        self.h = _lib.Handle(cfg, device)
+        self.device = self.h.device
+        # reference attributes
+        self.DRONE_MODEL, self.PHYSICS, self.OBS_TYPE, self.ACT_TYPE = drone_model, physics, obs, act
+        self.NUM_DRONES = 1
+        self.PYB_FREQ, self.CTRL_FREQ = int(pyb_freq), int(ctrl_freq)
+        self.PYB_STEPS_PER_CTRL = self.PYB_FREQ // self.CTRL_FREQ
+        self.PYB_TIMESTEP, self.CTRL_TIMESTEP = 1.0 / self.PYB_FREQ, 1.0 / self.CTRL_FREQ
+        self.ACTION_BUFFER_SIZE = int(ctrl_freq // 2)
+        self.TARGET_POS = np.array([0, 0, 1])
+        self.EPISODE_LEN_SEC = 8
+        d = cfg.drone
+        self.M, self.L, self.KF, self.KM = d.m, d.l, d.kf, d.km
+        self.J = np.diag([d.ixx, d.iyy, d.izz])
+        self.G = cfg.gravity
+        self.GRAVITY = self.G * self.M
+        self.HOVER_RPM = np.sqrt(self.GRAVITY / (4 * self.KF))
+        self.MAX_RPM = np.sqrt((d.thrust2weight * self.GRAVITY) / (4 * self.KF))
+        self.num_envs = cfg.num_envs
+        self.action_space = self._actionSpace()
+        self.observation_space = self._observationSpace()
+        E, D = self.num_envs, self.h.D
+        self._obs = torch.zeros((E, 1, D), dtype=torch.float32, device=self.device)
+        self._tobs = torch.zeros_like(self._obs)
+        self._rew = torch.zeros(E, dtype=torch.float32, device=self.device)
+        self._term = torch.zeros(E, dtype=torch.uint8, device=self.device)
+        self._trunc = torch.zeros(E, dtype=torch.uint8, device=self.device)
+
+    # ---- spaces (BaseRLAviary.py:132-156, 243-277) ----
+    def _actionSpace(self):
+        size = 1 if self.ACT_TYPE == ActionType.ONE_D_RPM else 4
+        return Box(low=-np.ones((1, size)), high=np.ones((1, size)), dtype=np.float32)
+
+    def _observationSpace(self):
+        lo, hi = -np.inf, np.inf
+        low = [lo, lo, 0] + [lo] * 9
+        high = [hi] * 12
+        size = 1 if self.ACT_TYPE == ActionType.ONE_D_RPM else 4
+        low += [-1] * size * self.ACTION_BUFFER_SIZE
+        high += [+1] * size * self.ACTION_BUFFER_SIZE
+        return Box(low=np.array([low]), high=np.array([high]), dtype=np.float32)
+
+    # ---- gymnasium-style API, batched ----
+    def reset(self, seed: int = None, options: dict = None, mask=None):
+        """Reset all envs (or those with mask[e] != 0). Returns (obs [E,1,D], info)."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        self.h.reset(self._obs, m)
+        return self._obs, {"answer": 42}
+
+    def step(self, action):
+        """One env.step of every env: action [E,1,A] (torch or numpy, in [-1,1])."""
+        act = torch.as_tensor(action, device=self.device, dtype=torch.float32)
+        if act.shape != (self.num_envs, 1, self.h.A):
+            act = act.reshape(self.num_envs, 1, self.h.A)
+        act = act.contiguous()
+        self.h.step(act, self._obs, self._rew, self._term, self._trunc, self._tobs)
+        info = {"answer": 42, "terminal_observation": self._tobs}
+        return self._obs, self._rew, self._term.bool(), self._trunc.bool(), info
+
+    def close(self):
+        self.h.close()
+
+    # ---- introspection (tests / teacher forcing) ----
+    def get_state(self):
+        return self.h.get_state()
+
+    def set_state(self, f, i):
+        self.h.set_state(f, i)
+
+    def state_field_names(self):
+        return self.h.field_names()
+
+    def step_bytes(self):
+        return self.h.step_bytes()

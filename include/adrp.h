@@ -181,8 +181,9 @@ int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
  * [E*N] vector (drone-major within env: index e*N+n).  Field names: adrp_state_field. */
 int adrp_state_layout(const adrp_t* h, int* nf, int* ni);
 const char* adrp_state_field(const adrp_t* h, int is_int, int index);
-int adrp_get_state(adrp_t* h, float* f_dev, int32_t* i_dev, void* stream);
-int adrp_set_state(adrp_t* h, const float* f_dev, const int32_t* i_dev, void* stream);
+/* f_dev elements are float32 for precision 0 and float64 for precision 1. */
+int adrp_get_state(adrp_t* h, void* f_dev, int32_t* i_dev, void* stream);
+int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev, void* stream);
 
 /* Algorithmic HBM bytes one adrp_step moves (roofline accounting). */
 int64_t adrp_step_bytes(const adrp_t* h);

@@ -670,10 +670,9 @@ static const char* k_hover_f[] = {"pos_x", "pos_y", "pos_z", "quat_x", "quat_y",
                                   "vel_x", "vel_y", "vel_z", "omega_x", "omega_y", "omega_z",
                                   "last_rpm_0", "last_rpm_1", "last_rpm_2", "last_rpm_3",
                                   "angv_x", "angv_y", "angv_z",
-                                  "link_quat_x", "link_quat_y", "link_quat_z", "link_quat_w",
-                                  "link_pos_x", "link_pos_y", "link_pos_z"};
+                                  "link_quat_x", "link_quat_y", "link_quat_z", "link_quat_w"};
 static const char* k_hover_i[] = {"step_counter", "episode", "ring_head"};
-#define HOVER_NF_BASE 27
+#define HOVER_NF_BASE 24
 
 int orc_state_layout(const orc_t* o, int* nf, int* ni) {
     *nf = HOVER_NF_BASE + o->cfg.action_buffer_size * o->A;
@@ -702,8 +701,7 @@ int orc_get_state(const orc_t* o, double* f, int32_t* ii) {
         qt lq = qconj(b->link_q_wtb);
         double v[HOVER_NF_BASE] = {b->pos.x, b->pos.y, b->pos.z, q.x, q.y, q.z, q.w, b->vel.x, b->vel.y, b->vel.z,
                                    w.x, w.y, w.z, b->last_rpm[0], b->last_rpm[1], b->last_rpm[2], b->last_rpm[3],
-                                   b->ang_v.x, b->ang_v.y, b->ang_v.z, lq.x, lq.y, lq.z, lq.w,
-                                   b->link_pos.x, b->link_pos.y, b->link_pos.z};
+                                   b->ang_v.x, b->ang_v.y, b->ang_v.z, lq.x, lq.y, lq.z, lq.w};
         for (int k = 0; k < HOVER_NF_BASE; ++k) f[(size_t)k * E + e] = v[k];
         for (int k = 0; k < B * A; ++k) f[(size_t)(HOVER_NF_BASE + k) * E + e] = o->ring[(size_t)e * B * A + k];
         ii[e] = o->step_counter[e];
@@ -733,7 +731,7 @@ int orc_set_state(orc_t* o, const double* f, const int32_t* ii) {
         for (int k = 0; k < 4; ++k) b->last_rpm[k] = F_(13 + k);
         qt lq = {F_(20), F_(21), F_(22), F_(23)};
         b->link_q_wtb = qconj(lq);
-        b->link_pos = V(F_(24), F_(25), F_(26));
+        b->link_pos = b->pos;
         for (int k = 0; k < B * A; ++k) o->ring[(size_t)e * B * A + k] = (float)F_(HOVER_NF_BASE + k);
 #undef F_
         o->step_counter[e] = ii[e];
