@@ -42,7 +42,6 @@ def parse():
     p.add_argument("--precision", default="fp32")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--graph", type=int, default=1, help="also time HIP-graph replay of the step loop")
     return p.parse_args()
 
 
@@ -96,17 +95,26 @@ def main():
         env.step(acts[k % nbuf])
     torch.cuda.synchronize()
 
-    # ---- timed region: K env.steps, per-launch HIP events on the launching stream ----
+    # ---- timed region: exactly K env.steps, replayed from a captured HIP graph ----
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    G = max(g for g in range(1, min(K, 256) + 1) if K % g == 0)   # steps per graph, G | K
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        env.step(acts[0])
+    torch.cuda.current_stream(dev).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for k in range(G):
+            env.step(acts[k % nbuf])
+    graph.replay()                                           # untimed: warms the graph
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        ev[k][0].record()
-        env.step(acts[k % nbuf])
-        ev[k][1].record()
+    for _ in range(K // G):
+        graph.replay()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -115,39 +123,32 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    kern_ms = np.array([s.elapsed_time(e) for s, e in ev])
-    kern_avg_s = float(kern_ms.mean()) / 1e3
 
-    # ---- HIP-graph replay of the same step loop (launch-bound regime) ----
-    graph = None
-    if args.graph:
-        try:
-            G = 64
-            s = torch.cuda.Stream(device=dev)
-            s.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(s):
-                for k in range(3):
-                    env.step(acts[k])
-            torch.cuda.current_stream(dev).wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for k in range(G):
-                    env.step(acts[k % nbuf])
-            g.replay()
-            torch.cuda.synchronize()
-            reps = max(1, K // G)
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            tg0 = time.perf_counter()
-            for _ in range(reps):
-                g.replay()
-            torch.cuda.synchronize()
-            tg = time.perf_counter() - tg0
-            graph = {"env_steps_per_s_per_gpu": E * G * reps / tg, "ms_per_step": tg / (G * reps) * 1e3,
-                     "steps_per_graph": G}
-        except Exception as exc:  # graph capture is an optimisation, not the measurement
-            graph = {"error": str(exc)[:200]}
+    # ---- kernel duration: per-launch HIP events on the launching stream.  The stream is
+    # pre-loaded with a device-side sleep so the host enqueues every launch before the GPU
+    # reaches them: launches then run back-to-back and each event pair brackets one kernel.
+    nk = min(K, 512)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
+    torch.cuda.synchronize()
+    torch.cuda._sleep(int(2e7))
+    for k in range(nk):
+        ev[k][0].record()
+        env.step(acts[k % nbuf])
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    kern_ms = np.array([s.elapsed_time(e) for s, e in ev])
+    kern_avg_s = float(np.median(kern_ms)) / 1e3
+    span_s = ev[0][0].elapsed_time(ev[-1][1]) / 1e3 / nk
+
+    # ---- eager (no graph) end-to-end rate, for reference ----
+    torch.cuda.synchronize()
+    te0 = time.perf_counter()
+    ne = min(K, 1000)
+    for k in range(ne):
+        env.step(acts[k % nbuf])
+    torch.cuda.synchronize()
+    eager = {"env_steps_per_s_per_gpu": E * ne / (time.perf_counter() - te0),
+             "ms_per_step": (time.perf_counter() - te0) / ne * 1e3}
 
     bytes_per_launch = env.step_bytes()
     achieved = bytes_per_launch / kern_avg_s / 1e9
@@ -177,8 +178,10 @@ def main():
                    "drones_per_env": 1, "parallelism": f"env-sharded dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                     "bytes_per_launch": bytes_per_launch, "kernel_us": kern_avg_s * 1e6},
-        "graph_replay": graph,
+                     "bytes_per_launch": bytes_per_launch, "kernel_us": kern_avg_s * 1e6,
+                     "back_to_back_us_per_launch": span_s * 1e6},
+        "timing": {"timed_region": f"{K // G} replays of a {G}-step HIP graph (one fused launch per env.step)",
+                   "eager": eager},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(env.cfg, args.cpu_seconds)

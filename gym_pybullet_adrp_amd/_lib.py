@@ -98,6 +98,7 @@ class Handle:
         self.lib.adrp_state_layout(h, ctypes.byref(nf), ctypes.byref(ni))
         self.nf, self.ni = nf.value, ni.value
         self.real = torch.float64 if cfg.precision else torch.float32
+        self._step = self.lib.adrp_step
 
     def close(self):
         if getattr(self, "h", None):
@@ -115,7 +116,7 @@ class Handle:
             raise AdrpError(f"{what}: {self.lib.adrp_last_error(self.h).decode()}")
 
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return torch.cuda.current_stream(self.device).cuda_stream
 
     def field_names(self):
         return ([self.lib.adrp_state_field(self.h, 0, k).decode() for k in range(self.nf)],
@@ -125,8 +126,11 @@ class Handle:
         self._check(self.lib.adrp_reset(self.h, _p(mask), _p(obs), self._stream()), "adrp_reset")
 
     def step(self, act, obs, rew, term, trunc, tobs=None):
-        self._check(self.lib.adrp_step(self.h, _p(act), _p(obs), _p(rew), _p(term), _p(trunc), _p(tobs),
-                                       self._stream()), "adrp_step")
+        rc = self._step(self.h, act.data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
+                        trunc.data_ptr(), None if tobs is None else tobs.data_ptr(),
+                        torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            self._check(rc, "adrp_step")
 
     def get_state(self):
         f = torch.empty((self.nf, self.E * self.N), dtype=self.real, device=self.device)

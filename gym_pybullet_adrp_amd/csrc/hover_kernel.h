@@ -75,10 +75,16 @@ struct Body {
     Real prev_rpm[4];
 };
 
-template <typename Real>
-__device__ __forceinline__ Real clamp100(Real x) {
-    return x < Real(-100) ? Real(-100) : (x > Real(100) ? Real(100) : x);
+// float32 1 + 0.05 a, two roundings as NumPy does it (no FMA contraction)
+__device__ __forceinline__ float rpm_gain(float a) {
+#pragma clang fp contract(off)
+    const float m = 0.05f * a;
+    return 1.0f + m;
 }
+
+// btClamp(x, -m_maxCoordinateVelocity, m_maxCoordinateVelocity): one v_med3_f32
+__device__ __forceinline__ float clamp100(float x) { return __builtin_amdgcn_fmed3f(x, -100.0f, 100.0f); }
+__device__ __forceinline__ double clamp100(double x) { return x < -100.0 ? -100.0 : (x > 100.0 ? 100.0 : x); }
 
 // One Bullet stepSimulation of one drone after the reference's force calls.
 // R = rot(b.q) on entry; Rs = rotation of the cached link basis.  On exit R/Rs are the
@@ -160,11 +166,9 @@ __device__ __forceinline__ bool pyb_substep(const HoverArgs<Real>& a, Body<Real>
     b.q = {q1.x * inv, q1.y * inv, q1.z * inv, q1.w * inv};
     R = rot(b.q);
     if (!a.link_lag) Rs = R;
-    // plane contact model: non-penetration, no inward velocity
-    const Real r22 = R.a22;
-    Real s2 = Real(1) - r22 * r22;
-    s2 = s2 < Real(0) ? Real(0) : s2;
-    const Real low = b.pos.z + a.coll_zoff - a.coll_hh * fabs_(r22) - a.coll_r * hsqrt_(s2);
+    // plane contact model: non-penetration, no inward velocity.
+    // lowest point of the body cylinder: cos(tilt) = R22, sin(tilt) = |(R02, R12)|
+    const Real low = b.pos.z + a.coll_zoff - a.coll_hh * fabs_(R.a22) - a.coll_r * hsqrt_(R.a02 * R.a02 + R.a12 * R.a12);
     if (low < Real(0)) {
         b.pos.z -= low;
         if (b.vel.z < Real(0)) b.vel.z = Real(0);
@@ -389,10 +393,7 @@ __global__ void __launch_bounds__(256) hover_step_kernel(HoverArgs<Real> a) {
     // ---- _preprocessAction: RPM = HOVER_RPM * (1 + 0.05 a), the gain in float32 (NEP 50) ----
     Real rpm[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float g = __fadd_rn(1.0f, __fmul_rn(0.05f, act[A == 1 ? 0 : i]));
-        rpm[i] = a.hover_rpm * Real(g);
-    }
+    for (int i = 0; i < 4; ++i) rpm[i] = a.hover_rpm * Real(rpm_gain(act[A == 1 ? 0 : i]));
     // ---- sub-step loop (BaseAviary.py:347-376) ----
     bool touched = false;
     if constexpr (DYN) {

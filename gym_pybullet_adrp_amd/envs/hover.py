@@ -82,8 +82,11 @@ class HoverAviary:
         self._obs = torch.zeros((E, 1, D), dtype=torch.float32, device=self.device)
         self._tobs = torch.zeros_like(self._obs)
         self._rew = torch.zeros(E, dtype=torch.float32, device=self.device)
-        self._term = torch.zeros(E, dtype=torch.uint8, device=self.device)
-        self._trunc = torch.zeros(E, dtype=torch.uint8, device=self.device)
+        # the kernel writes 0/1 bytes: valid torch.bool storage, returned without a cast
+        self._term = torch.zeros(E, dtype=torch.bool, device=self.device)
+        self._trunc = torch.zeros(E, dtype=torch.bool, device=self.device)
+        self._act_shape = (E, 1, self.h.A)
+        self._info = {"answer": 42, "terminal_observation": self._tobs}
 
     # ---- spaces (BaseRLAviary.py:132-156, 243-277) ----
     def _actionSpace(self):
@@ -109,14 +112,17 @@ class HoverAviary:
         return self._obs, {"answer": 42}
 
     def step(self, action):
-        """One env.step of every env: action [E,1,A] (torch or numpy, in [-1,1])."""
-        act = torch.as_tensor(action, device=self.device, dtype=torch.float32)
-        if act.shape != (self.num_envs, 1, self.h.A):
-            act = act.reshape(self.num_envs, 1, self.h.A)
-        act = act.contiguous()
+        """One env.step of every env: action [E,1,A] (torch or numpy, in [-1,1]).
+
+        Returns views of persistent device buffers (obs [E,1,D], reward [E],
+        terminated [E], truncated [E]) that the next step overwrites."""
+        act = action
+        if not (isinstance(act, torch.Tensor) and act.dtype == torch.float32 and act.device == self.device
+                and act.is_contiguous() and act.shape == self._act_shape):
+            act = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(self._act_shape)
+            act = act.contiguous()
         self.h.step(act, self._obs, self._rew, self._term, self._trunc, self._tobs)
-        info = {"answer": 42, "terminal_observation": self._tobs}
-        return self._obs, self._rew, self._term.bool(), self._trunc.bool(), info
+        return self._obs, self._rew, self._term, self._trunc, self._info
 
     def close(self):
         self.h.close()

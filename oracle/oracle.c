@@ -480,10 +480,9 @@ static int bullet_step(const orc_t* o, body_t* b, const forces_t* F, double mass
     /* ground model (plane z = 0 vs the URDF collision cylinder): non-penetration +
        zero inward normal velocity.  Not Bullet's contact solver: excluded from parity. */
     m33 R = mat_from_quat(qconj(b->q_wtb));
-    double r33 = R.m[2][2];
-    double s = 1.0 - r33 * r33; if (s < 0) s = 0;
-    double low = b->pos.z + o->cfg.drone.collision_z_offset - 0.5 * o->cfg.drone.collision_h * fabs(r33)
-                 - o->cfg.drone.collision_r * sqrt(s);
+    /* lowest point of the body cylinder: cos(tilt) = R33, sin(tilt) = |(R13, R23)| */
+    double low = b->pos.z + o->cfg.drone.collision_z_offset - 0.5 * o->cfg.drone.collision_h * fabs(R.m[2][2])
+                 - o->cfg.drone.collision_r * sqrt(R.m[0][2] * R.m[0][2] + R.m[1][2] * R.m[1][2]);
     if (low < 0.0) {
         b->pos.z -= low;
         if (b->vel.z < 0) b->vel.z = 0;
