@@ -55,8 +55,14 @@ def load():
     lib.adrp_set_state.argtypes = [P, P, P, P]
     lib.adrp_step_bytes.argtypes = [P]
     lib.adrp_step_bytes.restype = ctypes.c_int64
-    lib.adrp_debug_contact_count.argtypes = [P, I]
-    lib.adrp_debug_contact_count.restype = I
+    lib.adrp_profile_begin.argtypes = [P, I]
+    lib.adrp_profile_begin.restype = I
+    lib.adrp_profile_end.argtypes = [P, P, I]
+    lib.adrp_profile_end.restype = I
+    lib.adrp_set_diagnostics.argtypes = [P, I]
+    lib.adrp_set_diagnostics.restype = I
+    lib.adrp_diagnostic_contact_count.argtypes = [P, I]
+    lib.adrp_diagnostic_contact_count.restype = I
     if lib.adrp_abi_version() != abi.ABI_VERSION:
         raise AdrpError(f"libadrp ABI {lib.adrp_abi_version()} != python mirror {abi.ABI_VERSION}")
     _lib = lib
@@ -147,5 +153,20 @@ class Handle:
     def step_bytes(self):
         return self.lib.adrp_step_bytes(self.h)
 
+    def set_diagnostics(self, enable=True):
+        self._check(self.lib.adrp_set_diagnostics(self.h, 1 if enable else 0), "adrp_set_diagnostics")
+
     def contact_count(self, reset=True):
-        return self.lib.adrp_debug_contact_count(self.h, 1 if reset else 0)
+        """env-steps that touched the plane contact model since the last reset (diagnostics on)"""
+        return self.lib.adrp_diagnostic_contact_count(self.h, 1 if reset else 0)
+
+    def profile_begin(self, n):
+        self._check(self.lib.adrp_profile_begin(self.h, n), "adrp_profile_begin")
+
+    def profile_end(self, n):
+        import numpy as np
+        out = np.zeros(n, np.float32)
+        got = self.lib.adrp_profile_end(self.h, out.ctypes.data_as(ctypes.c_void_p), n)
+        if got < 0:
+            self._check(got, "adrp_profile_end")
+        return out[:got]

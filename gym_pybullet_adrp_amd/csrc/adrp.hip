@@ -3,13 +3,16 @@
 // Build (gfx950 only):  see gym_pybullet_adrp_amd/csrc/Makefile
 // No CPU fallback: every entry point that computes needs a HIP device and fails with
 // ADRP_ERR_DEVICE otherwise.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <vector>
 
 #include "../../include/adrp.h"
 #include "hover_kernel.h"
@@ -26,6 +29,10 @@ struct adrp_handle {
     float* ring = nullptr;    // [B*A][E]
     int32_t* ist = nullptr;   // [ni][E*N]
     int32_t* counters = nullptr;  // device diagnostics (ground-model hits)
+    int diagnostics = 0;
+    // kernel timing (adrp_profile_begin/end)
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    int prof_cap = 0, prof_n = 0;
     std::string err;
 };
 
@@ -159,7 +166,7 @@ static HoverArgs<Real> hover_args(const adrp_t* h) {
     a.f = (Real*)h->f;
     a.ring = h->ring;
     a.ist = h->ist;
-    a.contact_count = h->counters;
+    a.contact_count = h->diagnostics ? h->counters : nullptr;
     return a;
 }
 
@@ -228,6 +235,8 @@ extern "C" void adrp_destroy(adrp_t* h) {
     if (!h) return;
     hipSetDevice(h->device);
     hipDeviceSynchronize();
+    for (auto e : h->ev_start) hipEventDestroy(e);
+    for (auto e : h->ev_stop) hipEventDestroy(e);
     hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters);
     delete h;
 }
@@ -240,16 +249,27 @@ extern "C" int adrp_act_dim(const adrp_t* h) { return h ? h->A : ADRP_ERR_INVALI
 // ---------------------------------------------------------------------------------------------
 constexpr int kBlock = 64;   // one wave per workgroup: E=4096 -> 64 CUs busy, no intra-block sync
 
+// launch with optional start/stop events recorded by the dispatch itself
+template <typename K, typename Args>
+static void launch(K kernel, dim3 grid, dim3 blk, hipStream_t s, const Args& a, adrp_t* h) {
+    if (h->prof_n < h->prof_cap) {
+        hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
+        ++h->prof_n;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
+    }
+}
+
 template <typename Real, int A, int B>
-static void launch_step_ph(const HoverArgs<Real>& a, int physics, dim3 grid, hipStream_t s) {
+static void launch_step_ph(const HoverArgs<Real>& a, int physics, dim3 grid, hipStream_t s, adrp_t* h) {
     const dim3 blk(kBlock);
     switch (physics) {
-        case ADRP_PHYS_PYB: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB, A, B>), grid, blk, 0, s, a); break;
-        case ADRP_PHYS_DYN: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_DYN, A, B>), grid, blk, 0, s, a); break;
-        case ADRP_PHYS_PYB_GND: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B>), grid, blk, 0, s, a); break;
-        case ADRP_PHYS_PYB_DRAG: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B>), grid, blk, 0, s, a); break;
-        case ADRP_PHYS_PYB_DW: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B>), grid, blk, 0, s, a); break;
-        default: hipLaunchKernelGGL((hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B>), grid, blk, 0, s, a); break;
+        case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_GND: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_DRAG: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_DW: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B>, grid, blk, s, a, h); break;
+        default: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B>, grid, blk, s, a, h); break;
     }
 }
 
@@ -261,11 +281,11 @@ static int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8
     const dim3 grid((h->E + kBlock - 1) / kBlock);
     const int ph = h->cfg.physics;
     if (h->A == 1) {
-        if (h->B == 15) launch_step_ph<Real, 1, 15>(a, ph, grid, s);
-        else launch_step_ph<Real, 1, 0>(a, ph, grid, s);
+        if (h->B == 15) launch_step_ph<Real, 1, 15>(a, ph, grid, s, h);
+        else launch_step_ph<Real, 1, 0>(a, ph, grid, s, h);
     } else {
-        if (h->B == 15) launch_step_ph<Real, 4, 15>(a, ph, grid, s);
-        else launch_step_ph<Real, 4, 0>(a, ph, grid, s);
+        if (h->B == 15) launch_step_ph<Real, 4, 15>(a, ph, grid, s, h);
+        else launch_step_ph<Real, 4, 0>(a, ph, grid, s, h);
     }
     HIPCHK(h, hipGetLastError());
     return ADRP_OK;
@@ -377,8 +397,44 @@ extern "C" int64_t adrp_step_bytes(const adrp_t* h) {
     return per_env * h->E;
 }
 
-// diagnostics for tests: number of envs whose last step touched the plane contact model
-extern "C" int adrp_debug_contact_count(adrp_t* h, int reset) {
+// ---------------------------------------------------------------------------------------------
+// kernel timing and diagnostics
+// ---------------------------------------------------------------------------------------------
+extern "C" int adrp_profile_begin(adrp_t* h, int max_launches) {
+    if (!h || max_launches < 0 || max_launches > (1 << 20)) return seterr(h, ADRP_ERR_INVALID, "max_launches");
+    HIPCHK(h, hipSetDevice(h->device));
+    while ((int)h->ev_start.size() < max_launches) {
+        hipEvent_t a, b;
+        HIPCHK(h, hipEventCreate(&a));
+        HIPCHK(h, hipEventCreate(&b));
+        h->ev_start.push_back(a);
+        h->ev_stop.push_back(b);
+    }
+    h->prof_cap = max_launches;
+    h->prof_n = 0;
+    return ADRP_OK;
+}
+
+extern "C" int adrp_profile_end(adrp_t* h, float* kernel_ms, int cap) {
+    if (!h) return ADRP_ERR_INVALID;
+    HIPCHK(h, hipSetDevice(h->device));
+    const int n = std::min(h->prof_n, cap);
+    for (int k = 0; k < n; ++k) {
+        HIPCHK(h, hipEventSynchronize(h->ev_stop[k]));
+        HIPCHK(h, hipEventElapsedTime(&kernel_ms[k], h->ev_start[k], h->ev_stop[k]));
+    }
+    h->prof_cap = 0;
+    h->prof_n = 0;
+    return n;
+}
+
+extern "C" int adrp_set_diagnostics(adrp_t* h, int enable) {
+    if (!h) return ADRP_ERR_INVALID;
+    h->diagnostics = enable ? 1 : 0;
+    return ADRP_OK;
+}
+
+extern "C" int adrp_diagnostic_contact_count(adrp_t* h, int reset) {
     if (!h) return ADRP_ERR_INVALID;
     int32_t v = 0;
     if (hipMemcpy(&v, h->counters, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return ADRP_ERR_DEVICE;

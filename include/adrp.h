@@ -188,6 +188,18 @@ int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev, void* str
 /* Algorithmic HBM bytes one adrp_step moves (roofline accounting). */
 int64_t adrp_step_bytes(const adrp_t* h);
 
+/* Kernel timing with HIP events attached to the step kernel's own dispatch
+ * (hipExtLaunchKernelGGL start/stop events): after adrp_profile_begin(h, n) the next n
+ * adrp_step launches are timed; adrp_profile_end synchronises and writes up to `cap`
+ * kernel durations [ms] to kernel_ms (host memory), returning how many were written. */
+int adrp_profile_begin(adrp_t* h, int max_launches);
+int adrp_profile_end(adrp_t* h, float* kernel_ms, int cap);
+
+/* Diagnostics (off by default, costs a same-address atomic per touching wave):
+ * count env-steps whose sub-steps touched the plane contact model. */
+int adrp_set_diagnostics(adrp_t* h, int enable);
+int adrp_diagnostic_contact_count(adrp_t* h, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -191,6 +191,7 @@ def test_ground_contact_model():
     env, orc = pair(E, Physics.PYB, autoreset=False)   # default start z = 0.1125
     env.reset(); orc.reset()
     act = -np.ones((E, 1, 4), np.float32)              # 0.95 HOVER_RPM: sinks, then rests
+    env.h.set_diagnostics(True)
     env.h.contact_count(reset=True)
     touched = 0
     for t in range(40):
