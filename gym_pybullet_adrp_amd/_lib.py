@@ -53,6 +53,8 @@ def load():
     lib.adrp_state_field.restype = ctypes.c_char_p
     lib.adrp_get_state.argtypes = [P, P, P, P]
     lib.adrp_set_state.argtypes = [P, P, P, P]
+    lib.adrp_kernel_name.argtypes = [P]
+    lib.adrp_kernel_name.restype = ctypes.c_char_p
     lib.adrp_step_bytes.argtypes = [P]
     lib.adrp_step_bytes.restype = ctypes.c_int64
     lib.adrp_profile_begin.argtypes = [P, I]
@@ -75,6 +77,11 @@ def default_config(task):
     if rc != 0:
         raise AdrpError(load().adrp_last_error(None).decode())
     return cfg
+
+
+def kernel_name(cfg):
+    """step-kernel instantiation this config selects (see include/adrp.h)"""
+    return load().adrp_kernel_name(ctypes.byref(cfg)).decode()
 
 
 def _p(t):

@@ -29,6 +29,8 @@ struct adrp_handle {
     float* ring = nullptr;    // [B*A][E]
     int32_t* ist = nullptr;   // [ni][E*N]
     int32_t* counters = nullptr;  // device diagnostics (ground-model hits)
+    void* cblk = nullptr;         // device HoverConst<Real> + HoverReset<Real>
+    bool cf2x = false;            // compiled-in constants (hover_step_kernel<..., DEF=true>)
     int diagnostics = 0;
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -124,19 +126,23 @@ static void derived(const adrp_config& c, double* hover_rpm, double* gnd_clip) {
     *gnd_clip = 0.25 * d.prop_radius * sqrt((15 * maxr * maxr * d.kf * d.gnd_eff_coeff) / maxt);
 }
 
-template <typename Real>
-static HoverArgs<Real> hover_args(const adrp_t* h) {
-    const adrp_config& c = h->cfg;
-    const adrp_drone_params& d = c.drone;
-    HoverArgs<Real> a;
-    memset(&a, 0, sizeof a);
-    a.E = h->E; a.S = h->S; a.A = h->A; a.B = h->B; a.D = h->D;
-    a.physics = c.physics; a.autoreset = c.autoreset; a.link_lag = c.link_frame_lag ? 1 : 0;
+static int trunc_steps(const adrp_config& c) {
     // truncated when step_counter / PYB_FREQ > EPISODE_LEN_SEC in float64 (HoverAviary.py:114)
     long long t = (long long)floor(c.episode_len_sec * c.pyb_freq) - 2;
     if (t < 0) t = 0;
     while (!((double)t / (double)c.pyb_freq > c.episode_len_sec)) ++t;
-    a.trunc_steps = (int)t;
+    return (int)t;
+}
+
+template <typename Real>
+static HoverConst<Real> hover_const(const adrp_config& c) {
+    const adrp_drone_params& d = c.drone;
+    HoverConst<Real> a;
+    memset(&a, 0, sizeof a);
+    a.S = c.pyb_freq / c.ctrl_freq;
+    a.trunc_steps = trunc_steps(c);
+    a.link_lag = c.link_frame_lag ? 1 : 0;
+    a.physics = c.physics;
     a.dt = Real(1.0 / c.pyb_freq);
     a.mass = Real(d.m); a.inv_mass = Real(1.0 / d.m); a.gravity = Real(c.gravity);
     a.ixx = Real(d.ixx); a.iyy = Real(d.iyy); a.izz = Real(d.izz);
@@ -155,12 +161,45 @@ static HoverArgs<Real> hover_args(const adrp_t* h) {
     for (int k = 0; k < 3; ++k) a.drag[k] = Real(d.drag_coeff[k]);
     a.dyn_arm = Real(d.l / sqrt(2.0));
     a.coll_hh = Real(0.5 * d.collision_h); a.coll_r = Real(d.collision_r); a.coll_zoff = Real(d.collision_z_offset);
+    for (int k = 0; k < 3; ++k) a.target[k] = Real(c.target_pos[k]);
+    return a;
+}
+
+template <typename Real>
+static HoverReset<Real> hover_reset_dist(const adrp_config& c) {
+    HoverReset<Real> r;
+    memset(&r, 0, sizeof r);
     for (int k = 0; k < 3; ++k) {
-        a.target[k] = Real(c.target_pos[k]);
-        a.init_xyz[k] = Real(c.init_xyz[0][k]); a.init_rpy[k] = Real(c.init_rpy[0][k]);
-        a.n_xyz[k] = Real(c.init_xyz_noise[k]); a.n_rpy[k] = Real(c.init_rpy_noise[k]);
-        a.n_vel[k] = Real(c.init_vel_noise[k]); a.n_om[k] = Real(c.init_omega_noise[k]);
+        r.init_xyz[k] = Real(c.init_xyz[0][k]); r.init_rpy[k] = Real(c.init_rpy[0][k]);
+        r.n_xyz[k] = Real(c.init_xyz_noise[k]); r.n_rpy[k] = Real(c.init_rpy_noise[k]);
+        r.n_vel[k] = Real(c.init_vel_noise[k]); r.n_om[k] = Real(c.init_omega_noise[k]);
     }
+    return r;
+}
+
+// the compiled-in constants are used only when the runtime block is bit-identical
+template <typename Real>
+static bool is_cf2x(const adrp_config& c) {
+    const HoverConst<Real> rt = hover_const<Real>(c);
+    HoverConst<Real> ct;
+    memset(&ct, 0, sizeof ct);
+    ct = cf2x_consts<Real>(c.physics);
+    return memcmp(&rt, &ct, sizeof rt) == 0;
+}
+
+static bool config_is_cf2x(const adrp_config& c) {
+    return c.precision ? is_cf2x<double>(c) : is_cf2x<float>(c);
+}
+
+template <typename Real>
+static HoverArgs<Real> hover_args(const adrp_t* h) {
+    const adrp_config& c = h->cfg;
+    HoverArgs<Real> a;
+    memset(&a, 0, sizeof a);
+    a.c = (const HoverConst<Real>*)h->cblk;
+    a.r = (const HoverReset<Real>*)((const char*)h->cblk + sizeof(HoverConst<Real>));
+    a.E = h->E; a.B = h->B; a.D = h->D;
+    a.autoreset = c.autoreset;
     a.seed = c.seed;
     a.env_offset = c.env_offset;
     a.f = (Real*)h->f;
@@ -168,6 +207,29 @@ static HoverArgs<Real> hover_args(const adrp_t* h) {
     a.ist = h->ist;
     a.contact_count = h->diagnostics ? h->counters : nullptr;
     return a;
+}
+
+template <typename Real>
+static int upload_const(adrp_t* h) {
+    const HoverConst<Real> k = hover_const<Real>(h->cfg);
+    const HoverReset<Real> r = hover_reset_dist<Real>(h->cfg);
+    if (hipMalloc(&h->cblk, sizeof k + sizeof r) != hipSuccess) return ADRP_ERR_OOM;
+    if (hipMemcpy(h->cblk, &k, sizeof k, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy((char*)h->cblk + sizeof k, &r, sizeof r, hipMemcpyHostToDevice) != hipSuccess)
+        return ADRP_ERR_DEVICE;
+    h->cf2x = is_cf2x<Real>(h->cfg);
+    return ADRP_OK;
+}
+
+extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
+    static thread_local char buf[96];
+    if (!cfg || cfg->struct_size != sizeof(adrp_config)) return nullptr;
+    static const char* ph[] = {"PYB", "DYN", "PYB_GND", "PYB_DRAG", "PYB_DW", "PYB_GND_DRAG_DW"};
+    const int p = cfg->physics >= 0 && cfg->physics <= 5 ? cfg->physics : 0;
+    const int A = cfg->act_type == ADRP_ACT_ONE_D_RPM ? 1 : 4;
+    snprintf(buf, sizeof buf, "hover_step<%s,%s,A%d,B%s,%s>", cfg->precision ? "f64" : "f32", ph[p], A,
+             cfg->action_buffer_size == 15 ? "15" : "n", config_is_cf2x(*cfg) ? "cf2x" : "generic");
+    return buf;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -211,7 +273,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     h->real_size = c.precision ? 8 : 4;
     const size_t EN = size_t(h->E) * h->N;
     auto cleanup = [&](int rc) {
-        hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters);
+        hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters); hipFree(h->cblk);
         g_err = h->err;
         delete h;
         return rc;
@@ -227,6 +289,8 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
         hipMemset(h->ist, 0, h->ni * EN * sizeof(int32_t)) != hipSuccess ||
         hipMemset(h->counters, 0, 64 * sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return cleanup(seterr(h, ADRP_ERR_DEVICE, "initialisation failed"));
+    const int rc = h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h);
+    if (rc != ADRP_OK) return cleanup(seterr(h, rc, "constant block upload failed"));
     *out = h;
     return ADRP_OK;
 }
@@ -237,7 +301,7 @@ extern "C" void adrp_destroy(adrp_t* h) {
     hipDeviceSynchronize();
     for (auto e : h->ev_start) hipEventDestroy(e);
     for (auto e : h->ev_stop) hipEventDestroy(e);
-    hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters);
+    hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters); hipFree(h->cblk);
     delete h;
 }
 
@@ -247,29 +311,34 @@ extern "C" int adrp_act_dim(const adrp_t* h) { return h ? h->A : ADRP_ERR_INVALI
 // ---------------------------------------------------------------------------------------------
 // launch dispatch
 // ---------------------------------------------------------------------------------------------
-constexpr int kBlock = 64;   // one wave per workgroup: E=4096 -> 64 CUs busy, no intra-block sync
+constexpr int kBlock = kStepBlock;
 
 // launch with optional start/stop events recorded by the dispatch itself
-template <typename K, typename Args>
-static void launch(K kernel, dim3 grid, dim3 blk, hipStream_t s, const Args& a, adrp_t* h) {
+template <typename K, typename Real>
+static void launch(K kernel, dim3 grid, dim3 blk, hipStream_t s, const HoverArgs<Real>& a, adrp_t* h) {
+    HoverTail<Real> t;
+    memset(&t, 0, sizeof t);
+    t.c = a.c; t.r = a.r; t.term = a.term; t.trunc = a.trunc; t.tobs = a.tobs; t.contact_count = a.contact_count;
+    t.seed = a.seed; t.env_offset = a.env_offset; t.B = a.B; t.D = a.D; t.autoreset = a.autoreset;
     if (h->prof_n < h->prof_cap) {
-        hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
+        hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0,
+                              a.f, a.ring, a.ist, a.act, a.obs, a.rew, a.E, t);
         ++h->prof_n;
     } else {
-        hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
+        hipLaunchKernelGGL(kernel, grid, blk, 0, s, a.f, a.ring, a.ist, a.act, a.obs, a.rew, a.E, t);
     }
 }
 
-template <typename Real, int A, int B>
+template <typename Real, int A, int B, bool DEF>
 static void launch_step_ph(const HoverArgs<Real>& a, int physics, dim3 grid, hipStream_t s, adrp_t* h) {
     const dim3 blk(kBlock);
     switch (physics) {
-        case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_GND: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_DRAG: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_DW: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B>, grid, blk, s, a, h); break;
-        default: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B, DEF>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B, DEF>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_GND: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B, DEF>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_DRAG: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B, DEF>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_DW: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B, DEF>, grid, blk, s, a, h); break;
+        default: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B, DEF>, grid, blk, s, a, h); break;
     }
 }
 
@@ -280,12 +349,16 @@ static int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8
     a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
     const dim3 grid((h->E + kBlock - 1) / kBlock);
     const int ph = h->cfg.physics;
-    if (h->A == 1) {
-        if (h->B == 15) launch_step_ph<Real, 1, 15>(a, ph, grid, s, h);
-        else launch_step_ph<Real, 1, 0>(a, ph, grid, s, h);
+    // compiled-in constants exist for the reference default (CF2X @ 240/30 Hz, B = 15)
+    if (h->cf2x && h->B == 15) {
+        if (h->A == 1) launch_step_ph<Real, 1, 15, true>(a, ph, grid, s, h);
+        else launch_step_ph<Real, 4, 15, true>(a, ph, grid, s, h);
+    } else if (h->A == 1) {
+        if (h->B == 15) launch_step_ph<Real, 1, 15, false>(a, ph, grid, s, h);
+        else launch_step_ph<Real, 1, 0, false>(a, ph, grid, s, h);
     } else {
-        if (h->B == 15) launch_step_ph<Real, 4, 15>(a, ph, grid, s, h);
-        else launch_step_ph<Real, 4, 0>(a, ph, grid, s, h);
+        if (h->B == 15) launch_step_ph<Real, 4, 15, false>(a, ph, grid, s, h);
+        else launch_step_ph<Real, 4, 0, false>(a, ph, grid, s, h);
     }
     HIPCHK(h, hipGetLastError());
     return ADRP_OK;

@@ -37,10 +37,12 @@ enum HoverField {
 };
 enum HoverInt { HI_STEP = 0, HI_EPISODE = 1, HI_RING_HEAD = 2, HI_N = 3 };
 
+// Per-config constants.  Device-resident (one block per handle, written at create, warm
+// in L2 across launches), or compiled in as literals for the reference's default drone
+// (cf2x_consts: CF2X / cf2x_IROS.urdf at 240 Hz), where they fold into immediates.
 template <typename Real>
-struct HoverArgs {
-    int E, S, A, B, D;
-    int physics, autoreset, link_lag, trunc_steps;   // truncated once step_counter >= trunc_steps
+struct HoverConst {
+    int S, trunc_steps, link_lag, physics;   // truncated once step_counter >= trunc_steps
     Real dt, mass, inv_mass, gravity;
     Real ixx, iyy, izz, inv_ixx, inv_iyy, inv_izz;
     Real kf, km, hover_rpm;
@@ -51,9 +53,46 @@ struct HoverArgs {
     Real coll_hh, coll_r, coll_zoff;         // collision cylinder half-height, radius, z offset
     Real ang_max;                            // ANGULAR_MOTION_THRESHOLD / dt
     Real target[3];
+};
+
+// HoverAviary defaults: cf2x_IROS.urdf, PYB_FREQ 240, CTRL_FREQ 30, target (0,0,1), 8 s.
+// Derived values are the float64 results of BaseAviary.py:117-128's formulas; the host
+// selects this path only when its computed block is bit-identical (adrp.hip).
+template <typename Real>
+__host__ __device__ constexpr HoverConst<Real> cf2x_consts(int physics) {
+    HoverConst<Real> c{};
+    c.S = 8; c.trunc_steps = 1921; c.link_lag = 1; c.physics = physics;
+    c.dt = Real(0.004166666666666667);
+    c.mass = Real(0.03454); c.inv_mass = Real(28.951939779965258); c.gravity = Real(9.8);
+    c.ixx = Real(1.4e-5); c.iyy = Real(1.4e-5); c.izz = Real(2.17e-5);
+    c.inv_ixx = Real(71428.57142857143); c.inv_iyy = Real(71428.57142857143); c.inv_izz = Real(46082.949308755764);
+    c.kf = Real(3.16e-10); c.km = Real(7.94e-12); c.hover_rpm = Real(16364.421890108686);
+    c.px[0] = Real(0.028); c.px[1] = Real(-0.028); c.px[2] = Real(-0.028); c.px[3] = Real(0.028);
+    c.py[0] = Real(0.028); c.py[1] = Real(0.028); c.py[2] = Real(-0.028); c.py[3] = Real(-0.028);
+    c.pz[0] = Real(0); c.pz[1] = Real(0); c.pz[2] = Real(0); c.pz[3] = Real(0);
+    c.gnd_kf = Real(3.5924744399999996e-09); c.prop_r4 = Real(0.0057837); c.gnd_clip = Real(0.03776371349209501);
+    c.drag[0] = Real(9.1785e-7); c.drag[1] = Real(9.1785e-7); c.drag[2] = Real(10.311e-7);
+    c.dyn_arm = Real(0.028072139213105935);
+    c.coll_hh = Real(0.0125); c.coll_r = Real(0.06); c.coll_zoff = Real(0);
+    c.ang_max = Real(188.49555921538757);
+    c.target[0] = Real(0); c.target[1] = Real(0); c.target[2] = Real(1);
+    return c;
+}
+
+// reset distribution (only the auto-reset / reset path reads it)
+template <typename Real>
+struct HoverReset {
     Real init_xyz[3], init_rpy[3], n_xyz[3], n_rpy[3], n_vel[3], n_om[3];
-    uint64_t seed;
-    int64_t env_offset;
+};
+
+// kernel argument block: pointers and a few scalars only (it is rewritten for every
+// launch, so it is cold in every cache: keep it to two 64-byte lines)
+constexpr int kStepBlock = 64;   // one wave per workgroup: E = 4096 -> 64 CUs, no intra-block sync
+
+template <typename Real>
+struct HoverArgs {
+    const HoverConst<Real>* c;   // device-resident constants (generic path)
+    const HoverReset<Real>* r;
     Real* f;           // [HF_NBASE][E]
     float* ring;       // [B][E][A]  (slot-major, the A floats of one env contiguous)
     int32_t* ist;      // [HI_N][E]
@@ -64,7 +103,10 @@ struct HoverArgs {
     uint8_t* trunc;
     float* tobs;       // [E][D] or null
     const uint8_t* mask;  // reset mask or null
-    int32_t* contact_count;  // device counter of ground-model hits (diagnostics)
+    int32_t* contact_count;  // device counter of ground-model hits (diagnostics) or null
+    uint64_t seed;
+    int64_t env_offset;
+    int E, B, D, autoreset;
 };
 
 template <typename Real>
@@ -90,7 +132,7 @@ __device__ __forceinline__ double clamp100(double x) { return x < -100.0 ? -100.
 // R = rot(b.q) on entry; Rs = rotation of the cached link basis.  On exit R/Rs are the
 // matrices the next sub-step needs.  Returns true if the plane contact model acted.
 template <typename Real, int PH>
-__device__ __forceinline__ bool pyb_substep(const HoverArgs<Real>& a, Body<Real>& b, M3<Real>& R, M3<Real>& Rs,
+__device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real>& b, M3<Real>& R, M3<Real>& Rs,
                                             const Real rpm[4], Real sum_f, V3<Real> P, Real tau_z) {
     constexpr bool GND = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
@@ -179,7 +221,7 @@ __device__ __forceinline__ bool pyb_substep(const HoverArgs<Real>& a, Body<Real>
 
 // Physics.DYN (BaseAviary.py:822-896): explicit model, forward Euler, _integrateQ
 template <typename Real>
-__device__ __forceinline__ void dyn_substep(const HoverArgs<Real>& a, Body<Real>& b, const Real rpm[4]) {
+__device__ __forceinline__ void dyn_substep(const HoverConst<Real>& a, Body<Real>& b, const Real rpm[4]) {
     const M3<Real> R = rot(b.q);
     Real f[4], zt[4], sum = 0;
 #pragma unroll
@@ -223,12 +265,13 @@ __device__ __forceinline__ Real u01r(uint32_t x) {
 
 // BaseAviary.reset -> _housekeeping (+ the optional init_noise extension), Real precision
 template <typename Real>
-__device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& a, int e, Body<Real>& b,
-                                                  int32_t& sc, int32_t& ep) {
-    const uint64_t gid = uint64_t(a.env_offset + e);
-    const U4 r0 = draw(a.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 0);
-    const U4 r1 = draw(a.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 1);
-    const U4 r2 = draw(a.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 2);
+__device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& args, const HoverConst<Real>& C, int e,
+                                                  Body<Real>& b, int32_t& sc, int32_t& ep) {
+    const HoverReset<Real>& a = *args.r;
+    const uint64_t gid = uint64_t(args.env_offset + e);
+    const U4 r0 = draw(args.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 0);
+    const U4 r1 = draw(args.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 1);
+    const U4 r2 = draw(args.seed, gid, uint32_t(ep), TAG_HOVER_RESET, 2);
     const uint32_t w0[4] = {r0.a, r0.b, r0.c, r0.d}, w1[4] = {r1.a, r1.b, r1.c, r1.d},
                    w2[4] = {r2.a, r2.b, r2.c, r2.d};
     Real p[3], e_[3], v[3], om[3];
@@ -245,7 +288,7 @@ __device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& a, int 
     b.pos = v3(p[0], p[1], p[2]);
     b.ql = b.q;
     b.vel = v3(v[0], v[1], v[2]);
-    if (a.physics == ADRP_PHYS_DYN) {
+    if (C.physics == ADRP_PHYS_DYN) {
         b.w = mulT(rot(b.q), v3(om[0], om[1], om[2]));
         b.angv = v3(om[0], om[1], om[2]);
     } else {
@@ -259,7 +302,7 @@ __device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& a, int 
 }
 
 template <typename Real>
-__device__ __forceinline__ V3<Real> hover_obs12(const HoverArgs<Real>& a, const Body<Real>& b, float o[12]) {
+__device__ __forceinline__ V3<Real> hover_obs12(const HoverConst<Real>& a, const Body<Real>& b, float o[12]) {
     const V3<Real> rpy = euler_xyz(b.q);
     const V3<Real> w = a.physics == ADRP_PHYS_DYN ? b.angv : b.w;
     o[0] = float(b.pos.x); o[1] = float(b.pos.y); o[2] = float(b.pos.z);
@@ -357,13 +400,15 @@ __device__ __forceinline__ void store_body(const HoverArgs<Real>& a, int e, cons
 // env.step kernel: lane = env; B (ring length) is a template parameter so the ring lives
 // in registers
 // ------------------------------------------------------------------------------------------
-template <typename Real, int PH, int A, int B>   // B == 0: runtime ring length a.B
-__global__ void __launch_bounds__(256) hover_step_kernel(HoverArgs<Real> a) {
+// B == 0: runtime ring length a.B;  SC > 0: compile-time sub-step count (loop fully unrolled)
+template <typename Real, int PH, int A, int B, int SC>
+__device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const HoverConst<Real>& C) {
     constexpr int BR = B > 0 ? B : 1;
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     constexpr bool DYN = (PH == ADRP_PHYS_DYN);
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    const int E = a.E, D = a.D;
+    const int e = blockIdx.x * kStepBlock + threadIdx.x;
+    const int E = a.E;
+    const int D = B > 0 ? 12 + B * A : a.D;
     if (e >= E) return;
     // ---- issue every load up front: action, the whole ring, ints, state ----
     float act[A];
@@ -387,45 +432,56 @@ __global__ void __launch_bounds__(256) hover_step_kernel(HoverArgs<Real> a) {
     }
     int32_t sc = a.ist[HI_STEP * E + e], ep = a.ist[HI_EPISODE * E + e];
     const int32_t head = a.ist[HI_RING_HEAD * E + e];
-    const bool lag = a.link_lag && !DYN;
+    const bool lag = C.link_lag && !DYN;
     Body<Real> b;
     load_body(a, e, b, lag, DRAG, DYN);
     // ---- _preprocessAction: RPM = HOVER_RPM * (1 + 0.05 a), the gain in float32 (NEP 50) ----
     Real rpm[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rpm[i] = a.hover_rpm * Real(rpm_gain(act[A == 1 ? 0 : i]));
+    for (int i = 0; i < 4; ++i) rpm[i] = C.hover_rpm * Real(rpm_gain(act[A == 1 ? 0 : i]));
     // ---- sub-step loop (BaseAviary.py:347-376) ----
     bool touched = false;
     if constexpr (DYN) {
-        for (int s = 0; s < a.S; ++s) dyn_substep(a, b, rpm);
+        if constexpr (SC > 0) {
+#pragma unroll
+            for (int s = 0; s < SC; ++s) dyn_substep(C, b, rpm);
+        } else {
+            for (int s = 0; s < C.S; ++s) dyn_substep(C, b, rpm);
+        }
     } else {
         Real sum_f = 0, t2 = 0;
         V3<Real> P = v3(Real(0), Real(0), Real(0));
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const Real r2 = rpm[i] * rpm[i];
-            const Real f = r2 * a.kf;
+            const Real f = r2 * C.kf;
             sum_f += f;
-            P = P + v3(f * a.px[i], f * a.py[i], f * a.pz[i]);
+            P = P + v3(f * C.px[i], f * C.py[i], f * C.pz[i]);
             t2 += (i & 1) ? -r2 : r2;
         }
-        const Real tau_z = t2 * a.km;    // KM*(rpm0^2 - rpm1^2 + rpm2^2 - rpm3^2), IROS sign
+        const Real tau_z = t2 * C.km;    // KM*(rpm0^2 - rpm1^2 + rpm2^2 - rpm3^2), IROS sign
         M3<Real> R = rot(b.q);
         M3<Real> Rs = lag ? rot(b.ql) : R;
-        for (int s = 0; s < a.S; ++s) {
-            touched |= pyb_substep<Real, PH>(a, b, R, Rs, rpm, sum_f, P, tau_z);
+        auto substep = [&]() {
+            touched |= pyb_substep<Real, PH>(C, b, R, Rs, rpm, sum_f, P, tau_z);
 #pragma unroll
             for (int i = 0; i < 4; ++i) b.prev_rpm[i] = rpm[i];  // last_clipped_action
+        };
+        if constexpr (SC > 0) {
+#pragma unroll
+            for (int s = 0; s < SC; ++s) substep();
+        } else {
+            for (int s = 0; s < C.S; ++s) substep();
         }
     }
     if (touched && a.contact_count) atomicAdd(a.contact_count, 1);
     // ---- action ring: append this action at `head` (deque.append, BaseRLAviary.py:187) ----
 #pragma unroll
-    for (int p = 0; p < B; ++p)
-        if (p == head) {
+    for (int p = 0; p < B; ++p) {
+        const bool hit = p == head;
 #pragma unroll
-            for (int j = 0; j < A; ++j) ring[p][j] = act[j];
-        }
+        for (int j = 0; j < A; ++j) ring[p][j] = hit ? act[j] : ring[p][j];
+    }
     if constexpr (A == 4)
         reinterpret_cast<float4*>(a.ring)[size_t(head) * E + e] = make_float4(act[0], act[1], act[2], act[3]);
     else
@@ -434,24 +490,24 @@ __global__ void __launch_bounds__(256) hover_step_kernel(HoverArgs<Real> a) {
     const int head1 = head + 1 == B ? 0 : head + 1;
     // ---- obs / reward / terminated / truncated (HoverAviary.py:68-117) ----
     float o12[12];
-    const V3<Real> rpy = hover_obs12(a, b, o12);
-    const Real dx = a.target[0] - b.pos.x, dy = a.target[1] - b.pos.y, dz = a.target[2] - b.pos.z;
+    const V3<Real> rpy = hover_obs12(C, b, o12);
+    const Real dx = C.target[0] - b.pos.x, dy = C.target[1] - b.pos.y, dz = C.target[2] - b.pos.z;
     const Real d2 = dx * dx + dy * dy + dz * dz;
     const Real r = Real(2) - d2 * d2;
     a.rew[e] = float(r > Real(0) ? r : Real(0));
     const bool te = d2 < Real(1e-8);   // |target - pos| < 1e-4
     const bool tr = fabs_(b.pos.x) > Real(1.5) || fabs_(b.pos.y) > Real(1.5) || b.pos.z > Real(2.0) ||
-                    fabs_(rpy.x) > Real(0.4) || fabs_(rpy.y) > Real(0.4) || sc >= a.trunc_steps;
+                    fabs_(rpy.x) > Real(0.4) || fabs_(rpy.y) > Real(0.4) || sc >= C.trunc_steps;
     a.term[e] = te;
     a.trunc[e] = tr;
-    sc += a.S;
+    sc += C.S;
     if (a.autoreset && (te || tr)) {
         if (a.tobs) {
             if constexpr (B > 0) write_row<A, B>(a.tobs + size_t(e) * D, o12, ring, head1);
             else write_row_generic<A>(a.tobs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
         }
-        hover_reset_state(a, e, b, sc, ep);
-        hover_obs12(a, b, o12);
+        hover_reset_state(a, C, e, b, sc, ep);
+        hover_obs12(C, b, o12);
     }
     if constexpr (B > 0) write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
     else write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
@@ -461,23 +517,58 @@ __global__ void __launch_bounds__(256) hover_step_kernel(HoverArgs<Real> a) {
     a.ist[HI_RING_HEAD * E + e] = head1;
 }
 
+// Arguments the step needs at wave start are separate scalars so the CP preloads them into
+// SGPRs (-amdgpu-kernarg-preload-count); the rest (used at the end) is one aggregate.
+template <typename Real>
+struct HoverTail {
+    const HoverConst<Real>* c;
+    const HoverReset<Real>* r;
+    uint8_t* term;
+    uint8_t* trunc;
+    float* tobs;
+    int32_t* contact_count;
+    uint64_t seed;
+    int64_t env_offset;
+    int B, D, autoreset;
+};
+
+// DEF: compiled-in cf2x_consts (the reference default) instead of the device block.
+// Launch with kStepBlock threads per workgroup.
+template <typename Real, int PH, int A, int B, bool DEF>
+__global__ void __launch_bounds__(256) hover_step_kernel(Real* f, float* ring, int32_t* ist, const float* act,
+                                                         float* obs, float* rew, int E, HoverTail<Real> t) {
+    HoverArgs<Real> a;
+    a.c = t.c; a.r = t.r;
+    a.f = f; a.ring = ring; a.ist = ist; a.act = act; a.obs = obs; a.rew = rew;
+    a.term = t.term; a.trunc = t.trunc; a.tobs = t.tobs; a.mask = nullptr; a.contact_count = t.contact_count;
+    a.seed = t.seed; a.env_offset = t.env_offset;
+    a.E = E; a.B = t.B; a.D = t.D; a.autoreset = t.autoreset;
+    if constexpr (DEF) {
+        constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
+        hover_step_body<Real, PH, A, B, C.S>(a, C);
+    } else {
+        hover_step_body<Real, PH, A, B, 0>(a, *a.c);
+    }
+}
+
 // reset kernel (BaseAviary.reset -> _housekeeping -> _computeObs); ring is NOT cleared (Q21)
 template <typename Real, int A>
 __global__ void __launch_bounds__(256) hover_reset_kernel(HoverArgs<Real> a) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.E || (a.mask && !a.mask[e])) return;
+    const HoverConst<Real>& C = *a.c;
     const int E = a.E;
-    const bool dyn = a.physics == ADRP_PHYS_DYN;
-    const bool drag = a.physics == ADRP_PHYS_PYB_DRAG || a.physics == ADRP_PHYS_PYB_GND_DRAG_DW;
+    const bool dyn = C.physics == ADRP_PHYS_DYN;
+    const bool drag = C.physics == ADRP_PHYS_PYB_DRAG || C.physics == ADRP_PHYS_PYB_GND_DRAG_DW;
     Body<Real> b;
     int32_t sc = a.ist[HI_STEP * E + e], ep = a.ist[HI_EPISODE * E + e];
     const int head = a.ist[HI_RING_HEAD * E + e];
-    hover_reset_state(a, e, b, sc, ep);
-    store_body(a, e, b, a.link_lag && !dyn, drag, dyn);
+    hover_reset_state(a, C, e, b, sc, ep);
+    store_body(a, e, b, C.link_lag && !dyn, drag, dyn);
     a.ist[HI_STEP * E + e] = sc;
     a.ist[HI_EPISODE * E + e] = ep;
     float o12[12];
-    hover_obs12(a, b, o12);
+    hover_obs12(C, b, o12);
     const float none[A] = {};
     write_row_generic<A>(a.obs + size_t(e) * a.D, o12, a.ring, a.B, E, e, head, none, false);
 }

@@ -185,6 +185,12 @@ const char* adrp_state_field(const adrp_t* h, int is_int, int index);
 int adrp_get_state(adrp_t* h, void* f_dev, int32_t* i_dev, void* stream);
 int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev, void* stream);
 
+/* Name of the step-kernel instantiation a config selects (no device needed), e.g.
+ * "hover_step<f32,PYB,A4,B15,cf2x>": "cf2x" = per-config constants compiled in (the
+ * reference default drone at 240/30 Hz, chosen only when the config's derived constants
+ * are bit-identical), "generic" = read from the handle's device-resident block. */
+const char* adrp_kernel_name(const adrp_config* cfg);
+
 /* Algorithmic HBM bytes one adrp_step moves (roofline accounting). */
 int64_t adrp_step_bytes(const adrp_t* h);
 

@@ -79,3 +79,26 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 text = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.sub(r"#.*|//.*", "", text).replace("oracle/", ""), f
+
+
+def test_kernel_variant_selection(lib):
+    """the compiled-constant kernel is chosen for the reference default drone only"""
+    from gym_pybullet_adrp_amd import _lib
+    cfg = _lib.default_config(abi.TASK_HOVER)
+    assert _lib.kernel_name(cfg) == "hover_step<f32,PYB,A4,B15,cf2x>"
+    for ph, name in ((1, "DYN"), (5, "PYB_GND_DRAG_DW")):
+        c = cfg.copy()
+        c.physics = ph
+        assert _lib.kernel_name(c) == f"hover_step<f32,{name},A4,B15,cf2x>"
+    c = cfg.copy()
+    c.precision = 1
+    assert _lib.kernel_name(c).endswith(",cf2x>") and "f64" in _lib.kernel_name(c)
+    c = cfg.copy()
+    c.init_xyz_noise[0] = 0.3                 # reset distribution is not part of the constants
+    assert _lib.kernel_name(c).endswith(",cf2x>")
+    for mutate in (lambda c: setattr(c.drone, "m", 0.027), lambda c: c.target_pos.__setitem__(2, 1.5),
+                   lambda c: setattr(c, "pyb_freq", 480), lambda c: setattr(c, "episode_len_sec", 5.0),
+                   lambda c: setattr(c, "link_frame_lag", 0)):
+        c = cfg.copy()
+        mutate(c)
+        assert _lib.kernel_name(c).endswith(",generic>"), _lib.kernel_name(c)
