@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--precision", default="fp32")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-allgather", action="store_true", help="N>1: skip the obs all-gather variant")
     return p.parse_args()
 
 
@@ -78,13 +79,22 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
+    import functools
+    from gym_pybullet_adrp_amd import _lib
     from gym_pybullet_adrp_amd.envs.hover import HoverAviary
     from gym_pybullet_adrp_amd.utils.enums import Physics
 
     E = args.envs
-    env = HoverAviary(physics=Physics[args.physics], num_envs=E, device=local, precision=args.precision,
-                      seed=2024, env_offset=rank * E, initial_xyzs=[0, 0, 1.0],
-                      init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1})
+    make = functools.partial(HoverAviary, physics=Physics[args.physics], device=local, precision=args.precision,
+                             seed=2024, initial_xyzs=[0, 0, 1.0],
+                             init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1})
+    sharded = None
+    if world > 1:
+        from gym_pybullet_adrp_amd.sharding import ShardedAviary
+        sharded = ShardedAviary(E * world, make)     # rank r owns global envs [r*E, (r+1)*E)
+        env = sharded.env
+    else:
+        env = make(num_envs=E, env_offset=0)
     dev = env.device
     env.reset()
     gen = torch.Generator(device=dev)
@@ -144,6 +154,26 @@ def main():
     eager = {"env_steps_per_s_per_gpu": E * ne / (time.perf_counter() - te0),
              "ms_per_step": (time.perf_counter() - te0) / ne * 1e3}
 
+    # ---- config 5 variant (N > 1): every step followed by the RCCL all-gather that
+    # reassembles obs/reward/flags for a learner (eager; not part of `value`) ----
+    allgather = None
+    if sharded is not None and not args.no_allgather:
+        ng = min(K, 500)
+        for k in range(10):
+            sharded.gather(*env.step(acts[k % nbuf])[:4])
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg0 = time.perf_counter()
+        for k in range(ng):
+            sharded.gather(*env.step(acts[k % nbuf])[:4])
+        torch.cuda.synchronize()
+        tg = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+        tg = float(tg.item())
+        allgather = {"value": E * world * ng / tg, "unit": "env-steps/s", "ms_per_step": tg / ng * 1e3,
+                     "steps": ng, "collective": "all_gather_into_tensor (RCCL) of packed fp32 obs+reward+flags",
+                     "bytes_per_rank_per_step": E * (env.h.D + 3) * 4}
+
     bytes_per_launch = env.step_bytes()
     achieved = bytes_per_launch / kern_avg_s / 1e9
     traffic = None
@@ -176,7 +206,10 @@ def main():
                      "kernel_us_median": float(np.median(kern_ms)) * 1e3, "timed_launches": int(len(kern_ms))},
         "timing": {"timed_region": f"{K // G} replays of a {G}-step HIP graph (one fused launch per env.step)",
                    "eager": eager},
+        "kernel": _lib.kernel_name(env.cfg),
     }
+    if allgather is not None:
+        result["with_obs_allgather"] = allgather
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(env.cfg, args.cpu_seconds)
     elif rank == 0:

@@ -1,18 +1,52 @@
-"""Summarise rocprofv3 --pmc CSVs: mean per-dispatch counter of the hover step kernel."""
+"""Summarise rocprofv3 --pmc passes of the HoverAviary step kernel into per-launch HBM bytes.
+
+usage: python tools/pmc_summary.py OUT.json KEY FETCH_DIR WRITE_DIR [KEY FETCH_DIR WRITE_DIR ...]
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
+FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is
+taken as is.  The first 8 dispatches (cold caches, first-touch) are skipped; the median of
+the rest is reported.
+"""
 import csv
 import glob
 import json
+import statistics
 import sys
 
-out = {}
-for path in sys.argv[1:]:
-    for f in glob.glob(path + "/**/*counter_collection.csv", recursive=True):
-        rows = list(csv.DictReader(open(f)))
-        for r in rows:
-            if "hover_step_kernel" not in r.get("Kernel_Name", ""):
-                continue
-            key = (f.split("/")[-3] if "/" in f else f, r["Counter_Name"])
-            out.setdefault(key, []).append(float(r["Counter_Value"]))
-res = {f"{k[0]}:{k[1]}": {"dispatches": len(v), "mean": sum(v) / len(v), "min": min(v), "max": max(v)}
-       for k, v in out.items()}
-print(json.dumps(res, indent=1))
+
+def counter(d, name):
+    vals = []
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "hover_step_kernel" in r.get("Kernel_Name", "") and r["Counter_Name"] == name:
+                vals.append((int(r.get("Dispatch_Id", len(vals))), float(r["Counter_Value"])))
+    vals = [v for _, v in sorted(vals)]
+    steady = vals[8:] if len(vals) > 16 else vals
+    if not steady:
+        raise SystemExit(f"no {name} rows for hover_step_kernel under {d}")
+    return statistics.median(steady), len(vals)
+
+
+def main():
+    out_path, rest = sys.argv[1], sys.argv[2:]
+    try:
+        rec = json.load(open(out_path))
+    except (OSError, ValueError):
+        rec = {}
+    for i in range(0, len(rest), 3):
+        key, fdir, wdir = rest[i:i + 3]
+        fetch_kib, nf = counter(fdir, "FETCH_SIZE")
+        write_kib, nw = counter(wdir, "WRITE_SIZE")
+        rd = fetch_kib * 1024 * 2
+        wr = write_kib * 1024
+        rec[key] = {"hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
+                    "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib,
+                    "dispatches": [nf, nw],
+                    "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes; FETCH_SIZE x2 "
+                              "(gfx950 correction), median over dispatches after the first 8"}
+        print(key, json.dumps(rec[key]))
+    json.dump(rec, open(out_path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
