@@ -16,6 +16,7 @@
 
 #include "../../include/adrp.h"
 #include "hover_kernel.h"
+#include "race_kernel.h"
 
 using namespace adrp;
 
@@ -126,13 +127,15 @@ static void derived(const adrp_config& c, double* hover_rpm, double* gnd_clip) {
     *gnd_clip = 0.25 * d.prop_radius * sqrt((15 * maxr * maxr * d.kf * d.gnd_eff_coeff) / maxt);
 }
 
-static int trunc_steps(const adrp_config& c) {
-    // truncated when step_counter / PYB_FREQ > EPISODE_LEN_SEC in float64 (HoverAviary.py:114)
-    long long t = (long long)floor(c.episode_len_sec * c.pyb_freq) - 2;
+static int trunc_steps(double episode_len_sec, int pyb_freq) {
+    // truncated when step_counter / PYB_FREQ > EPISODE_LEN_SEC in float64 (HoverAviary.py:114,
+    // MultiRaceAviary.py:709): the smallest such step_counter
+    long long t = (long long)floor(episode_len_sec * pyb_freq) - 2;
     if (t < 0) t = 0;
-    while (!((double)t / (double)c.pyb_freq > c.episode_len_sec)) ++t;
+    while (!((double)t / (double)pyb_freq > episode_len_sec)) ++t;
     return (int)t;
 }
+static int trunc_steps(const adrp_config& c) { return trunc_steps(c.episode_len_sec, c.pyb_freq); }
 
 template <typename Real>
 static HoverConst<Real> hover_const(const adrp_config& c) {
@@ -221,11 +224,93 @@ static int upload_const(adrp_t* h) {
     return ADRP_OK;
 }
 
+template <typename Real>
+static RaceConst<Real> race_const(const adrp_config& c) {
+    const adrp_drone_params& d = c.drone;
+    const adrp_track& t = c.track;
+    RaceConst<Real> k;
+    memset(&k, 0, sizeof k);
+    k.N = c.num_drones;
+    k.S = c.pyb_freq / c.ctrl_freq;
+    k.physics = c.physics;
+    k.link_lag = c.link_frame_lag ? 1 : 0;
+    k.compete = c.race_mode == ADRP_RACE_COMPETE;
+    k.num_gates = t.num_gates;
+    k.num_obstacles = t.num_obstacles;
+    k.trunc_steps = trunc_steps(t.episode_len_sec, c.pyb_freq);
+    k.disturbances = t.disturbances ? 1 : 0;
+    k.reward_wrapper = t.reward_wrapper ? 1 : 0;
+    k.random_gates = t.random_gates_obstacles ? 1 : 0;
+    k.random_state = t.random_drone_state ? 1 : 0;
+    k.random_inertia = t.random_drone_inertia ? 1 : 0;
+    k.D = 49 + (k.compete ? 6 * (c.num_drones - 1) : 0);
+    k.autoreset = c.autoreset ? 1 : 0;
+    k.dt = Real(1.0 / c.pyb_freq);
+    k.gravity = Real(c.gravity);
+    k.kf = Real(d.kf); k.km = Real(d.km);
+    for (int i = 0; i < 4; ++i) {
+        k.px[i] = Real(d.prop_pos[i][0]); k.py[i] = Real(d.prop_pos[i][1]); k.pz[i] = Real(d.prop_pos[i][2]);
+    }
+    double hover_rpm, gnd_clip;
+    derived(c, &hover_rpm, &gnd_clip);
+    k.gnd_kf = Real(d.kf * d.gnd_eff_coeff);
+    k.prop_r4 = Real(d.prop_radius / 4);
+    k.gnd_clip = Real(gnd_clip);
+    for (int i = 0; i < 3; ++i) k.drag[i] = Real(d.drag_coeff[i]);
+    k.dw1 = Real(d.dw_coeff[0]); k.dw2 = Real(d.dw_coeff[1]); k.dw3 = Real(d.dw_coeff[2]);
+    k.prop_r = Real(d.prop_radius);
+    k.dyn_mass = Real(d.m); k.dyn_inv_mass = Real(1.0 / d.m);
+    k.dyn_i[0] = Real(d.ixx); k.dyn_i[1] = Real(d.iyy); k.dyn_i[2] = Real(d.izz);
+    k.dyn_inv_i[0] = Real(1.0 / d.ixx); k.dyn_inv_i[1] = Real(1.0 / d.iyy); k.dyn_inv_i[2] = Real(1.0 / d.izz);
+    k.dyn_arm = Real(d.l / sqrt(2.0));
+    k.coll_hh = Real(0.5 * d.collision_h); k.coll_r = Real(d.collision_r); k.coll_zoff = Real(d.collision_z_offset);
+    k.ang_max = Real(0.5 * (M_PI / 2) * c.pyb_freq);
+    for (int g = 0; g < ADRP_MAX_GATES; ++g) {
+        k.gate_nom[g][0] = Real(t.gates[g][0]); k.gate_nom[g][1] = Real(t.gates[g][1]);
+        k.gate_nom[g][2] = Real(t.gates[g][2]); k.gate_nom[g][3] = Real(t.gates[g][5]);
+        k.gate_type[g] = t.gates[g][6] > 0 ? 1 : 0;
+    }
+    for (int o = 0; o < ADRP_MAX_OBSTACLES; ++o)
+        for (int j = 0; j < 3; ++j) k.obst_nom[o][j] = Real(t.obstacles[o][j]);
+    for (int j = 0; j < 3; ++j) {
+        k.bounds[j] = Real(t.bounds_hi[j]);
+        k.dist_lo[j] = Real(t.dyn_dist_low[j]); k.dist_hi[j] = Real(t.dyn_dist_high[j]);
+        for (int m = 0; m < 2; ++m) { k.pos_off[j][m] = Real(t.pos_offset_range[j][m]); k.rot_off[j][m] = Real(t.rot_offset_range[j][m]); }
+    }
+    k.noise_std = Real(t.action_noise_std);
+    for (int m = 0; m < 2; ++m) { k.gate_off[m] = Real(t.gate_offset_range[m]); k.obst_off[m] = Real(t.obstacle_offset_range[m]); }
+    for (int j = 0; j < 4; ++j)
+        for (int m = 0; m < 2; ++m) k.inertia_off[j][m] = Real(t.inertia_offset_range[j][m]);
+    for (int i = 0; i < ADRP_MAX_DRONES; ++i)
+        for (int j = 0; j < 3; ++j) {
+            k.init_pos[i][j] = Real(t.init_pos[i][j]); k.init_rpy[i][j] = Real(t.init_rpy[i][j]);
+            k.init_vel[i][j] = Real(t.init_vel[i][j]); k.init_pqr[i][j] = Real(t.init_pqr[i][j]);
+        }
+    k.race_mass = Real(t.race_mass);
+    for (int j = 0; j < 3; ++j) k.race_inertia[j] = Real(t.race_inertia[j]);
+    return k;
+}
+
+template <typename Real>
+static int upload_race_const(adrp_t* h) {
+    const RaceConst<Real> k = race_const<Real>(h->cfg);
+    if (hipMalloc(&h->cblk, sizeof k) != hipSuccess) return ADRP_ERR_OOM;
+    if (hipMemcpy(h->cblk, &k, sizeof k, hipMemcpyHostToDevice) != hipSuccess) return ADRP_ERR_DEVICE;
+    return ADRP_OK;
+}
+
+static int race_group(int n) { return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : 8; }
+
 extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
     static thread_local char buf[96];
     if (!cfg || cfg->struct_size != sizeof(adrp_config)) return nullptr;
     static const char* ph[] = {"PYB", "DYN", "PYB_GND", "PYB_DRAG", "PYB_DW", "PYB_GND_DRAG_DW"};
     const int p = cfg->physics >= 0 && cfg->physics <= 5 ? cfg->physics : 0;
+    if (cfg->task == ADRP_TASK_RACE) {
+        snprintf(buf, sizeof buf, "race_step<%s,%s,G%d>", cfg->precision ? "f64" : "f32", ph[p],
+                 race_group(cfg->num_drones));
+        return buf;
+    }
     const int A = cfg->act_type == ADRP_ACT_ONE_D_RPM ? 1 : 4;
     snprintf(buf, sizeof buf, "hover_step<%s,%s,A%d,B%s,%s>", cfg->precision ? "f64" : "f32", ph[p], A,
              cfg->action_buffer_size == 15 ? "15" : "n", config_is_cf2x(*cfg) ? "cf2x" : "generic");
@@ -252,7 +337,15 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
         if (c.action_buffer_size <= 0 || c.action_buffer_size > 4096)
             return seterr(nullptr, ADRP_ERR_INVALID, "action_buffer_size");
     } else if (c.task == ADRP_TASK_RACE) {
-        return seterr(nullptr, ADRP_ERR_INVALID, "ADRP_TASK_RACE is not built yet in this library version");
+        if (c.num_drones < 1 || c.num_drones > ADRP_MAX_DRONES)
+            return seterr(nullptr, ADRP_ERR_INVALID, "MultiRaceAviary num_drones must be 1..8");
+        if (c.act_type != ADRP_ACT_FULLSTATE)
+            return seterr(nullptr, ADRP_ERR_INVALID, "MultiRaceAviary act_type must be FULLSTATE");
+        if (c.race_mode != ADRP_RACE_COMPARE && c.race_mode != ADRP_RACE_COMPETE)
+            return seterr(nullptr, ADRP_ERR_INVALID, "race_mode");
+        if (c.track.num_gates < 0 || c.track.num_gates > ADRP_MAX_GATES || c.track.num_obstacles < 0 ||
+            c.track.num_obstacles > ADRP_MAX_OBSTACLES)
+            return seterr(nullptr, ADRP_ERR_INVALID, "track: at most 4 gates and 4 obstacles (MultiRaceAviary.py:591-651)");
     } else {
         return seterr(nullptr, ADRP_ERR_INVALID, "unknown task");
     }
@@ -264,12 +357,13 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     h->cfg = c;
     h->device = device;
     h->E = c.num_envs; h->N = c.num_drones;
+    const bool race = c.task == ADRP_TASK_RACE;
     h->A = c.act_type == ADRP_ACT_ONE_D_RPM ? 1 : 4;
-    h->B = c.action_buffer_size;
-    h->D = 12 + h->B * h->A;
+    h->B = race ? 0 : c.action_buffer_size;
+    h->D = race ? 49 + (c.race_mode == ADRP_RACE_COMPETE ? 6 * (c.num_drones - 1) : 0) : 12 + h->B * h->A;
     h->S = c.pyb_freq / c.ctrl_freq;
-    h->nf_base = HF_NBASE;
-    h->ni = HI_N;
+    h->nf_base = race ? RF_N : HF_NBASE;
+    h->ni = race ? RI_N : HI_N;
     h->real_size = c.precision ? 8 : 4;
     const size_t EN = size_t(h->E) * h->N;
     auto cleanup = [&](int rc) {
@@ -279,17 +373,19 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
         return rc;
     };
     if (hipSetDevice(device) != hipSuccess) return cleanup(seterr(h, ADRP_ERR_DEVICE, "hipSetDevice failed"));
+    const size_t ring_bytes = size_t(h->B) * h->A * h->E * sizeof(float);
     if (hipMalloc(&h->f, h->nf_base * EN * h->real_size) != hipSuccess ||
-        hipMalloc((void**)&h->ring, size_t(h->B) * h->A * h->E * sizeof(float)) != hipSuccess ||
+        (ring_bytes && hipMalloc((void**)&h->ring, ring_bytes) != hipSuccess) ||
         hipMalloc((void**)&h->ist, h->ni * EN * sizeof(int32_t)) != hipSuccess ||
         hipMalloc((void**)&h->counters, 64 * sizeof(int32_t)) != hipSuccess)
         return cleanup(seterr(h, ADRP_ERR_OOM, "hipMalloc failed"));
     if (hipMemset(h->f, 0, h->nf_base * EN * h->real_size) != hipSuccess ||
-        hipMemset(h->ring, 0, size_t(h->B) * h->A * h->E * sizeof(float)) != hipSuccess ||
+        (ring_bytes && hipMemset(h->ring, 0, ring_bytes) != hipSuccess) ||
         hipMemset(h->ist, 0, h->ni * EN * sizeof(int32_t)) != hipSuccess ||
         hipMemset(h->counters, 0, 64 * sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return cleanup(seterr(h, ADRP_ERR_DEVICE, "initialisation failed"));
-    const int rc = h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h);
+    const int rc = race ? (h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h))
+                        : (h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h));
     if (rc != ADRP_OK) return cleanup(seterr(h, rc, "constant block upload failed"));
     *out = h;
     return ADRP_OK;
@@ -375,10 +471,73 @@ static int hover_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s
     return ADRP_OK;
 }
 
+template <typename Real>
+static RaceArgs<Real> race_args(const adrp_t* h) {
+    RaceArgs<Real> a;
+    memset(&a, 0, sizeof a);
+    a.c = (const RaceConst<Real>*)h->cblk;
+    a.f = (Real*)h->f;
+    a.ist = h->ist;
+    a.seed = h->cfg.seed;
+    a.env_offset = h->cfg.env_offset;
+    a.E = h->E;
+    return a;
+}
+
+template <typename Real, int PH>
+static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
+    const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G + kRaceBlock - 1) / kRaceBlock));
+    auto go = [&](auto kernel) {
+        if (h->prof_n < h->prof_cap) {
+            hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
+            ++h->prof_n;
+        } else {
+            hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
+        }
+    };
+    switch (G) {
+        case 1: go(race_step_kernel<Real, PH, 1>); break;
+        case 2: go(race_step_kernel<Real, PH, 2>); break;
+        case 4: go(race_step_kernel<Real, PH, 4>); break;
+        default: go(race_step_kernel<Real, PH, 8>); break;
+    }
+}
+
+template <typename Real>
+static int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                     float* tobs, hipStream_t s) {
+    RaceArgs<Real> a = race_args<Real>(h);
+    a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
+    const int G = race_group(h->N);
+    switch (h->cfg.physics) {
+        case ADRP_PHYS_PYB: launch_race_g<Real, ADRP_PHYS_PYB>(a, G, s, h); break;
+        case ADRP_PHYS_DYN: launch_race_g<Real, ADRP_PHYS_DYN>(a, G, s, h); break;
+        case ADRP_PHYS_PYB_GND: launch_race_g<Real, ADRP_PHYS_PYB_GND>(a, G, s, h); break;
+        case ADRP_PHYS_PYB_DRAG: launch_race_g<Real, ADRP_PHYS_PYB_DRAG>(a, G, s, h); break;
+        case ADRP_PHYS_PYB_DW: launch_race_g<Real, ADRP_PHYS_PYB_DW>(a, G, s, h); break;
+        default: launch_race_g<Real, ADRP_PHYS_PYB_GND_DRAG_DW>(a, G, s, h); break;
+    }
+    HIPCHK(h, hipGetLastError());
+    return ADRP_OK;
+}
+
+template <typename Real>
+static int race_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s) {
+    RaceArgs<Real> a = race_args<Real>(h);
+    a.mask = mask; a.obs = obs;
+    const dim3 grid((unsigned)((size_t(h->E) * h->N + kRaceBlock - 1) / kRaceBlock));
+    hipLaunchKernelGGL((race_reset_kernel<Real>), grid, dim3(kRaceBlock), 0, s, a);
+    HIPCHK(h, hipGetLastError());
+    return ADRP_OK;
+}
+
 extern "C" int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev, void* stream) {
     if (!h || !obs_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_reset: NULL argument");
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
+    if (h->cfg.task == ADRP_TASK_RACE)
+        return h->real_size == 8 ? race_reset<double>(h, env_mask_dev, obs_dev, s)
+                                 : race_reset<float>(h, env_mask_dev, obs_dev, s);
     return h->real_size == 8 ? hover_reset<double>(h, env_mask_dev, obs_dev, s)
                              : hover_reset<float>(h, env_mask_dev, obs_dev, s);
 }
@@ -389,6 +548,9 @@ extern "C" int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float*
         return seterr(h, ADRP_ERR_INVALID, "adrp_step: NULL argument");
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
+    if (h->cfg.task == ADRP_TASK_RACE)
+        return h->real_size == 8 ? race_step<double>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s)
+                                 : race_step<float>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s);
     return h->real_size == 8 ? hover_step<double>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s)
                              : hover_step<float>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s);
 }
@@ -409,9 +571,34 @@ extern "C" int adrp_state_layout(const adrp_t* h, int* nf, int* ni) {
     return ADRP_OK;
 }
 
+static const char* k_race_f[64] = {
+    "pos_x", "pos_y", "pos_z", "quat_x", "quat_y", "quat_z", "quat_w", "vel_x", "vel_y", "vel_z",
+    "omega_x", "omega_y", "omega_z", "rpm_0", "rpm_1", "rpm_2", "rpm_3", "prev_rpm_0", "prev_rpm_1",
+    "prev_rpm_2", "prev_rpm_3", "angv_x", "angv_y", "angv_z", "link_quat_x", "link_quat_y", "link_quat_z",
+    "link_quat_w", "link_pos_x", "link_pos_y", "link_pos_z", "kin_pos_x", "kin_pos_y", "kin_pos_z",
+    "prev_rpy_0", "prev_rpy_1", "prev_rpy_2", "prev_vel_0", "prev_vel_1", "prev_vel_2",
+    "lpf_d1_0", "lpf_d1_1", "lpf_d1_2", "lpf_d2_0", "lpf_d2_1", "lpf_d2_2",
+    "i_err_0", "i_err_1", "i_err_2", "i_err_m_0", "i_err_m_1", "i_err_m_2",
+    "prev_omega_roll", "prev_omega_pitch", "prev_sp_roll", "prev_sp_pitch",
+    "ctl_roll", "ctl_pitch", "ctl_yaw", "ctl_thrust", "mass", "ixx", "iyy", "izz"};
+static const char* k_race_i[RI_N] = {"step_counter", "episode", "tick", "last_att_tick", "last_pos_tick",
+                                     "tumble", "gate", "flags", "wr_gate"};
+
 extern "C" const char* adrp_state_field(const adrp_t* h, int is_int, int index) {
     static thread_local char buf[32];
     if (!h || index < 0) return nullptr;
+    if (h->cfg.task == ADRP_TASK_RACE) {
+        if (is_int) return index < RI_N ? k_race_i[index] : nullptr;
+        if (index < 64) return k_race_f[index];
+        static const char* gc[4] = {"x", "y", "z", "yaw"};
+        static const char* oc[3] = {"x", "y", "z"};
+        if (index < 80) snprintf(buf, sizeof buf, "gate_%d_%s", (index - 64) / 4, gc[(index - 64) % 4]);
+        else if (index < 92) snprintf(buf, sizeof buf, "obst_%d_%s", (index - 80) / 3, oc[(index - 80) % 3]);
+        else if (index < 95) snprintf(buf, sizeof buf, "wr_target_%d", index - 92);
+        else if (index < RF_N) snprintf(buf, sizeof buf, "wr_prev_%d", index - 95);
+        else return nullptr;
+        return buf;
+    }
     if (is_int) return index < h->ni ? k_hover_i[index] : nullptr;
     if (index < h->nf_base) return k_hover_f[index];
     const int k = index - h->nf_base;
@@ -427,7 +614,7 @@ extern "C" int adrp_get_state(adrp_t* h, void* f_dev, int32_t* i_dev, void* stre
     const size_t EN = size_t(h->E) * h->N, nb = h->nf_base * EN, nr = size_t(h->B) * h->A * h->E;
     HIPCHK(h, hipMemcpyAsync(f_dev, h->f, nb * h->real_size, hipMemcpyDeviceToDevice, s));
     void* ring_dst = (char*)f_dev + nb * h->real_size;
-    hipLaunchKernelGGL(ring_get_kernel, dim3((h->E + 255) / 256), dim3(256), 0, s, h->ring, ring_dst,
+    if (h->B > 0) hipLaunchKernelGGL(ring_get_kernel, dim3((h->E + 255) / 256), dim3(256), 0, s, h->ring, ring_dst,
                        int(h->real_size == 8), h->B, h->A, h->E);
     HIPCHK(h, hipGetLastError());
     (void)nr;
@@ -442,7 +629,7 @@ extern "C" int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev
     const size_t EN = size_t(h->E) * h->N, nb = h->nf_base * EN, nr = size_t(h->B) * h->A * h->E;
     HIPCHK(h, hipMemcpyAsync(h->f, f_dev, nb * h->real_size, hipMemcpyDeviceToDevice, s));
     const void* ring_src = (const char*)f_dev + nb * h->real_size;
-    hipLaunchKernelGGL(ring_set_kernel, dim3((h->E + 255) / 256), dim3(256), 0, s, h->ring, ring_src,
+    if (h->B > 0) hipLaunchKernelGGL(ring_set_kernel, dim3((h->E + 255) / 256), dim3(256), 0, s, h->ring, ring_src,
                        int(h->real_size == 8), h->B, h->A, h->E);
     HIPCHK(h, hipGetLastError());
     (void)nr;
@@ -455,6 +642,15 @@ extern "C" int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev
 // ---------------------------------------------------------------------------------------------
 extern "C" int64_t adrp_step_bytes(const adrp_t* h) {
     if (!h) return ADRP_ERR_INVALID;
+    if (h->cfg.task == ADRP_TASK_RACE) {
+        // per drone: 64 state fields read + 60 written (mass/inertia are read-only), the env's
+        // 28 track fields read, 9 ints read + 7 written, the FULLSTATE action, the obs row;
+        // per env: reward + 2 flags (+ RewardWrapper: 6 fields r/w, 1 int)
+        const int64_t rs = int64_t(h->real_size);
+        const int64_t per_drone = (64 + 60 + 28) * rs + (9 + 7) * 4 + 16 + int64_t(h->D) * 4;
+        const int64_t per_env = 6 + (h->cfg.track.reward_wrapper ? 12 * rs + 4 : 0);
+        return (per_drone * h->N + per_env) * h->E;
+    }
     const int ph = h->cfg.physics;
     const bool dyn = ph == ADRP_PHYS_DYN;
     const bool drag = ph == ADRP_PHYS_PYB_DRAG || ph == ADRP_PHYS_PYB_GND_DRAG_DW;

@@ -1,0 +1,1093 @@
+// race_kernel.h — MultiRaceAviary env.step as one fused launch (gfx950).
+//
+// One lane per drone: lane = env * G + drone, G = next power of two >= N, so the drones of
+// an env sit in G adjacent lanes of one wave and exchange poses with __shfl (ds_bpermute,
+// no LDS allocation): downwash every sub-step; rays, COMPETE obs/contacts and the
+// per-env termination reduction once per env.step.  Per lane and env.step:
+//   S x [ forces (motor, ground effect, drag, downwash, level1-3 disturbance) -> Bullet
+//         floating-base step -> MellingerControl wrapper + firmware controllerMellinger +
+//         PWM chain (500 Hz) ]
+//   -> _gate_progress rays -> _computeObs (GJK range tests) -> elimination / terminated /
+//   truncated -> RewardWrapper -> auto-reset.
+// Reference: envs/MultiRaceAviary.py:171-270 (see oracle/race.c for the line-by-line map).
+#pragma once
+
+#include "../../include/adrp.h"
+#include "adrp_device.h"
+
+namespace adrp {
+
+constexpr uint32_t TAG_RACE_TRACK = 0x52540000u;
+constexpr uint32_t TAG_RACE_DRONE = 0x52440000u;
+constexpr uint32_t TAG_RACE_NOISE = 0x524e0000u;
+constexpr uint32_t TAG_RACE_DIST = 0x52460000u;
+constexpr int kRaceBlock = 64;
+
+// per-drone SoA fields ([field][E*N]); env fields are replicated in every drone slot
+enum RaceField {
+    RF_POS = 0, RF_QUAT = 3, RF_VEL = 7, RF_OMEGA = 10, RF_RPM = 13, RF_PREV_RPM = 17, RF_ANGV = 21,
+    RF_LINK_QUAT = 24, RF_LINK_POS = 28, RF_KIN_POS = 31, RF_PREV_RPY = 34, RF_PREV_VEL = 37,
+    RF_LPF_D1 = 40, RF_LPF_D2 = 43, RF_I_ERR = 46, RF_I_ERR_M = 49, RF_PREV_OMEGA_ROLL = 52,
+    RF_PREV_OMEGA_PITCH = 53, RF_PREV_SP_ROLL = 54, RF_PREV_SP_PITCH = 55, RF_CTL = 56, RF_MASS = 60,
+    RF_INERTIA = 61, RF_GATE = 64, RF_OBST = 80, RF_WR_TARGET = 92, RF_WR_PREV = 95, RF_N = 98
+};
+enum RaceInt { RI_STEP = 0, RI_EPISODE, RI_TICK, RI_LAST_ATT, RI_LAST_POS, RI_TUMBLE, RI_GATE, RI_FLAGS, RI_WR_GATE, RI_N };
+
+template <typename Real>
+struct RaceConst {
+    int N, S, physics, link_lag, compete, num_gates, num_obstacles, trunc_steps;
+    int disturbances, reward_wrapper, random_gates, random_state, random_inertia, D, autoreset;
+    Real dt, gravity, kf, km, hover_unused;
+    Real px[4], py[4], pz[4];
+    Real gnd_kf, prop_r4, gnd_clip, drag[3], dw1, dw2, dw3, prop_r;
+    Real dyn_mass, dyn_inv_mass, dyn_i[3], dyn_inv_i[3], dyn_arm;   // Physics.DYN uses the IROS URDF M, J
+    Real coll_hh, coll_r, coll_zoff, ang_max;
+    Real gate_nom[ADRP_MAX_GATES][4];
+    int gate_type[ADRP_MAX_GATES];
+    Real obst_nom[ADRP_MAX_OBSTACLES][3];
+    Real bounds[3];
+    Real noise_std, dist_lo[3], dist_hi[3];
+    Real gate_off[2], obst_off[2], pos_off[3][2], rot_off[3][2], inertia_off[4][2];
+    Real init_pos[ADRP_MAX_DRONES][3], init_rpy[ADRP_MAX_DRONES][3], init_vel[ADRP_MAX_DRONES][3],
+        init_pqr[ADRP_MAX_DRONES][3];
+    Real race_mass, race_inertia[3];
+};
+
+template <typename Real>
+struct RaceArgs {
+    const RaceConst<Real>* c;
+    Real* f;             // [RF_N][E*N]
+    int32_t* ist;        // [RI_N][E*N]
+    const float* act;    // [E][N][4]
+    float* obs;          // [E][N][D]
+    float* rew;          // [E]
+    uint8_t* term;
+    uint8_t* trunc;
+    float* tobs;         // [E][N][D] or null
+    const uint8_t* mask; // reset mask or null
+    uint64_t seed;
+    int64_t env_offset;
+    int E;
+};
+
+// ---------------------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float clampf_(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+template <typename Real>
+__device__ __forceinline__ Real clampr_(Real v, Real lo, Real hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ float radf_(float d) { return (3.14159265358979323846f / 180.0f) * d; }
+__device__ __forceinline__ float degf_(float r) { return (180.0f / 3.14159265358979323846f) * r; }
+
+template <typename Real>
+__device__ __forceinline__ Real shfl_(Real v, int src, int width) { return __shfl(v, src, width); }
+
+// ---------------------------------------------------------------------------------------
+// geometry: URDF collision shapes, GJK distance, ray vs cylinder
+// ---------------------------------------------------------------------------------------
+template <typename Real>
+struct Shape {
+    V3<Real> c;
+    M3<Real> R;      // body -> world
+    V3<Real> h;      // box half extents / cylinder (.z = half height)
+    Real r;          // cylinder radius (0 for a box)
+    int cyl;
+};
+
+template <typename Real>
+__device__ __forceinline__ V3<Real> support(const Shape<Real>& s, V3<Real> d) {
+    const V3<Real> dl = mulT(s.R, d);
+    V3<Real> pl;
+    if (s.cyl) {
+        const Real n2 = dl.x * dl.x + dl.y * dl.y;
+        const Real k = n2 > Real(0) ? s.r / sqrt_(n2) : Real(0);
+        pl = v3(k * dl.x, k * dl.y, dl.z >= Real(0) ? s.h.z : -s.h.z);
+    } else {
+        pl = v3(dl.x >= Real(0) ? s.h.x : -s.h.x, dl.y >= Real(0) ? s.h.y : -s.h.y, dl.z >= Real(0) ? s.h.z : -s.h.z);
+    }
+    return s.c + mul(s.R, pl);
+}
+
+// closest point of triangle (a,b,c) to the origin (Ericson 5.1.5); the supporting
+// vertices are written to o0..o2 (m of them)
+template <typename Real>
+__device__ __forceinline__ V3<Real> tri_closest(V3<Real> a, V3<Real> b, V3<Real> c, V3<Real>& o0, V3<Real>& o1,
+                                               V3<Real>& o2, int& m) {
+    const V3<Real> ab = b - a, ac = c - a;
+    const Real d1 = -dot(ab, a), d2 = -dot(ac, a);
+    if (d1 <= Real(0) && d2 <= Real(0)) { o0 = a; m = 1; return a; }
+    const Real d3 = -dot(ab, b), d4 = -dot(ac, b);
+    if (d3 >= Real(0) && d4 <= d3) { o0 = b; m = 1; return b; }
+    const Real vc = d1 * d4 - d3 * d2;
+    if (vc <= Real(0) && d1 >= Real(0) && d3 <= Real(0)) {
+        o0 = a; o1 = b; m = 2;
+        return a + (d1 / (d1 - d3)) * ab;
+    }
+    const Real d5 = -dot(ab, c), d6 = -dot(ac, c);
+    if (d6 >= Real(0) && d5 <= d6) { o0 = c; m = 1; return c; }
+    const Real vb = d5 * d2 - d1 * d6;
+    if (vb <= Real(0) && d2 >= Real(0) && d6 <= Real(0)) {
+        o0 = a; o1 = c; m = 2;
+        return a + (d2 / (d2 - d6)) * ac;
+    }
+    const Real va = d3 * d6 - d5 * d4;
+    if (va <= Real(0) && (d4 - d3) >= Real(0) && (d5 - d6) >= Real(0)) {
+        o0 = b; o1 = c; m = 2;
+        return b + ((d4 - d3) / ((d4 - d3) + (d5 - d6))) * (c - b);
+    }
+    const Real den = Real(1) / (va + vb + vc);
+    o0 = a; o1 = b; o2 = c; m = 3;
+    return a + (vb * den) * ab + (vc * den) * ac;
+}
+
+// Euclidean distance of two convex shapes (0 if they overlap); GJK with the simplex kept
+// in named registers (no dynamic indexing -> no scratch)
+template <typename Real>
+__device__ __noinline__ Real gjk_distance(const Shape<Real>& A, const Shape<Real>& B) {
+    const Real eps = sizeof(Real) == 4 ? Real(1e-6) : Real(1e-13);
+    V3<Real> W0, W1, W2, W3;
+    int n = 0;
+    V3<Real> v = A.c - B.c;
+    if (dot(v, v) < Real(1e-20)) v = v3(Real(1), Real(0), Real(0));
+    for (int it = 0; it < 48; ++it) {
+        const V3<Real> w = support(A, Real(-1) * v) - support(B, v);
+        const Real vv = dot(v, v);
+        if (vv - dot(v, w) <= eps * vv) break;
+        const V3<Real> dw0 = W0 - w, dw1 = W1 - w, dw2 = W2 - w;
+        if ((n > 0 && dot(dw0, dw0) < Real(1e-20)) || (n > 1 && dot(dw1, dw1) < Real(1e-20)) ||
+            (n > 2 && dot(dw2, dw2) < Real(1e-20)))
+            break;
+        if (n == 0) { W0 = w; n = 1; v = w; }
+        else if (n == 1) {
+            W1 = w;
+            const V3<Real> ab = W1 - W0;
+            const Real t = -dot(W0, ab) / dot(ab, ab);
+            if (t <= Real(0)) { n = 1; v = W0; }
+            else if (t >= Real(1)) { W0 = W1; n = 1; v = W0; }
+            else { n = 2; v = W0 + t * ab; }
+        } else if (n == 2) {
+            int m;
+            v = tri_closest(W0, W1, w, W0, W1, W2, m);
+            n = m;
+        } else {
+            W3 = w;
+            // faces (0,1,2|3) (0,2,3|1) (0,3,1|2) (1,3,2|0)
+            Real best = Real(3.0e38);
+            V3<Real> bv = v, b0 = W0, b1 = W1, b2 = W2;
+            int bm = 0;
+            bool outside = false;
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const V3<Real> p0 = f == 3 ? W1 : W0;
+                const V3<Real> p1 = f == 0 ? W1 : (f == 1 ? W2 : W3);
+                const V3<Real> p2 = f == 0 ? W2 : (f == 1 ? W3 : (f == 2 ? W1 : W2));
+                const V3<Real> po = f == 0 ? W3 : (f == 1 ? W1 : (f == 2 ? W2 : W0));
+                const V3<Real> nrm = cross(p1 - p0, p2 - p0);
+                const Real so = -dot(nrm, p0), sd = dot(nrm, po - p0);
+                if (so * sd < Real(0)) {
+                    outside = true;
+                    V3<Real> q0, q1, q2;
+                    int m;
+                    const V3<Real> vf = tri_closest(p0, p1, p2, q0, q1, q2, m);
+                    const Real dd = dot(vf, vf);
+                    if (dd < best) { best = dd; bv = vf; b0 = q0; b1 = q1; b2 = q2; bm = m; }
+                }
+            }
+            if (!outside) return Real(0);
+            v = bv; W0 = b0; W1 = b1; W2 = b2; n = bm;
+        }
+        if (dot(v, v) < Real(1e-20)) return Real(0);
+    }
+    return sqrt_(dot(v, v));
+}
+
+// entry fraction of the segment p0 -> p1 into a cylinder, > 1 on a miss
+template <typename Real>
+__device__ __forceinline__ Real ray_cylinder(const Shape<Real>& s, V3<Real> p0, V3<Real> p1) {
+    const V3<Real> a = mulT(s.R, p0 - s.c), d = mulT(s.R, p1 - p0);
+    Real lo = Real(-3.0e38), hi = Real(3.0e38);
+    if (d.z == Real(0)) {
+        if (fabs_(a.z) > s.h.z) return Real(2);
+    } else {
+        Real t1 = (-s.h.z - a.z) / d.z, t2 = (s.h.z - a.z) / d.z;
+        if (t1 > t2) { const Real t = t1; t1 = t2; t2 = t; }
+        lo = t1; hi = t2;
+    }
+    const Real qa = d.x * d.x + d.y * d.y, qb = Real(2) * (a.x * d.x + a.y * d.y),
+               qc = a.x * a.x + a.y * a.y - s.r * s.r;
+    if (qa == Real(0)) {
+        if (qc > Real(0)) return Real(2);
+    } else {
+        const Real disc = qb * qb - Real(4) * qa * qc;
+        if (disc < Real(0)) return Real(2);
+        const Real sq = sqrt_(disc);
+        const Real t3 = (-qb - sq) / (Real(2) * qa), t4 = (-qb + sq) / (Real(2) * qa);
+        if (t3 > lo) lo = t3;
+        if (t4 < hi) hi = t4;
+    }
+    if (lo > hi || hi < Real(0) || lo > Real(1)) return Real(2);
+    return lo < Real(0) ? Real(0) : lo;
+}
+
+template <typename Real>
+__device__ __forceinline__ M3<Real> rotz_(Real yaw) {
+    Real s, c;
+    sincos_(yaw, &s, &c);
+    return {c, -s, Real(0), s, c, Real(0), Real(0), Real(0), Real(1)};
+}
+template <typename Real>
+__device__ __forceinline__ M3<Real> mmul_(const M3<Real>& a, const M3<Real>& b) {
+    return {a.a00 * b.a00 + a.a01 * b.a10 + a.a02 * b.a20, a.a00 * b.a01 + a.a01 * b.a11 + a.a02 * b.a21,
+            a.a00 * b.a02 + a.a01 * b.a12 + a.a02 * b.a22, a.a10 * b.a00 + a.a11 * b.a10 + a.a12 * b.a20,
+            a.a10 * b.a01 + a.a11 * b.a11 + a.a12 * b.a21, a.a10 * b.a02 + a.a11 * b.a12 + a.a12 * b.a22,
+            a.a20 * b.a00 + a.a21 * b.a10 + a.a22 * b.a20, a.a20 * b.a01 + a.a21 * b.a11 + a.a22 * b.a21,
+            a.a20 * b.a02 + a.a21 * b.a12 + a.a22 * b.a22};
+}
+
+// part k of a gate (portal.urdf / low_portal.urdf) or obstacle (obstacle.urdf), own frame
+template <typename Real>
+__device__ __forceinline__ void gate_part(int k, int low, V3<Real>& off, M3<Real>& R, V3<Real>& h, Real& r, int& cyl) {
+    const Real c157 = Real(0.0007963267107332633), s157 = Real(0.9999996829318346);   // cos/sin(1.57)
+    const M3<Real> I = {Real(1), Real(0), Real(0), Real(0), Real(1), Real(0), Real(0), Real(0), Real(1)};
+    const M3<Real> Ry = {c157, Real(0), s157, Real(0), Real(1), Real(0), -s157, Real(0), c157};
+    h = v3(Real(0.25), Real(0.025), Real(0.025)); r = Real(0); cyl = 0; R = I;
+    if (k == 0) off = v3(Real(0), Real(0), Real(-0.225));
+    else if (k == 1) off = v3(Real(0), Real(0), Real(0.225));
+    else if (k == 2) { off = v3(Real(0.225), Real(0), Real(0)); R = Ry; }
+    else if (k == 3) { off = v3(Real(-0.225), Real(0), Real(0)); R = Ry; }
+    else if (low) { off = v3(Real(0), Real(0), Real(-0.4)); h = v3(Real(0.075), Real(0.075), Real(0.125)); }
+    else { off = v3(Real(0), Real(0), Real(-0.6)); h = v3(Real(0), Real(0), Real(0.4)); r = Real(0.05); cyl = 1; }
+}
+template <typename Real>
+__device__ __forceinline__ void obst_part(int k, V3<Real>& off, V3<Real>& h, Real& r, int& cyl) {
+    if (k == 0) { off = v3(Real(0), Real(0), Real(0)); h = v3(Real(0), Real(0), Real(0.4)); r = Real(0.05); cyl = 1; }
+    else { off = v3(Real(0), Real(0), Real(-0.4)); h = v3(Real(0.075), Real(0.075), Real(0.125)); r = Real(0); cyl = 0; }
+}
+
+// min distance drone <-> gate g or obstacle; parts whose bounding sphere is farther than
+// `cut` are skipped (their distance is then reported as >= cut)
+template <typename Real>
+__device__ __noinline__ Real gate_distance(const Shape<Real>& ds, V3<Real> org, Real yaw, int low, Real cut) {
+    const M3<Real> Rg = rotz_(yaw);
+    const Real dr = sqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
+    Real best = Real(3.0e38);
+    for (int k = 0; k < 5; ++k) {
+        V3<Real> off, h;
+        M3<Real> R;
+        Real r;
+        int cyl;
+        gate_part(k, low, off, R, h, r, cyl);
+        Shape<Real> s{org + mul(Rg, off), mmul_(Rg, R), h, r, cyl};
+        const Real pr = cyl ? sqrt_(r * r + h.z * h.z) : sqrt_(dot(h, h));
+        const V3<Real> dc = s.c - ds.c;
+        const Real lb = sqrt_(dot(dc, dc)) - pr - dr;
+        if (lb >= cut) { if (lb < best) best = lb; continue; }
+        const Real dd = gjk_distance(ds, s);
+        if (dd < best) best = dd;
+    }
+    return best;
+}
+template <typename Real>
+__device__ __noinline__ Real obst_distance(const Shape<Real>& ds, V3<Real> org, Real cut) {
+    const M3<Real> I = {Real(1), Real(0), Real(0), Real(0), Real(1), Real(0), Real(0), Real(0), Real(1)};
+    const Real dr = sqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
+    Real best = Real(3.0e38);
+    for (int k = 0; k < 2; ++k) {
+        V3<Real> off, h;
+        Real r;
+        int cyl;
+        obst_part(k, off, h, r, cyl);
+        Shape<Real> s{org + off, I, h, r, cyl};
+        const Real pr = cyl ? sqrt_(r * r + h.z * h.z) : sqrt_(dot(h, h));
+        const V3<Real> dc = s.c - ds.c;
+        const Real lb = sqrt_(dot(dc, dc)) - pr - dr;
+        if (lb >= cut) { if (lb < best) best = lb; continue; }
+        const Real dd = gjk_distance(ds, s);
+        if (dd < best) best = dd;
+    }
+    return best;
+}
+
+template <typename Real>
+__device__ __forceinline__ Shape<Real> drone_shape(const RaceConst<Real>& C, V3<Real> pos, Q4<Real> q) {
+    const M3<Real> R = rot(q);
+    return Shape<Real>{pos + C.coll_zoff * col2(R), R, v3(Real(0), Real(0), C.coll_hh), C.coll_r, 1};
+}
+
+// ---------------------------------------------------------------------------------------
+// lane state
+// ---------------------------------------------------------------------------------------
+template <typename Real>
+struct RDrone {
+    V3<Real> pos, vel, w, angv, lpos, kpos;
+    Q4<Real> q, ql;
+    Real rpm[4], prev[4];
+    Real prev_rpy[3], prev_vel[3];
+    float lpf1[3], lpf2[3], ierr[3], ierrm[3];
+    float pw_roll, pw_pitch, psp_roll, psp_pitch;
+    float ctl[4];
+    Real mass, inertia[3];
+    int tick, last_att, last_pos, tumble, gate, flags;
+};
+
+template <typename Real>
+__device__ __forceinline__ Real ld(const Real* f, int field, size_t EN, size_t slot) { return f[size_t(field) * EN + slot]; }
+template <typename Real>
+__device__ __forceinline__ void st(Real* f, int field, size_t EN, size_t slot, Real v) { f[size_t(field) * EN + slot] = v; }
+
+template <typename Real>
+__device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, size_t slot, RDrone<Real>& d) {
+    const Real* f = a.f;
+#define L_(k) ld(f, (k), EN, slot)
+    d.pos = v3(L_(RF_POS), L_(RF_POS + 1), L_(RF_POS + 2));
+    d.q = {L_(RF_QUAT), L_(RF_QUAT + 1), L_(RF_QUAT + 2), L_(RF_QUAT + 3)};
+    d.vel = v3(L_(RF_VEL), L_(RF_VEL + 1), L_(RF_VEL + 2));
+    d.w = v3(L_(RF_OMEGA), L_(RF_OMEGA + 1), L_(RF_OMEGA + 2));
+    d.angv = v3(L_(RF_ANGV), L_(RF_ANGV + 1), L_(RF_ANGV + 2));
+    d.ql = {L_(RF_LINK_QUAT), L_(RF_LINK_QUAT + 1), L_(RF_LINK_QUAT + 2), L_(RF_LINK_QUAT + 3)};
+    d.lpos = v3(L_(RF_LINK_POS), L_(RF_LINK_POS + 1), L_(RF_LINK_POS + 2));
+    d.kpos = v3(L_(RF_KIN_POS), L_(RF_KIN_POS + 1), L_(RF_KIN_POS + 2));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d.rpm[k] = L_(RF_RPM + k); d.prev[k] = L_(RF_PREV_RPM + k); d.ctl[k] = float(L_(RF_CTL + k)); }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        d.prev_rpy[k] = L_(RF_PREV_RPY + k); d.prev_vel[k] = L_(RF_PREV_VEL + k);
+        d.lpf1[k] = float(L_(RF_LPF_D1 + k)); d.lpf2[k] = float(L_(RF_LPF_D2 + k));
+        d.ierr[k] = float(L_(RF_I_ERR + k)); d.ierrm[k] = float(L_(RF_I_ERR_M + k));
+        d.inertia[k] = L_(RF_INERTIA + k);
+    }
+    d.pw_roll = float(L_(RF_PREV_OMEGA_ROLL)); d.pw_pitch = float(L_(RF_PREV_OMEGA_PITCH));
+    d.psp_roll = float(L_(RF_PREV_SP_ROLL)); d.psp_pitch = float(L_(RF_PREV_SP_PITCH));
+    d.mass = L_(RF_MASS);
+#undef L_
+    const int32_t* ist = a.ist;
+    d.tick = ist[RI_TICK * EN + slot]; d.last_att = ist[RI_LAST_ATT * EN + slot];
+    d.last_pos = ist[RI_LAST_POS * EN + slot]; d.tumble = ist[RI_TUMBLE * EN + slot];
+    d.gate = ist[RI_GATE * EN + slot]; d.flags = ist[RI_FLAGS * EN + slot];
+}
+
+template <typename Real>
+__device__ __forceinline__ void store_drone(const RaceArgs<Real>& a, size_t EN, size_t slot, const RDrone<Real>& d,
+                                            bool params) {
+    Real* f = a.f;
+#define S_(k, v) st(f, (k), EN, slot, Real(v))
+    S_(RF_POS, d.pos.x); S_(RF_POS + 1, d.pos.y); S_(RF_POS + 2, d.pos.z);
+    S_(RF_QUAT, d.q.x); S_(RF_QUAT + 1, d.q.y); S_(RF_QUAT + 2, d.q.z); S_(RF_QUAT + 3, d.q.w);
+    S_(RF_VEL, d.vel.x); S_(RF_VEL + 1, d.vel.y); S_(RF_VEL + 2, d.vel.z);
+    S_(RF_OMEGA, d.w.x); S_(RF_OMEGA + 1, d.w.y); S_(RF_OMEGA + 2, d.w.z);
+    S_(RF_ANGV, d.angv.x); S_(RF_ANGV + 1, d.angv.y); S_(RF_ANGV + 2, d.angv.z);
+    S_(RF_LINK_QUAT, d.ql.x); S_(RF_LINK_QUAT + 1, d.ql.y); S_(RF_LINK_QUAT + 2, d.ql.z); S_(RF_LINK_QUAT + 3, d.ql.w);
+    S_(RF_LINK_POS, d.lpos.x); S_(RF_LINK_POS + 1, d.lpos.y); S_(RF_LINK_POS + 2, d.lpos.z);
+    S_(RF_KIN_POS, d.kpos.x); S_(RF_KIN_POS + 1, d.kpos.y); S_(RF_KIN_POS + 2, d.kpos.z);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { S_(RF_RPM + k, d.rpm[k]); S_(RF_PREV_RPM + k, d.prev[k]); S_(RF_CTL + k, d.ctl[k]); }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        S_(RF_PREV_RPY + k, d.prev_rpy[k]); S_(RF_PREV_VEL + k, d.prev_vel[k]);
+        S_(RF_LPF_D1 + k, d.lpf1[k]); S_(RF_LPF_D2 + k, d.lpf2[k]);
+        S_(RF_I_ERR + k, d.ierr[k]); S_(RF_I_ERR_M + k, d.ierrm[k]);
+    }
+    S_(RF_PREV_OMEGA_ROLL, d.pw_roll); S_(RF_PREV_OMEGA_PITCH, d.pw_pitch);
+    S_(RF_PREV_SP_ROLL, d.psp_roll); S_(RF_PREV_SP_PITCH, d.psp_pitch);
+    if (params) {   // mass / inertia: written by the reset only
+        S_(RF_MASS, d.mass);
+        S_(RF_INERTIA, d.inertia[0]); S_(RF_INERTIA + 1, d.inertia[1]); S_(RF_INERTIA + 2, d.inertia[2]);
+    }
+#undef S_
+    int32_t* ist = a.ist;
+    ist[RI_TICK * EN + slot] = d.tick; ist[RI_LAST_ATT * EN + slot] = d.last_att;
+    ist[RI_LAST_POS * EN + slot] = d.last_pos; ist[RI_TUMBLE * EN + slot] = d.tumble;
+    ist[RI_GATE * EN + slot] = d.gate; ist[RI_FLAGS * EN + slot] = d.flags;
+}
+
+// ---------------------------------------------------------------------------------------
+// firmware controllerMellinger (C float) + MellingerControl wrapper
+// ---------------------------------------------------------------------------------------
+struct Lpf { float b0, b1, b2, a1, a2; };
+__device__ __forceinline__ float lpf_apply(const Lpf& l, float& d1, float& d2, float sample) {
+    float d0 = sample - d1 * l.a1 - d2 * l.a2;
+    if (!isfinite(d0)) d0 = sample;
+    const float out = d0 * l.b0 + d1 * l.b1 + d2 * l.b2;
+    d2 = d1;
+    d1 = d0;
+    return out;
+}
+
+// FULLSTATE setpoint modes (MellingerControl.py:510-543): x,y,z,quat abs; rates 0
+template <typename Real>
+__device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3], float xc_x, float xc_y,
+                                             const float gyro[3], const float pos[3], const float vel[3],
+                                             const float Rm[9]) {
+    const float dt = float(1.0f / 500);
+    const float rx = sp[0] - pos[0], ry = sp[1] - pos[1], rz = sp[2] - pos[2];
+    const float vx = 0.0f - vel[0], vy = 0.0f - vel[1], vz = 0.0f - vel[2];
+    d.ierr[2] = clampf_(d.ierr[2] + rz * dt, -0.4f, 0.4f);
+    d.ierr[0] = clampf_(d.ierr[0] + rx * dt, -2.0f, 2.0f);
+    d.ierr[1] = clampf_(d.ierr[1] + ry * dt, -2.0f, 2.0f);
+    const float tx = 0.027f * 0.0f + 0.4f * rx + 0.2f * vx + 0.05f * d.ierr[0];
+    const float ty = 0.027f * 0.0f + 0.4f * ry + 0.2f * vy + 0.05f * d.ierr[1];
+    const float tz = 0.027f * (0.0f + 9.81f) + 1.25f * rz + 0.4f * vz + 0.05f * d.ierr[2];
+    // R columns
+    const float Rx0 = Rm[0], Rx1 = Rm[3], Rx2 = Rm[6];
+    const float Ry0 = Rm[1], Ry1 = Rm[4], Ry2 = Rm[7];
+    const float Rz0 = Rm[2], Rz1 = Rm[5], Rz2 = Rm[8];
+    const float current_thrust = tx * Rz0 + ty * Rz1 + tz * Rz2;
+    const float tn = sqrtf(tx * tx + ty * ty + tz * tz);
+    const float zd0 = tx / tn, zd1 = ty / tn, zd2 = tz / tn;
+    // y_des = normalize(z_des x x_c), x_c = (cos yaw, sin yaw, 0)
+    float yd0 = zd1 * 0.0f - zd2 * xc_y, yd1 = zd2 * xc_x - zd0 * 0.0f, yd2 = zd0 * xc_y - zd1 * xc_x;
+    const float yn = sqrtf(yd0 * yd0 + yd1 * yd1 + yd2 * yd2);
+    yd0 /= yn; yd1 /= yn; yd2 /= yn;
+    const float xd0 = yd1 * zd2 - yd2 * zd1, xd1 = yd2 * zd0 - yd0 * zd2, xd2 = yd0 * zd1 - yd1 * zd0;
+    const float eRx = (zd0 * Ry0 + zd1 * Ry1 + zd2 * Ry2) - (Rz0 * yd0 + Rz1 * yd1 + Rz2 * yd2);
+    const float eRy = -((xd0 * Rz0 + xd1 * Rz1 + xd2 * Rz2) - (Rx0 * zd0 + Rx1 * zd1 + Rx2 * zd2));
+    const float eRz = (yd0 * Rx0 + yd1 * Rx1 + yd2 * Rx2) - (Ry0 * xd0 + Ry1 * xd1 + Ry2 * xd2);
+    const float rate_roll = radf_(gyro[0]), rate_pitch = -radf_(gyro[1]), rate_yaw = radf_(gyro[2]);
+    const float ewx = radf_(0.0f) - rate_roll, ewy = -radf_(0.0f) - rate_pitch, ewz = radf_(0.0f) - rate_yaw;
+    float err_d_roll = 0, err_d_pitch = 0;
+    if (d.pw_roll == d.pw_roll) {
+        err_d_roll = ((radf_(0.0f) - d.psp_roll) - (rate_roll - d.pw_roll)) / dt;
+        err_d_pitch = (-(radf_(0.0f) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) / dt;
+    }
+    d.pw_roll = rate_roll;
+    d.pw_pitch = rate_pitch;
+    d.psp_roll = radf_(0.0f);
+    d.psp_pitch = radf_(0.0f);
+    d.ierrm[0] = clampf_(d.ierrm[0] + (-eRx) * dt, -1.0f, 1.0f);
+    d.ierrm[1] = clampf_(d.ierrm[1] + (-eRy) * dt, -1.0f, 1.0f);
+    d.ierrm[2] = clampf_(d.ierrm[2] + (-eRz) * dt, -1500.0f, 1500.0f);
+    const float Mx = -70000.0f * eRx + 20000.0f * ewx + 0.0f * d.ierrm[0] + 200.0f * err_d_roll;
+    const float My = -70000.0f * eRy + 20000.0f * ewy + 0.0f * d.ierrm[1] + 200.0f * err_d_pitch;
+    const float Mz = -60000.0f * eRz + 12000.0f * ewz + 500.0f * d.ierrm[2];
+    d.ctl[3] = 132000.0f * current_thrust;
+    if (d.ctl[3] > 0) {
+        d.ctl[0] = float(int16_t(clampf_(Mx, -32000.0f, 32000.0f)));
+        d.ctl[1] = float(int16_t(clampf_(My, -32000.0f, 32000.0f)));
+        d.ctl[2] = float(int16_t(clampf_(-Mz, -32000.0f, 32000.0f)));
+    } else {
+        d.ctl[0] = d.ctl[1] = d.ctl[2] = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { d.ierr[k] = 0; d.ierrm[k] = 0; }
+    }
+}
+
+// MellingerControl.computeControl (154-262) -> rpm (float64 wrapper arithmetic in Real)
+template <typename Real>
+__device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lpf, const float sp[3], float xc_x,
+                                                  float xc_y, V3<Real> rpy, const Real noise[4]) {
+    const Real fdt = Real(0.002);
+    const Real r2d = Real(57.29577951308232);
+    Real rates[3];
+    const Real rr[3] = {rpy.x, rpy.y, rpy.z};
+    const Real vv[3] = {d.vel.x, d.vel.y, d.vel.z};
+    Real acc_z = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        rates[k] = (rr[k] - d.prev_rpy[k]) / fdt;
+        d.prev_rpy[k] = rr[k];
+        if (k == 2) acc_z = (vv[k] - d.prev_vel[k]) / fdt / Real(9.8) + Real(1);
+        d.prev_vel[k] = vv[k];
+    }
+    float gyro[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gyro[k] = lpf_apply(lpf, d.lpf1[k], d.lpf2[k], float(rates[k] * r2d));
+    Real pwm[4];
+    if (float(acc_z) < -0.5f) d.tumble += 1; else d.tumble = 0;
+    if (d.tumble >= 30) {
+        d.tick += 1;
+        pwm[0] = pwm[1] = pwm[2] = pwm[3] = Real(0);
+    } else {
+        const double cur = double(d.tick) / 500.0;
+        const double la = double(d.last_att) / 500.0, lp = double(d.last_pos) / 500.0;
+        int t;
+        if ((cur - la > 0.002) && (cur - lp > 0.01)) { t = 0; d.last_pos = d.tick; d.last_att = d.tick; }
+        else if (cur - la > 0.002) { d.last_att = d.tick; t = 2; }
+        else t = 1;
+        if ((t & 1) == 0) {   // RATE_DO_EXECUTE(500 Hz, tick)
+            // state: attitude quaternion from rpy -> rotation (quat2rotmat), position, velocity
+            float sr, cr, sp_, cp, sy, cy;
+            sincosf(float(rpy.x), &sr, &cr);
+            sincosf(float(rpy.y), &sp_, &cp);
+            sincosf(float(rpy.z), &sy, &cy);
+            const float Rm[9] = {cy * cp, cy * sp_ * sr - sy * cr, cy * sp_ * cr + sy * sr,
+                                 sy * cp, sy * sp_ * sr + cy * cr, sy * sp_ * cr - cy * sr,
+                                 -sp_, cp * sr, cp * cr};
+            const float pos[3] = {float(d.pos.x), float(d.pos.y), float(d.pos.z)};
+            const float vel[3] = {float(d.vel.x), float(d.vel.y), float(d.vel.z)};
+            mellinger_fw(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
+        }
+        d.tick += 1;
+        // _compute_pwms (423-442)
+        const Real r = Real(d.ctl[0]) / Real(2), p = Real(d.ctl[1]) / Real(2), y = Real(d.ctl[2]), th = Real(d.ctl[3]);
+        const Real m4[4] = {th - r + p + y, th - r - p - y, th + r - p + y, th + r + p - y};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const Real x = clampr_(m4[k], Real(0), Real(65535)) / Real(65535) * Real(60);
+            const Real volts = Real(-0.0006239) * x * x + Real(0.088) * x;
+            Real pct = volts / Real(3);
+            if (pct > Real(1)) pct = Real(1);
+            pwm[k] = pct * Real(65535);
+        }
+    }
+    // clip -> thrust -> reorder [3,2,1,0] -> + noise -> _thr2pwm -> rpm (246-262)
+    Real th[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const Real rp = Real(0.2685) * clampr_(pwm[k], Real(20000), Real(65535)) + Real(4070.3);
+        th[k] = Real(3.16e-10) * rp * rp;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        Real t = th[3 - k] + noise[k];
+        if (t < Real(0)) t = Real(0);
+        Real mp = (sqrt_(t / Real(1) / Real(3.16e-10)) - Real(4070.3)) / Real(0.2685);
+        mp = clampr_(mp, Real(20000), Real(65535));
+        d.prev[k] = d.rpm[k];
+        d.rpm[k] = Real(0.2685) * mp + Real(4070.3);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// one physics sub-step of one drone (Bullet floating-base step after the force calls)
+// ---------------------------------------------------------------------------------------
+template <typename Real>
+__device__ __forceinline__ Real clamp100r(Real x) { return clampr_(x, Real(-100), Real(100)); }
+
+template <typename Real, int PH>
+__device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDrone<Real>& d, V3<Real> F_ext,
+                                                 V3<Real> T_ext) {
+    constexpr bool GND = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
+    constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
+    const M3<Real> R = rot(d.q);
+    // cached link basis: GND modes refresh it (getLinkStates(computeForwardKinematics=1))
+    // before the ground-effect forces, after the motor forces (BaseAviary.py:739-744)
+    const M3<Real> Rs = C.link_lag ? rot(d.ql) : R;
+    Real sum_f = 0, t2 = 0;
+    V3<Real> P = v3(Real(0), Real(0), Real(0));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const Real r2 = d.rpm[i] * d.rpm[i];
+        const Real f = r2 * C.kf;
+        sum_f += f;
+        P = P + v3(f * C.px[i], f * C.py[i], f * C.pz[i]);
+        t2 += (i & 1) ? -r2 : r2;
+    }
+    const Real tau_z = t2 * C.km;
+    const V3<Real> zs = col2(Rs);
+    V3<Real> Fw = v3(sum_f * zs.x, sum_f * zs.y, sum_f * zs.z - d.mass * C.gravity) + F_ext;
+    const V3<Real> m3 = mulT(R, zs);
+    V3<Real> nb = cross(P, m3) + tau_z * m3 + mulT(R, T_ext);
+    if constexpr (GND) {
+        const Real sqx = d.q.x * d.q.x, sqy = d.q.y * d.q.y, sqz = d.q.z * d.q.z, squ = d.q.w * d.q.w;
+        const Real sarg = Real(-2) * (d.q.x * d.q.z - d.q.w * d.q.y);
+        const Real den = squ - sqx - sqy + sqz, num = Real(2) * (d.q.y * d.q.z + d.q.w * d.q.x);
+        const bool gate = fabs_(sarg) < Real(0.99999) && (den > Real(0) || (den == Real(0) && num == Real(0)));
+        if (gate) {
+            Real sg = 0;
+            V3<Real> G = v3(Real(0), Real(0), Real(0));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                Real h = d.pos.z + R.a20 * C.px[i] + R.a21 * C.py[i] + R.a22 * C.pz[i];
+                h = h < C.gnd_clip ? C.gnd_clip : h;
+                const Real k = C.prop_r4 / h;
+                const Real g = C.gnd_kf * d.rpm[i] * d.rpm[i] * k * k;
+                sg += g;
+                G = G + v3(g * C.px[i], g * C.py[i], g * C.pz[i]);
+            }
+            Fw = Fw + sg * col2(R);
+            nb = nb + v3(G.y, -G.x, Real(0));
+        }
+    }
+    if constexpr (DRAG) {
+        Real s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s += d.prev[i];
+        s = s * Real(0.10471975511965977);
+        const V3<Real> dw = v3(-C.drag[0] * s * d.vel.x, -C.drag[1] * s * d.vel.y, -C.drag[2] * s * d.vel.z);
+        Fw = Fw + (GND ? dw : mul(Rs, mulT(R, dw)));
+    }
+    const Real ixx = d.inertia[0], iyy = d.inertia[1], izz = d.inertia[2];
+    const V3<Real> wb = mulT(R, d.w);
+    const V3<Real> Iw = v3(ixx * wb.x, iyy * wb.y, izz * wb.z);
+    const Real kw = Real(0.04) + Real(0.04) * sqrt_(dot(wb, wb));
+    const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
+    const V3<Real> wdot = mul(R, v3(rhs.x / ixx, rhs.y / iyy, rhs.z / izz));
+    const Real kv = Real(0.04) + Real(0.04) * sqrt_(dot(d.vel, d.vel));
+    const V3<Real> acc = (Real(1) / d.mass) * Fw - kv * d.vel;
+    d.w = v3(clamp100r(d.w.x + C.dt * wdot.x), clamp100r(d.w.y + C.dt * wdot.y), clamp100r(d.w.z + C.dt * wdot.z));
+    d.vel = v3(clamp100r(d.vel.x + C.dt * acc.x), clamp100r(d.vel.y + C.dt * acc.y), clamp100r(d.vel.z + C.dt * acc.z));
+    // forwardKinematics of this step caches the pre-integration pose
+    d.ql = d.q;
+    d.lpos = d.pos;
+    d.pos = d.pos + C.dt * d.vel;
+    Real ang = sqrt_(dot(d.w, d.w));
+    if (ang > C.ang_max) ang = C.ang_max;
+    Real sh, ch;
+    sincos_(Real(0.5) * ang * C.dt, &sh, &ch);
+    const Real sc = ang < Real(0.001) ? Real(0.5) * C.dt - (C.dt * C.dt * C.dt) * Real(0.020833333333) * ang * ang
+                                      : sh / ang;
+    const V3<Real> ax = sc * d.w;
+    const Q4<Real> q0 = d.q;
+    const Q4<Real> q1 = {ch * q0.x + ax.x * q0.w + ax.y * q0.z - ax.z * q0.y,
+                         ch * q0.y + ax.y * q0.w + ax.z * q0.x - ax.x * q0.z,
+                         ch * q0.z + ax.z * q0.w + ax.x * q0.y - ax.y * q0.x,
+                         ch * q0.w - ax.x * q0.x - ax.y * q0.y - ax.z * q0.z};
+    const Real inv = rsqrt_(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
+    d.q = {q1.x * inv, q1.y * inv, q1.z * inv, q1.w * inv};
+    const M3<Real> Rn = rot(d.q);
+    const Real low = d.pos.z + C.coll_zoff - C.coll_hh * fabs_(Rn.a22) - C.coll_r * sqrt_(Rn.a02 * Rn.a02 + Rn.a12 * Rn.a12);
+    if (low < Real(0)) {
+        d.pos.z -= low;
+        if (d.vel.z < Real(0)) d.vel.z = Real(0);
+    }
+}
+
+template <typename Real>
+__device__ __forceinline__ void race_dyn_substep(const RaceConst<Real>& C, RDrone<Real>& d) {
+    const M3<Real> R = rot(d.q);
+    Real f[4], zt[4], sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[i] = d.rpm[i] * d.rpm[i] * C.kf;
+        zt[i] = d.rpm[i] * d.rpm[i] * C.km;
+        sum += f[i];
+    }
+    const V3<Real> zb = col2(R);
+    const V3<Real> force_w = v3(sum * zb.x, sum * zb.y, sum * zb.z - C.gravity * C.dyn_mass);
+    const Real tz = -zt[0] + zt[1] - zt[2] + zt[3];
+    const Real tx = (f[0] + f[1] - f[2] - f[3]) * C.dyn_arm;
+    const Real ty = (-f[0] + f[1] + f[2] - f[3]) * C.dyn_arm;
+    const V3<Real> rr = d.w;
+    const V3<Real> tq = v3(tx, ty, tz) - cross(rr, v3(C.dyn_i[0] * rr.x, C.dyn_i[1] * rr.y, C.dyn_i[2] * rr.z));
+    const V3<Real> rdd = v3(tq.x * C.dyn_inv_i[0], tq.y * C.dyn_inv_i[1], tq.z * C.dyn_inv_i[2]);
+    d.vel = d.vel + C.dt * (C.dyn_inv_mass * force_w);
+    d.w = rr + C.dt * rdd;
+    d.pos = d.pos + C.dt * d.vel;
+    const V3<Real> w = d.w;
+    const Real wn = sqrt_(dot(w, w));
+    if (!(wn <= Real(1e-8))) {
+        const Real th = wn * C.dt * Real(0.5);
+        Real s, c;
+        sincos_(th, &s, &c);
+        const Real k = s / wn;
+        const Q4<Real> q = d.q;
+        d.q = {c * q.x + k * (w.z * q.y - w.y * q.z + w.x * q.w), c * q.y + k * (-w.z * q.x + w.x * q.z + w.y * q.w),
+               c * q.z + k * (w.y * q.x - w.x * q.y + w.z * q.w), c * q.w + k * (-w.x * q.x - w.y * q.y - w.z * q.z)};
+    }
+    d.angv = mul(R, d.w);
+}
+
+// ---------------------------------------------------------------------------------------
+// obs row (MultiRaceAviary._computeObs, 566-661) written straight to global memory
+// ---------------------------------------------------------------------------------------
+template <typename Real>
+__device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
+                                             V3<Real> pos, Q4<Real> q, V3<Real> vel, V3<Real> w, int gate,
+                                             float* row, bool write, Real* row0) {
+    const V3<Real> rpy = euler_xyz(q);
+    const Real k12[12] = {pos.x, pos.y, pos.z, rpy.x, rpy.y, rpy.z, vel.x, vel.y, vel.z, w.x, w.y, w.z};
+    if (write)
+#pragma unroll
+        for (int k = 0; k < 12; ++k) row[k] = float(k12[k]);
+    if (row0)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) row0[k] = k12[k];
+    const Shape<Real> ds = drone_shape(C, pos, q);
+    for (int g = 0; g < ADRP_MAX_GATES; ++g) {
+        Real v4[4] = {Real(0), Real(0), Real(0), Real(0)};
+        Real in = 0;
+        if (g < C.num_gates) {
+            const V3<Real> org = v3(ld(f, RF_GATE + 4 * g, EN, slot), ld(f, RF_GATE + 4 * g + 1, EN, slot),
+                                    ld(f, RF_GATE + 4 * g + 2, EN, slot));
+            const Real yaw = ld(f, RF_GATE + 4 * g + 3, EN, slot);
+            in = gate_distance(ds, org, yaw, C.gate_type[g] > 0, Real(0.45)) < Real(0.45) ? Real(1) : Real(0);
+            if (in > Real(0)) { v4[0] = org.x; v4[1] = org.y; v4[2] = org.z; v4[3] = yaw; }
+            else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v4[j] = C.gate_nom[g][j];
+            }
+        }
+        if (write) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) row[12 + 4 * g + j] = float(v4[j]);
+            row[28 + g] = float(in);
+        }
+        if (row0 && g < C.num_gates)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) row0[3 + 3 * g + j] = v4[j];
+    }
+    for (int k = 0; k < ADRP_MAX_OBSTACLES; ++k) {
+        Real v3_[3] = {Real(0), Real(0), Real(0)};
+        Real in = 0;
+        if (k < C.num_obstacles) {
+            const V3<Real> org = v3(ld(f, RF_OBST + 3 * k, EN, slot), ld(f, RF_OBST + 3 * k + 1, EN, slot),
+                                    ld(f, RF_OBST + 3 * k + 2, EN, slot));
+            in = obst_distance(ds, org, Real(0.45)) < Real(0.45) ? Real(1) : Real(0);
+            if (in > Real(0)) { v3_[0] = org.x; v3_[1] = org.y; v3_[2] = org.z; }
+            else {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) v3_[j] = C.obst_nom[k][j];
+            }
+        }
+        if (write) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) row[32 + 3 * k + j] = float(v3_[j]);
+            row[44 + k] = float(in);
+        }
+    }
+    if (write) row[48] = float(gate);
+}
+
+// ---------------------------------------------------------------------------------------
+// reset of one drone (+ its env's replicated fields) -> state + initial obs row
+// (MultiRaceAviary.reset 127-167, _addObstacles 347-403, _drone_init 407-467)
+// ---------------------------------------------------------------------------------------
+template <typename Real>
+__device__ __noinline__ void race_reset_lane(const RaceArgs<Real>& a, const RaceConst<Real>& C, int e, int dn, size_t EN,
+                                size_t slot, int episode, float* obs_row) {
+    const uint64_t gid = uint64_t(a.env_offset + e);
+    const uint32_t ep = uint32_t(episode);
+    Real* f = a.f;
+    // track (every drone lane of the env computes the same draws)
+    for (int g = 0; g < ADRP_MAX_GATES; ++g) {
+        Real gx = C.gate_nom[g][0], gy = C.gate_nom[g][1], gyaw = C.gate_nom[g][3];
+        if (C.random_gates && g < C.num_gates) {
+            const U4 u = draw(a.seed, gid, ep, TAG_RACE_TRACK, uint32_t(g));
+            const Real lo = C.gate_off[0], hi = C.gate_off[1];
+            gx += lo + (hi - lo) * Real(u01(u.a));
+            gy += lo + (hi - lo) * Real(u01(u.b));
+            gyaw += lo + (hi - lo) * Real(u01(u.c));
+        }
+        st(f, RF_GATE + 4 * g, EN, slot, gx); st(f, RF_GATE + 4 * g + 1, EN, slot, gy);
+        st(f, RF_GATE + 4 * g + 2, EN, slot, C.gate_nom[g][2]); st(f, RF_GATE + 4 * g + 3, EN, slot, gyaw);
+    }
+    for (int k = 0; k < ADRP_MAX_OBSTACLES; ++k) {
+        Real ox = C.obst_nom[k][0], oy = C.obst_nom[k][1];
+        if (C.random_gates && k < C.num_obstacles) {
+            const U4 u = draw(a.seed, gid, ep, TAG_RACE_TRACK, uint32_t(4 + k));
+            const Real lo = C.obst_off[0], hi = C.obst_off[1];
+            ox += lo + (hi - lo) * Real(u01(u.a));
+            oy += lo + (hi - lo) * Real(u01(u.b));
+        }
+        st(f, RF_OBST + 3 * k, EN, slot, ox); st(f, RF_OBST + 3 * k + 1, EN, slot, oy);
+        st(f, RF_OBST + 3 * k + 2, EN, slot, C.obst_nom[k][2]);
+    }
+    // initial obs at the nominal (loadURDF) poses, at rest
+    const Real d2r = Real(0.017453292519943295);
+    const V3<Real> npos = v3(C.init_pos[dn][0], C.init_pos[dn][1], C.init_pos[dn][2]);
+    const Q4<Real> nq = quat_from_euler(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
+    Real row0[15];
+    const V3<Real> zero = v3(Real(0), Real(0), Real(0));
+    race_obs_row(C, f, EN, slot, npos, nq, zero, zero, 0, obs_row, obs_row != nullptr, row0);
+    if (C.compete && obs_row) {   // other drones' nominal pos + rpy
+        int idx = 0;
+        for (int k = 0; k < C.N; ++k) {
+            if (k == dn) continue;
+            const V3<Real> orpy = euler_xyz(quat_from_euler(C.init_rpy[k][0] * d2r, C.init_rpy[k][1] * d2r, C.init_rpy[k][2] * d2r));
+            float* p = obs_row + 49 + 6 * idx;
+            p[0] = float(C.init_pos[k][0]); p[1] = float(C.init_pos[k][1]); p[2] = float(C.init_pos[k][2]);
+            p[3] = float(orpy.x); p[4] = float(orpy.y); p[5] = float(orpy.z);
+            ++idx;
+        }
+    }
+    const V3<Real> nrpy = euler_xyz(nq);
+    // RewardWrapper.reset: current_target = obs[0, 12:15], previous_pos = obs[0, :3]
+    for (int k = 0; k < 3; ++k) {
+        st(f, RF_WR_TARGET + k, EN, slot, C.num_gates > 0 ? row0[3 + k] : Real(0));
+        st(f, RF_WR_PREV + k, EN, slot, row0[k]);
+    }
+    // controller reset with the initial obs; _drone_init
+    RDrone<Real> d;
+    d.prev_rpy[0] = nrpy.x; d.prev_rpy[1] = nrpy.y; d.prev_rpy[2] = nrpy.z;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        d.prev_vel[k] = Real(0); d.lpf1[k] = d.lpf2[k] = 0.0f; d.ierr[k] = d.ierrm[k] = 0.0f;
+    }
+    d.tick = d.last_att = d.last_pos = d.tumble = 0;
+    d.pw_roll = d.pw_pitch = __builtin_nanf("");
+    d.psp_roll = d.psp_pitch = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d.ctl[k] = 0.0f; d.rpm[k] = d.prev[k] = Real(0); }
+    d.gate = 0; d.flags = 0;
+    d.mass = C.race_mass;
+    d.inertia[0] = C.race_inertia[0]; d.inertia[1] = C.race_inertia[1]; d.inertia[2] = C.race_inertia[2];
+    const uint32_t dtag = TAG_RACE_DRONE | uint32_t(dn);
+    if (C.random_inertia) {
+        const U4 u = draw(a.seed, gid, ep, dtag, 2);
+        const uint32_t uu[4] = {u.a, u.b, u.c, u.d};
+        Real v[4] = {d.mass, d.inertia[0], d.inertia[1], d.inertia[2]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const Real lo = C.inertia_off[k][0], hi = C.inertia_off[k][1];
+            v[k] = clampr_(v[k] + lo + (hi - lo) * Real(u01(uu[k])), Real(0), Real(100));
+        }
+        d.mass = v[0]; d.inertia[0] = v[1]; d.inertia[1] = v[2]; d.inertia[2] = v[3];
+    }
+    Real po[3] = {0, 0, 0}, ro[3] = {0, 0, 0};
+    if (C.random_state) {
+        const U4 u = draw(a.seed, gid, ep, dtag, 0), u2 = draw(a.seed, gid, ep, dtag, 1);
+        const uint32_t a1[3] = {u.a, u.b, u.c}, a2[3] = {u2.a, u2.b, u2.c};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            po[k] = C.pos_off[k][0] + (C.pos_off[k][1] - C.pos_off[k][0]) * Real(u01(a1[k]));
+            ro[k] = C.rot_off[k][0] + (C.rot_off[k][1] - C.rot_off[k][0]) * Real(u01(a2[k]));
+        }
+    }
+    d.pos = v3(npos.x + po[0], npos.y + po[1], npos.z + po[2]);
+    d.q = quat_from_euler(C.init_rpy[dn][0] + ro[0], C.init_rpy[dn][1] + ro[1], C.init_rpy[dn][2] + ro[2]);
+    d.vel = v3(C.init_vel[dn][0], C.init_vel[dn][1], C.init_vel[dn][2]);
+    d.w = v3(C.init_pqr[dn][0], C.init_pqr[dn][1], C.init_pqr[dn][2]);
+    d.angv = d.w;
+    if (C.physics == ADRP_PHYS_DYN) d.w = v3(Real(0), Real(0), Real(0));   // rpy_rates zeroed by _housekeeping
+    d.ql = d.q;
+    d.lpos = d.pos;
+    d.kpos = C.physics == ADRP_PHYS_PYB ? npos : d.pos;   // self.pos: nominal until the first read
+    store_drone(a, EN, slot, d, true);
+    a.ist[RI_STEP * EN + slot] = 0;
+    a.ist[RI_EPISODE * EN + slot] = episode + 1;
+    a.ist[RI_WR_GATE * EN + slot] = 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// env.step kernel
+// ---------------------------------------------------------------------------------------
+template <typename Real, int PH, int G>
+__global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a) {
+    const RaceConst<Real>& C = *a.c;
+    const int lane = blockIdx.x * kRaceBlock + threadIdx.x;
+    const int e_raw = lane / G, d_raw = lane % G;
+    const int N = C.N;
+    const bool active = e_raw < a.E && d_raw < N;
+    const int e = e_raw < a.E ? e_raw : a.E - 1;
+    const int dn = d_raw < N ? d_raw : 0;
+    const size_t EN = size_t(a.E) * N;
+    const size_t slot = size_t(e) * N + dn;
+    const uint64_t gid = uint64_t(a.env_offset + e);
+    RDrone<Real> d;
+    load_drone(a, EN, slot, d);
+    const int sc0 = a.ist[RI_STEP * EN + slot];
+    const int episode = a.ist[RI_EPISODE * EN + slot];
+    const uint32_t ep = uint32_t(episode - 1);
+    // FULLSTATE setpoint (MultiRaceAviary.py:190-194; _sendFullStateCmd 510-543)
+    const float4 av = reinterpret_cast<const float4*>(a.act)[slot];
+    const float sp[3] = {av.x, av.y, av.z};
+    float xc_x, xc_y;
+    {
+        Real qs, qc;
+        sincos_(Real(av.w) * Real(0.5), &qs, &qc);          // get_quaternion_from_euler(0, 0, yaw)
+        const float qz = float(qs), qw = float(qc);
+        const float yaw_deg = degf_(atan2f(2.0f * (qw * qz + 0.0f * 0.0f), 1 - 2 * (0.0f * 0.0f + qz * qz)));
+        xc_x = cosf(radf_(yaw_deg));
+        xc_y = sinf(radf_(yaw_deg));
+    }
+    Lpf lpf;
+    {   // lpf2pInit(gyrolpf, 500, 30) (float)
+        const float fr = 500.0f / 30.0f;
+        const float ohm = tanf(3.14159265358979323846f / fr);
+        const float c = 1.0f + 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm;
+        lpf.b0 = ohm * ohm / c; lpf.b1 = 2.0f * lpf.b0; lpf.b2 = lpf.b0;
+        lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
+        lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
+    }
+    for (int s = 0; s < C.S; ++s) {
+        const uint32_t idx = uint32_t(sc0 + s);
+        if (PH != ADRP_PHYS_PYB) d.kpos = d.pos;          // KIN_PHYSICS read-back
+        if constexpr (PH == ADRP_PHYS_DYN) {
+            race_dyn_substep(C, d);
+        } else {
+            V3<Real> Fx = v3(Real(0), Real(0), Real(0)), Tx = v3(Real(0), Real(0), Real(0));
+            if constexpr (PH == ADRP_PHYS_PYB_DW || PH == ADRP_PHYS_PYB_GND_DRAG_DW) {
+                // _downwash (BaseAviary.py:792-818): every other drone above, LINK_FRAME on link 4
+                Real fz = 0;
+                for (int k = 0; k < N; ++k) {
+                    const Real ox = shfl_(d.pos.x, k, G), oy = shfl_(d.pos.y, k, G), oz = shfl_(d.pos.z, k, G);
+                    const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
+                    const Real dxy = sqrt_(dx * dx + dy * dy);
+                    if (dz > Real(0) && dxy < Real(10)) {
+                        const Real kk = C.prop_r / (Real(4) * dz);
+                        const Real alpha = C.dw1 * kk * kk, beta = C.dw2 * dz + C.dw3;
+                        fz -= alpha * exp_(Real(-0.5) * (dxy / beta) * (dxy / beta));
+                    }
+                }
+                const M3<Real> Rs = C.link_lag && !(PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? rot(d.ql) : rot(d.q);
+                Fx = fz * col2(Rs);
+            }
+            if (C.disturbances) {   // world-frame force on link 4 at posObj = self.pos (532-544)
+                const U4 u = draw(a.seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), idx);
+                const V3<Real> fd = v3(C.dist_lo[0] + (C.dist_hi[0] - C.dist_lo[0]) * Real(u01(u.a)),
+                                       C.dist_lo[1] + (C.dist_hi[1] - C.dist_lo[1]) * Real(u01(u.b)),
+                                       C.dist_lo[2] + (C.dist_hi[2] - C.dist_lo[2]) * Real(u01(u.c)));
+                const V3<Real> lo = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? d.pos : d.lpos;
+                Fx = Fx + fd;
+                Tx = cross(d.kpos - lo, fd);
+            }
+            race_pyb_substep<Real, PH>(C, d, Fx, Tx);
+        }
+        d.kpos = d.pos;
+        if (d.flags & 1) {      // eliminated: motors off (233-235)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d.rpm[k] = d.prev[k] = Real(0);
+        } else {
+            Real noise[4] = {Real(0), Real(0), Real(0), Real(0)};
+            if (C.disturbances) {
+                const U4 u = draw(a.seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
+                const uint32_t x[4] = {u.a, u.b, u.c, u.d};
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    const Real u1 = (Real(x[2 * p] >> 8) + Real(1)) * Real(1.0 / 16777216.0);
+                    const Real u2 = Real(x[2 * p + 1] >> 8) * Real(1.0 / 16777216.0);
+                    const Real r = sqrt_(Real(-2) * log(u1));
+                    Real sn, cs;
+                    sincos_(Real(6.283185307179586) * u2, &sn, &cs);
+                    noise[2 * p] = r * cs * C.noise_std;
+                    noise[2 * p + 1] = r * sn * C.noise_std;
+                }
+            }
+            mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz(d.q), noise);
+        }
+    }
+    // ---- _gate_progress (471-506): rays of my current gate vs every drone of the env ----
+    V3<Real> gpos[ADRP_MAX_DRONES];
+    Q4<Real> gq[ADRP_MAX_DRONES];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        gpos[k] = v3(shfl_(d.pos.x, k, G), shfl_(d.pos.y, k, G), shfl_(d.pos.z, k, G));
+        gq[k] = {shfl_(d.q.x, k, G), shfl_(d.q.y, k, G), shfl_(d.q.z, k, G), shfl_(d.q.w, k, G)};
+    }
+    const int gate0 = d.gate;
+    if (C.num_gates > 0 && gate0 < C.num_gates) {
+        const Real gx = ld(a.f, RF_GATE + 4 * gate0, EN, slot), gy = ld(a.f, RF_GATE + 4 * gate0 + 1, EN, slot);
+        const Real rotg = ld(a.f, RF_GATE + 4 * gate0 + 3, EN, slot);
+        const Real h = C.gate_type[gate0] == 0 ? Real(1.0) : Real(0.525), half = Real(0.1875);
+        Real sn, cs;
+        sincos_(rotg, &sn, &cs);
+        const Real dx = Real(0.05) * cs, dy = Real(0.05) * sn;
+        bool passed = false;
+        for (int r = -3; r <= 3 && !passed; ++r) {
+            const V3<Real> p0 = v3(gx + Real(r) * dx, gy + Real(r) * dy, h - half);
+            const V3<Real> p1 = v3(gx + Real(r) * dx, gy + Real(r) * dy, h + half);
+            Real best = Real(2);
+            int who = -1;
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if (k < N) {
+                    const Shape<Real> sk = drone_shape(C, gpos[k], gq[k]);
+                    const Real fr = ray_cylinder(sk, p0, p1);
+                    if (fr < best) { best = fr; who = k; }
+                }
+            }
+            if (who == dn && best < Real(0.9999)) passed = true;
+        }
+        if (passed) d.gate += 1;
+    }
+    if (gate0 >= C.num_gates) d.flags |= 2;
+    // ---- obs row, elimination (674-698) ----
+    const V3<Real> wv = PH == ADRP_PHYS_DYN ? d.angv : d.w;
+    float* row = a.obs + slot * size_t(C.D);
+    Real row0[15];
+    race_obs_row(C, a.f, EN, slot, d.pos, d.q, d.vel, wv, d.gate, row, active, row0);
+    if (C.compete && active) {   // other drones' pos + rpy (653-659)
+        int idx = 0;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            if (k < N && k != dn) {
+                const V3<Real> orpy = euler_xyz(gq[k]);
+                float* p = row + 49 + 6 * idx;
+                p[0] = float(gpos[k].x); p[1] = float(gpos[k].y); p[2] = float(gpos[k].z);
+                p[3] = float(orpy.x); p[4] = float(orpy.y); p[5] = float(orpy.z);
+                ++idx;
+            }
+        }
+    }
+    bool crashed = false;
+    {
+        const Shape<Real> ds = drone_shape(C, d.pos, d.q);
+        for (int g = 0; g < C.num_gates && !crashed; ++g) {
+            const V3<Real> org = v3(ld(a.f, RF_GATE + 4 * g, EN, slot), ld(a.f, RF_GATE + 4 * g + 1, EN, slot),
+                                    ld(a.f, RF_GATE + 4 * g + 2, EN, slot));
+            crashed = gate_distance(ds, org, ld(a.f, RF_GATE + 4 * g + 3, EN, slot), C.gate_type[g] > 0, Real(1e-6)) < Real(1e-6);
+        }
+        for (int k = 0; k < C.num_obstacles && !crashed; ++k) {
+            const V3<Real> org = v3(ld(a.f, RF_OBST + 3 * k, EN, slot), ld(a.f, RF_OBST + 3 * k + 1, EN, slot),
+                                    ld(a.f, RF_OBST + 3 * k + 2, EN, slot));
+            crashed = obst_distance(ds, org, Real(1e-6)) < Real(1e-6);
+        }
+        const M3<Real>& R = ds.R;
+        const Real low = ds.c.z - ds.h.z * fabs_(R.a22) - ds.r * sqrt_(R.a02 * R.a02 + R.a12 * R.a12);
+        if (low <= Real(1e-6)) crashed = true;
+        if (C.compete) {
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if (k < N && k != dn && !crashed) {
+                    const Shape<Real> sk = drone_shape(C, gpos[k], gq[k]);
+                    crashed = gjk_distance(ds, sk) < Real(1e-6);
+                }
+            }
+        }
+    }
+    const bool oob = fabs_(d.pos.x) > C.bounds[0] || fabs_(d.pos.y) > C.bounds[1] || fabs_(d.pos.z) > C.bounds[2];
+    const bool unstable = fabs_(wv.x) > Real(20) || fabs_(wv.y) > Real(20) || fabs_(wv.z) > Real(20);
+    if (oob || unstable || crashed) d.flags |= 1;
+    // per-env reduction over the drone lanes
+    const int mydone = ((d.flags & 1) || (d.flags & 2)) ? 1 : 0, myfin = (d.flags & 2) ? 1 : 0;
+    int all_done = 1, all_fin = 1;
+    for (int k = 0; k < N; ++k) {
+        all_done &= __shfl(mydone, k, G);
+        all_fin &= __shfl(myfin, k, G);
+    }
+    const bool te = all_done != 0;
+    const bool tr = sc0 >= C.trunc_steps;   // step_counter / PYB_FREQ > episode_len_sec, before += S
+    // ---- RewardWrapper (wrapper.py:121-186), drone 0 ----
+    float reward = 0.0f;
+    int wr_gate = a.ist[RI_WR_GATE * EN + slot];
+    if (C.reward_wrapper && dn == 0) {
+        const int gate_id = d.gate;
+        Real tgt[3] = {ld(a.f, RF_WR_TARGET, EN, slot), ld(a.f, RF_WR_TARGET + 1, EN, slot), ld(a.f, RF_WR_TARGET + 2, EN, slot)};
+        const Real prv[3] = {ld(a.f, RF_WR_PREV, EN, slot), ld(a.f, RF_WR_PREV + 1, EN, slot), ld(a.f, RF_WR_PREV + 2, EN, slot)};
+        Real r_passed = 0;
+        if (gate_id > wr_gate % 4) {
+            wr_gate = gate_id;
+            if (gate_id < 4 && gate_id < C.num_gates)
+                for (int k = 0; k < 3; ++k) tgt[k] = row0[3 + 3 * gate_id + k];
+            r_passed = Real(5);
+        }
+        const Real r_col = (te && !all_fin) ? Real(-1) : Real(0), r_lab = (te && all_fin) ? Real(10) : Real(0);
+        const Real pxy = sqrt_((tgt[0] - prv[0]) * (tgt[0] - prv[0]) + (tgt[1] - prv[1]) * (tgt[1] - prv[1]));
+        const Real cxy = sqrt_((tgt[0] - row0[0]) * (tgt[0] - row0[0]) + (tgt[1] - row0[1]) * (tgt[1] - row0[1]));
+        const Real pz = fabs_(tgt[2] - prv[2]), cz = fabs_(tgt[2] - row0[2]);
+        reward = float((pxy - cxy) + (pz - cz) + r_passed + r_col + r_lab);
+        if (active)
+            for (int k = 0; k < 3; ++k) { st(a.f, RF_WR_TARGET + k, EN, slot, tgt[k]); st(a.f, RF_WR_PREV + k, EN, slot, row0[k]); }
+    }
+    if (!active) return;
+    if (dn == 0) {
+        a.rew[e] = reward;
+        a.term[e] = te;
+        a.trunc[e] = tr;
+    }
+    if (C.autoreset && (te || tr)) {
+        if (a.tobs) {
+            float* trow = a.tobs + slot * size_t(C.D);
+            for (int k = 0; k < C.D; ++k) trow[k] = row[k];
+        }
+        race_reset_lane(a, C, e, dn, EN, slot, episode, row);
+        return;
+    }
+    store_drone(a, EN, slot, d, false);
+    a.ist[RI_STEP * EN + slot] = sc0 + C.S;
+    if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
+}
+
+// reset kernel (MultiRaceAviary.reset): masked envs, one lane per drone
+template <typename Real>
+__global__ void __launch_bounds__(kRaceBlock) race_reset_kernel(RaceArgs<Real> a) {
+    const RaceConst<Real>& C = *a.c;
+    const int lane = blockIdx.x * kRaceBlock + threadIdx.x;
+    const int e = lane / C.N, dn = lane % C.N;
+    if (e >= a.E || (a.mask && !a.mask[e])) return;
+    const size_t EN = size_t(a.E) * C.N, slot = size_t(e) * C.N + dn;
+    const int episode = a.ist[RI_EPISODE * EN + slot];
+    race_reset_lane(a, C, e, dn, EN, slot, episode, a.obs + slot * size_t(C.D));
+}
+
+}  // namespace adrp

@@ -1,0 +1,139 @@
+"""MultiRaceAviary on the GPU: E envs x N drones, one fused HIP launch per env.step.
+
+Mirrors envs/MultiRaceAviary.py:26-725 of the reference: the same constructor
+arguments (race_config, drone_model, num_drones, physics, pyb_freq, ctrl_freq, gui,
+record, racemode, obs, act), per-env spaces (action Box [-1,1]^(N,4); obs Box
+(N, 49 [+ 6(N-1) COMPETE]) with the reference bounds), FULLSTATE actions (absolute target
+x, y, z, yaw per drone), obs layout [pos, rpy, vel, ang_v | 4 x gate x,y,z,yaw | 4 gate
+in-range flags | 4 x obstacle x,y,z | 4 flags | current gate (| others' pos+rpy)],
+terminated = every drone eliminated or finished, truncated after episode_len_sec.
+The reference returns reward 0; ``reward="wrapper"`` computes utils/wrapper.py's
+RewardWrapper instead.  The Mellinger controllers that the reference runs in one OS
+process per drone are fused into the kernel (500 Hz).
+
+Batched extras: ``num_envs``, ``device``, ``precision``, ``seed``, ``autoreset``,
+``env_offset``, ``link_frame_lag``.  step/reset return persistent device tensors.
+"""
+import numpy as np
+import torch
+
+from .. import _lib
+from ..utils import abi
+from ..utils.enums import ActionType, DroneModel, ObservationType, Physics, PHYSICS_CODE, RaceMode
+from ..utils.spaces import Box
+from .tracks import fill_track
+
+
+class MultiRaceAviary:
+    """Batched counterpart of gym_pybullet_adrp.envs.MultiRaceAviary."""
+
+    def __init__(self, race_config="level0", drone_model: DroneModel = DroneModel.CF2X, num_drones: int = 2,
+                 physics: Physics = Physics.PYB, pyb_freq: int = 500, ctrl_freq: int = 25, gui=False, record=False,
+                 racemode: RaceMode = RaceMode.COMPARE, obs: ObservationType = ObservationType.KIN,
+                 act: ActionType = ActionType.PID, *, num_envs: int = 1, device: int = 0, precision: str = "fp32",
+                 seed: int = 0, autoreset: bool = True, env_offset: int = 0, link_frame_lag: bool = True,
+                 reward: str = "env"):
+        if drone_model not in (DroneModel.CF2X,):
+            raise ValueError(f"DroneModel {drone_model} not supported (cf2x_IROS.urdf constants only)")
+        if gui or record:
+            raise ValueError("GUI / video recording are out of scope (DESIGN.md)")
+        if obs != ObservationType.KIN:
+            raise ValueError("only ObservationType.KIN is supported")
+        if pyb_freq % ctrl_freq != 0:
+            raise ValueError("[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.")
+        if reward not in ("env", "wrapper"):
+            raise ValueError("reward must be 'env' (MultiRaceAviary._computeReward) or 'wrapper' (RewardWrapper)")
+        cfg = _lib.default_config(abi.TASK_RACE)
+        cfg.num_drones = int(num_drones)
+        self.config = fill_track(cfg, race_config, int(num_drones))
+        cfg.physics = PHYSICS_CODE[physics]
+        cfg.race_mode = abi.RACE_COMPETE if racemode == RaceMode.COMPETE else abi.RACE_COMPARE
+        cfg.num_envs = int(num_envs)
+        cfg.pyb_freq, cfg.ctrl_freq = int(pyb_freq), int(ctrl_freq)
+        cfg.autoreset = 1 if autoreset else 0
+        cfg.precision = {"fp32": 0, "fp64": 1}[precision]
+        cfg.link_frame_lag = 1 if link_frame_lag else 0
+        cfg.seed = int(seed) & (2 ** 64 - 1)
+        cfg.env_offset = int(env_offset)
+        cfg.track.reward_wrapper = 1 if reward == "wrapper" else 0
+        self.cfg = cfg
+        self.h = _lib.Handle(cfg, device)
+        self.device = self.h.device
+        # reference attributes
+        self.DRONE_MODEL, self.PHYSICS, self.racemode = drone_model, physics, racemode
+        self.observation_type, self.action_type = obs, act
+        self.NUM_DRONES = int(num_drones)
+        self.PYB_FREQ, self.CTRL_FREQ = int(pyb_freq), int(ctrl_freq)
+        self.PYB_STEPS_PER_CTRL = self.PYB_FREQ // self.CTRL_FREQ
+        self.PYB_TIMESTEP, self.CTRL_TIMESTEP = 1.0 / self.PYB_FREQ, 1.0 / self.CTRL_FREQ
+        self.num_gates = cfg.track.num_gates
+        self.env_bounds = np.array([[-cfg.track.bounds_hi[0], -cfg.track.bounds_hi[1], 0.0],
+                                    list(cfg.track.bounds_hi)])
+        self.action_scale = np.array([1, 1, 1, np.pi])
+        self.num_envs = cfg.num_envs
+        self.action_space = self._actionSpace()
+        self.observation_space = self._observationSpace()
+        E, N, D = self.num_envs, self.NUM_DRONES, self.h.D
+        self._obs = torch.zeros((E, N, D), dtype=torch.float32, device=self.device)
+        self._tobs = torch.zeros_like(self._obs)
+        self._rew = torch.zeros(E, dtype=torch.float32, device=self.device)
+        self._term = torch.zeros(E, dtype=torch.bool, device=self.device)
+        self._trunc = torch.zeros(E, dtype=torch.bool, device=self.device)
+        self._act_shape = (E, N, 4)
+        self._info = {"answer": 42, "terminal_observation": self._tobs}
+
+    # ---- spaces (MultiRaceAviary.py:284-343) ----
+    def _actionSpace(self):
+        lim = np.ones((self.NUM_DRONES, 4))
+        return Box(low=-1 * lim, high=lim, dtype=float)
+
+    def _observationSpace(self):
+        lo = np.concatenate([[-5] * 3, [-np.pi] * 3, [-10] * 3, [-10] * 3, [-5, -5, -5, -np.pi] * 4, [-1] * 4,
+                             [-5] * 12, [-1] * 4, [-1]])
+        hi = np.concatenate([[5] * 3, [np.pi] * 3, [10] * 3, [10] * 3, [5, 5, 5, np.pi] * 4, [1] * 4,
+                             [5] * 12, [1] * 4, [4]])
+        if self.racemode == RaceMode.COMPETE:
+            lo = np.concatenate([lo, ([-5] * 3 + [-np.pi] * 3) * (self.NUM_DRONES - 1)])
+            hi = np.concatenate([hi, ([5] * 3 + [np.pi] * 3) * (self.NUM_DRONES - 1)])
+        return Box(low=np.vstack([lo] * self.NUM_DRONES), high=np.vstack([hi] * self.NUM_DRONES), dtype=np.float64)
+
+    # ---- gymnasium-style API, batched ----
+    def reset(self, seed: int = None, options: dict = None, mask=None):
+        """Reset all envs (or those with mask[e] != 0). Returns (obs [E,N,D], info)."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        self.h.reset(self._obs, m)
+        return self._obs, {"answer": 42}
+
+    def step(self, action):
+        """action [E,N,4]: absolute FULLSTATE target (x, y, z, yaw) per drone."""
+        act = action
+        if not (isinstance(act, torch.Tensor) and act.dtype == torch.float32 and act.device == self.device
+                and act.is_contiguous() and act.shape == self._act_shape):
+            act = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(self._act_shape)
+            act = act.contiguous()
+        self.h.step(act, self._obs, self._rew, self._term, self._trunc, self._tobs)
+        return self._obs, self._rew, self._term, self._trunc, self._info
+
+    def close(self):
+        self.h.close()
+
+    # ---- state ----
+    @property
+    def current_gate(self):
+        """[E, N] gate index of every drone (MultiRaceAviary.current_gate)"""
+        _, i = self.h.get_state()
+        return i[6].reshape(self.num_envs, self.NUM_DRONES)
+
+    def get_state(self):
+        return self.h.get_state()
+
+    def set_state(self, f, i):
+        self.h.set_state(f, i)
+
+    def state_field_names(self):
+        return self.h.field_names()
+
+    def step_bytes(self):
+        return self.h.step_bytes()

@@ -65,6 +65,7 @@ class AdrpTrack(ctypes.Structure):
         ("init_pqr", _arr(_d, MAX_DRONES, 3)),
         ("race_mass", _d),
         ("race_inertia", _arr(_d, 3)),
+        ("reward_wrapper", _i32),
     ]
 
 

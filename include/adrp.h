@@ -109,6 +109,8 @@ typedef struct adrp_track {
     double init_pqr[ADRP_MAX_DRONES][3];
     double race_mass;                                /* cf2x.urdf base mass used by changeDynamics (0.027) */
     double race_inertia[3];
+    int32_t reward_wrapper;                          /* 0: env reward (0, MultiRaceAviary.py:665-670);
+                                                        1: RewardWrapper (utils/wrapper.py:121-186) */
 } adrp_track;
 
 typedef struct adrp_config {

@@ -240,7 +240,23 @@ struct orc_handle {
     float* ring;            /* [E][buf][A] */
     uint8_t* contact;       /* [E] ground-model flag of the last step */
     int64_t contacts;
+    struct rdrone_s* rd;    /* [E*N] MultiRace per-drone state (race.c) */
+    struct renv_s* re;      /* [E] MultiRace per-env state */
 };
+
+/* MultiRaceAviary (race.c, included at the end of this file) */
+static int race_obs_dim(const adrp_config* c);
+static int race_alloc(orc_t* o);
+static void race_reset_env(orc_t* o, int e, float* obs_env);
+static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, float* rew, uint8_t* term,
+                          uint8_t* trunc, float* tobs_env);
+static const char* race_field_name(int k);
+static void race_get_row(const orc_t* o, size_t slot, int e, double* v, int32_t* iv);
+static void race_set_row(orc_t* o, size_t slot, int e, int first, const double* v, const int32_t* iv);
+#define RACE_NF 98
+#define RACE_NI 9
+static const char* k_race_i[RACE_NI] = {"step_counter", "episode", "tick", "last_att_tick", "last_pos_tick",
+                                         "tumble", "gate", "flags", "wr_gate"};
 
 int orc_obs_dim(const orc_t* o) { return o->D; }
 int orc_act_dim(const orc_t* o) { return o->A; }
@@ -249,7 +265,32 @@ uint8_t orc_env_contact(const orc_t* o, int e) { return o->contact[e]; }
 
 int orc_create(const adrp_config* cfg, orc_t** out) {
     if (!cfg || cfg->struct_size != sizeof(adrp_config)) return fail("struct_size mismatch");
-    if (cfg->task != ADRP_TASK_HOVER) return fail("oracle: only ADRP_TASK_HOVER is implemented");
+    if (cfg->task == ADRP_TASK_RACE) {
+        if (cfg->num_envs <= 0 || cfg->num_drones < 1 || cfg->num_drones > ADRP_MAX_DRONES) return fail("race: num_drones");
+        if (cfg->ctrl_freq <= 0 || cfg->pyb_freq % cfg->ctrl_freq != 0) return fail("pyb_freq is not divisible by env_freq");
+        if (cfg->act_type != ADRP_ACT_FULLSTATE) return fail("race act_type must be FULLSTATE");
+        if (cfg->physics < 0 || cfg->physics > ADRP_PHYS_PYB_GND_DRAG_DW) return fail("physics");
+        if (cfg->track.num_gates < 0 || cfg->track.num_gates > ADRP_MAX_GATES ||
+            cfg->track.num_obstacles < 0 || cfg->track.num_obstacles > ADRP_MAX_OBSTACLES) return fail("track size");
+        orc_t* o = (orc_t*)calloc(1, sizeof *o);
+        o->cfg = *cfg;
+        o->E = cfg->num_envs; o->N = cfg->num_drones; o->A = 4;
+        o->D = race_obs_dim(cfg);
+        o->S = cfg->pyb_freq / cfg->ctrl_freq;
+        o->dt = 1.0 / cfg->pyb_freq;
+        double dc[6];
+        orc_derived_constants(cfg, dc);
+        o->hover_rpm = dc[0]; o->max_rpm = dc[1]; o->gnd_clip = dc[3];
+        o->b = (body_t*)calloc((size_t)o->E * o->N, sizeof(body_t));
+        o->step_counter = (int32_t*)calloc(o->E, 4);
+        o->episode = (int32_t*)calloc(o->E, 4);
+        o->ring_head = (int32_t*)calloc(o->E, 4);
+        o->contact = (uint8_t*)calloc(o->E, 1);
+        race_alloc(o);
+        *out = o;
+        return ADRP_OK;
+    }
+    if (cfg->task != ADRP_TASK_HOVER) return fail("unknown task");
     if (cfg->num_envs <= 0 || cfg->num_drones != 1) return fail("hover: num_envs > 0, num_drones == 1");
     if (cfg->ctrl_freq <= 0 || cfg->pyb_freq % cfg->ctrl_freq != 0)
         return fail("pyb_freq is not divisible by env_freq");
@@ -279,7 +320,7 @@ int orc_create(const adrp_config* cfg, orc_t** out) {
 void orc_destroy(orc_t* o) {
     if (!o) return;
     free(o->b); free(o->step_counter); free(o->episode); free(o->ring_head); free(o->ring);
-    free(o->contact); free(o);
+    free(o->contact); free(o->rd); free(o->re); free(o);
 }
 
 /* ---- per-link external force accumulators (what p.applyExternalForce/Torque build) ---- */
@@ -589,6 +630,10 @@ static void hover_reset_env(orc_t* o, int e) {
 int orc_reset(orc_t* o, const uint8_t* mask, float* obs) {
     for (int e = 0; e < o->E; ++e) {
         if (mask && !mask[e]) continue;
+        if (o->cfg.task == ADRP_TASK_RACE) {
+            race_reset_env(o, e, obs ? obs + (size_t)e * o->N * o->D : NULL);
+            continue;
+        }
         hover_reset_env(o, e);
         if (obs) hover_obs(o, e, obs + (size_t)e * o->D);
     }
@@ -658,6 +703,13 @@ int orc_hover_eval(const orc_t* o, float* obs, float* rew, uint8_t* term, uint8_
 int orc_step(orc_t* o, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
              float* terminal_obs) {
     o->contacts = 0;
+    if (o->cfg.task == ADRP_TASK_RACE) {
+        const size_t row = (size_t)o->N * o->D;
+        for (int e = 0; e < o->E; ++e)
+            race_step_env(o, e, act + (size_t)e * o->N * 4, obs + e * row, rew + e, term + e, trunc + e,
+                          terminal_obs ? terminal_obs + e * row : NULL);
+        return ADRP_OK;
+    }
     for (int e = 0; e < o->E; ++e)
         hover_step_env(o, e, act + (size_t)e * o->A, obs + (size_t)e * o->D, rew + e, term + e, trunc + e,
                        terminal_obs ? terminal_obs + (size_t)e * o->D : NULL);
@@ -674,12 +726,17 @@ static const char* k_hover_i[] = {"step_counter", "episode", "ring_head"};
 #define HOVER_NF_BASE 24
 
 int orc_state_layout(const orc_t* o, int* nf, int* ni) {
+    if (o->cfg.task == ADRP_TASK_RACE) { *nf = RACE_NF; *ni = RACE_NI; return ADRP_OK; }
     *nf = HOVER_NF_BASE + o->cfg.action_buffer_size * o->A;
     *ni = 3;
     return ADRP_OK;
 }
 const char* orc_state_field(const orc_t* o, int is_int, int index) {
     static char buf[32];
+    if (o->cfg.task == ADRP_TASK_RACE) {
+        if (is_int) return (index >= 0 && index < RACE_NI) ? k_race_i[index] : NULL;
+        return race_field_name(index);
+    }
     if (is_int) return (index >= 0 && index < 3) ? k_hover_i[index] : NULL;
     if (index < 0) return NULL;
     if (index < HOVER_NF_BASE) return k_hover_f[index];
@@ -692,6 +749,17 @@ const char* orc_state_field(const orc_t* o, int is_int, int index) {
 int orc_get_state(const orc_t* o, double* f, int32_t* ii) {
     int nf, ni;
     orc_state_layout(o, &nf, &ni);
+    if (o->cfg.task == ADRP_TASK_RACE) {
+        const size_t EN = (size_t)o->E * o->N;
+        double v[RACE_NF];
+        int32_t iv[RACE_NI];
+        for (size_t slot = 0; slot < EN; ++slot) {
+            race_get_row(o, slot, (int)(slot / o->N), v, iv);
+            for (int k = 0; k < RACE_NF; ++k) f[k * EN + slot] = v[k];
+            for (int k = 0; k < RACE_NI; ++k) ii[k * EN + slot] = iv[k];
+        }
+        return ADRP_OK;
+    }
     const int E = o->E, B = o->cfg.action_buffer_size, A = o->A;
     for (int e = 0; e < E; ++e) {
         const body_t* b = &o->b[e];
@@ -711,6 +779,17 @@ int orc_get_state(const orc_t* o, double* f, int32_t* ii) {
 }
 
 int orc_set_state(orc_t* o, const double* f, const int32_t* ii) {
+    if (o->cfg.task == ADRP_TASK_RACE) {
+        const size_t EN = (size_t)o->E * o->N;
+        double v[RACE_NF];
+        int32_t iv[RACE_NI];
+        for (size_t slot = 0; slot < EN; ++slot) {
+            for (int k = 0; k < RACE_NF; ++k) v[k] = f[k * EN + slot];
+            for (int k = 0; k < RACE_NI; ++k) iv[k] = ii[k * EN + slot];
+            race_set_row(o, slot, (int)(slot / o->N), (int)(slot % o->N) == 0, v, iv);
+        }
+        return ADRP_OK;
+    }
     const int E = o->E, B = o->cfg.action_buffer_size, A = o->A;
     for (int e = 0; e < E; ++e) {
         body_t* b = &o->b[e];
@@ -795,3 +874,8 @@ int orc_tick_schedule(int n, uint8_t* ticks) {
 }
 
 uint32_t orc_config_size(void) { return (uint32_t)sizeof(adrp_config); }
+
+/* ------------------------------------------------------------------------------------ */
+/* MultiRaceAviary                                                                        */
+/* ------------------------------------------------------------------------------------ */
+#include "race.c"

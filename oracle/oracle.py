@@ -56,6 +56,11 @@ def _load():
     lib.orc_compute_pwms.argtypes = [P, P]
     lib.orc_pwms_to_rpms.argtypes = [P, P, P]
     lib.orc_tick_schedule.argtypes = [I, P]
+    lib.orc_race_body_distance.argtypes = [P, P, P, I, I, P]
+    lib.orc_race_body_distance.restype = D
+    lib.orc_shape_distance.argtypes = [P, P]
+    lib.orc_shape_distance.restype = D
+    lib.orc_lpf_coeffs.argtypes = [D, D, P]
     return lib
 
 
@@ -93,9 +98,12 @@ class Oracle:
         self.nf, self.ni = nf.value, ni.value
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().orc_destroy(self.h)
-            self.h = None
+        try:
+            if getattr(self, "h", None):
+                lib().orc_destroy(self.h)
+                self.h = None
+        except Exception:   # interpreter shutdown
+            pass
 
     def field_names(self):
         return ([lib().orc_state_field(self.h, 0, k).decode() for k in range(self.nf)],
@@ -208,4 +216,22 @@ def pwms_to_rpms(pwm, noise):
 def tick_schedule(n):
     o = np.zeros(n, np.uint8)
     lib().orc_tick_schedule(n, _ptr(o))
+    return o
+
+
+def race_body_distance(cfg, pos, quat, kind, gate_type, pose):
+    """drone collision cylinder at (pos, quat) vs gate (kind 0, type 0 tall / 1 low) or obstacle (kind 1)"""
+    return lib().orc_race_body_distance(ctypes.byref(cfg), _ptr(np.ascontiguousarray(pos, float)),
+                                        _ptr(np.ascontiguousarray(quat, float)), kind, gate_type,
+                                        _ptr(np.ascontiguousarray(pose, float)))
+
+
+def shape_distance(a, b):
+    """GJK distance; shape = [type(0 box, 1 cyl), c(3), R(9 row-major), h(3), r]"""
+    return lib().orc_shape_distance(_ptr(np.ascontiguousarray(a, float)), _ptr(np.ascontiguousarray(b, float)))
+
+
+def lpf_coeffs(fs, fc):
+    o = np.zeros(5)
+    lib().orc_lpf_coeffs(fs, fc, _ptr(o))
     return o
