@@ -405,6 +405,7 @@ __device__ __forceinline__ void store_drone(const RaceArgs<Real>& a, size_t EN, 
 // ---------------------------------------------------------------------------------------
 struct Lpf { float b0, b1, b2, a1, a2; };
 __device__ __forceinline__ float lpf_apply(const Lpf& l, float& d1, float& d2, float sample) {
+#pragma clang fp contract(off)   // the firmware is C float code built without FMA contraction
     float d0 = sample - d1 * l.a1 - d2 * l.a2;
     if (!isfinite(d0)) d0 = sample;
     const float out = d0 * l.b0 + d1 * l.b1 + d2 * l.b2;
@@ -418,6 +419,7 @@ template <typename Real>
 __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3], float xc_x, float xc_y,
                                              const float gyro[3], const float pos[3], const float vel[3],
                                              const float Rm[9]) {
+#pragma clang fp contract(off)
     const float dt = float(1.0f / 500);
     const float rx = sp[0] - pos[0], ry = sp[1] - pos[1], rz = sp[2] - pos[2];
     const float vx = 0.0f - vel[0], vy = 0.0f - vel[1], vz = 0.0f - vel[2];
@@ -475,6 +477,7 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
 template <typename Real>
 __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lpf, const float sp[3], float xc_x,
                                                   float xc_y, V3<Real> rpy, const Real noise[4]) {
+#pragma clang fp contract(off)   // numpy / C arithmetic of the reference wrapper and firmware
     const Real fdt = Real(0.002);
     const Real r2d = Real(57.29577951308232);
     Real rates[3];
@@ -792,9 +795,9 @@ __device__ __noinline__ void race_reset_lane(const RaceArgs<Real>& a, const Race
     }
     const V3<Real> nrpy = euler_xyz(nq);
     // RewardWrapper.reset: current_target = obs[0, 12:15], previous_pos = obs[0, :3]
-    for (int k = 0; k < 3; ++k) {
-        st(f, RF_WR_TARGET + k, EN, slot, C.num_gates > 0 ? row0[3 + k] : Real(0));
-        st(f, RF_WR_PREV + k, EN, slot, row0[k]);
+    for (int k = 0; k < 3; ++k) {   // per-env state, kept in drone 0's slot
+        st(f, RF_WR_TARGET + k, EN, slot, dn == 0 && C.num_gates > 0 ? row0[3 + k] : Real(0));
+        st(f, RF_WR_PREV + k, EN, slot, dn == 0 ? row0[k] : Real(0));
     }
     // controller reset with the initial obs; _drone_init
     RDrone<Real> d;
@@ -873,6 +876,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
     const float sp[3] = {av.x, av.y, av.z};
     float xc_x, xc_y;
     {
+#pragma clang fp contract(off)
         Real qs, qc;
         sincos_(Real(av.w) * Real(0.5), &qs, &qc);          // get_quaternion_from_euler(0, 0, yaw)
         const float qz = float(qs), qw = float(qc);
@@ -882,6 +886,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
     }
     Lpf lpf;
     {   // lpf2pInit(gyrolpf, 500, 30) (float)
+#pragma clang fp contract(off)
         const float fr = 500.0f / 30.0f;
         const float ohm = tanf(3.14159265358979323846f / fr);
         const float c = 1.0f + 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm;

@@ -849,10 +849,12 @@ static void race_get_row(const orc_t* o, size_t slot, int e, double* v, int32_t*
     memcpy(v, base, sizeof base);
     for (int g = 0; g < 4; ++g) for (int j = 0; j < 4; ++j) v[64 + 4 * g + j] = re->gate[g][j];
     for (int k = 0; k < 4; ++k) for (int j = 0; j < 3; ++j) v[80 + 3 * k + j] = re->obst[k][j];
-    for (int j = 0; j < 3; ++j) { v[92 + j] = re->wr_target[j]; v[95 + j] = re->wr_prev[j]; }
+    /* RewardWrapper state is per env and lives in drone 0's slot (0 elsewhere) */
+    const int lead = (slot % (size_t)o->N) == 0;
+    for (int j = 0; j < 3; ++j) { v[92 + j] = lead ? re->wr_target[j] : 0; v[95 + j] = lead ? re->wr_prev[j] : 0; }
     iv[0] = o->step_counter[e]; iv[1] = o->episode[e]; iv[2] = d->tick; iv[3] = d->last_att_tick;
     iv[4] = d->last_pos_tick; iv[5] = d->tumble; iv[6] = d->gate; iv[7] = (d->elim ? 1 : 0) | (d->fin ? 2 : 0);
-    iv[8] = re->wr_gate;
+    iv[8] = lead ? re->wr_gate : 0;
 }
 
 static void race_set_row(orc_t* o, size_t slot, int e, int first, const double* v, const int32_t* iv) {
