@@ -43,6 +43,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-allgather", action="store_true", help="N>1: skip the obs all-gather variant")
+    p.add_argument("--task", default="hover", choices=["hover", "race"],
+                   help="hover = BASELINE configs[1] (default); race = configs[2]/[3] (MultiRaceAviary)")
+    p.add_argument("--level", default="level0", help="race: track preset (level0 = config 3, level3 = config 4)")
+    p.add_argument("--drones", type=int, default=2, help="race: drones per env")
+    p.add_argument("--racemode", default="COMPARE", choices=["COMPARE", "COMPETE"])
     return p.parse_args()
 
 
@@ -51,12 +56,18 @@ def cpu_baseline(cfg, seconds):
     workload: 4096 envs stepped until ~`seconds` of CPU time."""
     from oracle import oracle as O
     c = cfg.copy()
-    c.num_envs = ENVS_PER_GPU
+    race = c.task == 1
+    c.num_envs = 256 if race else ENVS_PER_GPU
     c.env_offset = 0
     orc = O.Oracle(c)
-    orc.reset()
+    obs0 = orc.reset()
     rng = np.random.default_rng(1)
-    acts = rng.uniform(-1, 1, (8, c.num_envs, 1, 4)).astype(np.float32)
+    if race:
+        t = obs0[None, ..., :3] + rng.uniform(-0.3, 0.3, (8,) + obs0.shape[:2] + (3,))
+        t[..., 2] = np.clip(t[..., 2], 0.2, 1.5)
+        acts = np.concatenate([t, np.zeros(t.shape[:-1] + (1,))], -1).astype(np.float32)
+    else:
+        acts = rng.uniform(-1, 1, (8, c.num_envs, 1, 4)).astype(np.float32)
     orc.step(acts[0])                     # warm
     steps, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -85,9 +96,15 @@ def main():
     from gym_pybullet_adrp_amd.utils.enums import Physics
 
     E = args.envs
-    make = functools.partial(HoverAviary, physics=Physics[args.physics], device=local, precision=args.precision,
-                             seed=2024, initial_xyzs=[0, 0, 1.0],
-                             init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1})
+    if args.task == "race":
+        from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary
+        from gym_pybullet_adrp_amd.utils.enums import RaceMode
+        make = functools.partial(MultiRaceAviary, args.level, num_drones=args.drones, physics=Physics[args.physics],
+                                 racemode=RaceMode[args.racemode], device=local, precision=args.precision, seed=2024)
+    else:
+        make = functools.partial(HoverAviary, physics=Physics[args.physics], device=local, precision=args.precision,
+                                 seed=2024, initial_xyzs=[0, 0, 1.0],
+                                 init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1})
     sharded = None
     if world > 1:
         from gym_pybullet_adrp_amd.sharding import ShardedAviary
@@ -96,11 +113,20 @@ def main():
     else:
         env = make(num_envs=E, env_offset=0)
     dev = env.device
-    env.reset()
+    obs0, _ = env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(1 + rank)
     nbuf = 64
-    acts = (torch.rand((nbuf, E, 1, 4), generator=gen, device=dev) * 2 - 1).contiguous()
+    if args.task == "race":
+        # FULLSTATE targets = start + U(+-0.3) m, z clipped to [0.2, 1.5], yaw 0
+        # (re-drawn per buffer slot)
+        N = args.drones
+        off = (torch.rand((nbuf, E, N, 3), generator=gen, device=dev) * 0.6 - 0.3)
+        tgt = obs0[..., :3].unsqueeze(0) + off
+        tgt[..., 2] = tgt[..., 2].clamp(0.2, 1.5)
+        acts = torch.cat([tgt, torch.zeros((nbuf, E, N, 1), device=dev)], -1).contiguous()
+    else:
+        acts = (torch.rand((nbuf, E, 1, 4), generator=gen, device=dev) * 2 - 1).contiguous()
     for k in range(args.warmup):
         env.step(acts[k % nbuf])
     torch.cuda.synchronize()
@@ -181,7 +207,8 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as fh:
             rec = json.load(fh)
-        key = f"{args.physics}_{args.precision}_{E}"
+        key = f"{args.physics}_{args.precision}_{E}" if args.task == "hover" else \
+            f"race_{args.level}_{args.drones}_{args.physics}_{args.precision}_{E}"
         if key in rec:
             traffic = rec[key]["hbm_bytes_per_launch"]
     result = {
@@ -210,6 +237,13 @@ def main():
     }
     if allgather is not None:
         result["with_obs_allgather"] = allgather
+    if args.task == "race":
+        result["config"] = {"workload": f"MultiRaceAviary {args.racemode} {args.level}, {args.drones} drones x {E} envs "
+                                        f"per GPU, Physics.{args.physics} 500/25 Hz (20 sub-steps, Mellinger 500 Hz)",
+                            "envs_per_gpu": E, "global_envs": E * world, "drones_per_env": args.drones,
+                            "parallelism": f"env-sharded dp{world}"}
+        result["data"] = "synthetic: level preset resets (device Philox), FULLSTATE targets start + U(+-0.3) m"
+        result["drone_steps_per_s"] = result["value"] * args.drones
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(env.cfg, args.cpu_seconds)
     elif rank == 0:

@@ -327,7 +327,9 @@ struct RDrone {
     float pw_roll, pw_pitch, psp_roll, psp_pitch;
     float ctl[4];
     Real mass, inertia[3];
+    Real inv_mass, inv_i[3];        // per env.step
     int tick, last_att, last_pos, tumble, gate, flags;
+    double t_att, t_pos;            // last_att_pid_call / last_pos_pid_call (float64, MellingerControl.py:395-407)
 };
 
 template <typename Real>
@@ -364,6 +366,11 @@ __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, s
     d.tick = ist[RI_TICK * EN + slot]; d.last_att = ist[RI_LAST_ATT * EN + slot];
     d.last_pos = ist[RI_LAST_POS * EN + slot]; d.tumble = ist[RI_TUMBLE * EN + slot];
     d.gate = ist[RI_GATE * EN + slot]; d.flags = ist[RI_FLAGS * EN + slot];
+    d.t_att = double(d.last_att) / 500.0;
+    d.t_pos = double(d.last_pos) / 500.0;
+    d.inv_mass = Real(1) / d.mass;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d.inv_i[k] = Real(1) / d.inertia[k];
 }
 
 template <typename Real>
@@ -478,6 +485,7 @@ template <typename Real>
 __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lpf, const float sp[3], float xc_x,
                                                   float xc_y, V3<Real> rpy, const Real noise[4]) {
 #pragma clang fp contract(off)   // numpy / C arithmetic of the reference wrapper and firmware
+    constexpr bool F32 = sizeof(Real) == 4;   // fp32 kernel: reciprocal multiplies; fp64: numpy's divisions
     const Real fdt = Real(0.002);
     const Real r2d = Real(57.29577951308232);
     Real rates[3];
@@ -486,9 +494,11 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
     Real acc_z = 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        rates[k] = (rr[k] - d.prev_rpy[k]) / fdt;
+        rates[k] = F32 ? (rr[k] - d.prev_rpy[k]) * Real(500) : (rr[k] - d.prev_rpy[k]) / fdt;
         d.prev_rpy[k] = rr[k];
-        if (k == 2) acc_z = (vv[k] - d.prev_vel[k]) / fdt / Real(9.8) + Real(1);
+        if (k == 2)
+            acc_z = F32 ? (vv[k] - d.prev_vel[k]) * Real(500.0 / 9.8) + Real(1)
+                        : (vv[k] - d.prev_vel[k]) / fdt / Real(9.8) + Real(1);
         d.prev_vel[k] = vv[k];
     }
     float gyro[3];
@@ -501,20 +511,33 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
         pwm[0] = pwm[1] = pwm[2] = pwm[3] = Real(0);
     } else {
         const double cur = double(d.tick) / 500.0;
-        const double la = double(d.last_att) / 500.0, lp = double(d.last_pos) / 500.0;
         int t;
-        if ((cur - la > 0.002) && (cur - lp > 0.01)) { t = 0; d.last_pos = d.tick; d.last_att = d.tick; }
-        else if (cur - la > 0.002) { d.last_att = d.tick; t = 2; }
-        else t = 1;
+        if ((cur - d.t_att > 0.002) && (cur - d.t_pos > 0.01)) {
+            t = 0; d.last_pos = d.tick; d.last_att = d.tick; d.t_pos = cur; d.t_att = cur;
+        } else if (cur - d.t_att > 0.002) {
+            d.last_att = d.tick; d.t_att = cur; t = 2;
+        } else {
+            t = 1;
+        }
         if ((t & 1) == 0) {   // RATE_DO_EXECUTE(500 Hz, tick)
-            // state: attitude quaternion from rpy -> rotation (quat2rotmat), position, velocity
-            float sr, cr, sp_, cp, sy, cy;
-            sincosf(float(rpy.x), &sr, &cr);
-            sincosf(float(rpy.y), &sp_, &cp);
-            sincosf(float(rpy.z), &sy, &cy);
-            const float Rm[9] = {cy * cp, cy * sp_ * sr - sy * cr, cy * sp_ * cr + sy * sr,
-                                 sy * cp, sy * sp_ * sr + cy * cr, sy * sp_ * cr - cy * sr,
-                                 -sp_, cp * sr, cp * cr};
+            // state.attitudeQuaternion = get_quaternion_from_euler(rpy) -> quat2rotmat: the body
+            // rotation itself, except in getEulerFromQuaternion's gimbal branches
+            float Rm[9];
+            const Real sarg = Real(-2) * (d.q.x * d.q.z - d.q.w * d.q.y);
+            if (fabs_(sarg) < Real(0.99999)) {
+                const M3<Real> Rq = rot(d.q);
+                Rm[0] = float(Rq.a00); Rm[1] = float(Rq.a01); Rm[2] = float(Rq.a02);
+                Rm[3] = float(Rq.a10); Rm[4] = float(Rq.a11); Rm[5] = float(Rq.a12);
+                Rm[6] = float(Rq.a20); Rm[7] = float(Rq.a21); Rm[8] = float(Rq.a22);
+            } else {
+                float sr, cr, sp_, cp, sy, cy;
+                sincosf(float(rpy.x), &sr, &cr);
+                sincosf(float(rpy.y), &sp_, &cp);
+                sincosf(float(rpy.z), &sy, &cy);
+                Rm[0] = cy * cp; Rm[1] = cy * sp_ * sr - sy * cr; Rm[2] = cy * sp_ * cr + sy * sr;
+                Rm[3] = sy * cp; Rm[4] = sy * sp_ * sr + cy * cr; Rm[5] = sy * sp_ * cr - cy * sr;
+                Rm[6] = -sp_; Rm[7] = cp * sr; Rm[8] = cp * cr;
+            }
             const float pos[3] = {float(d.pos.x), float(d.pos.y), float(d.pos.z)};
             const float vel[3] = {float(d.vel.x), float(d.vel.y), float(d.vel.z)};
             mellinger_fw(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
@@ -525,9 +548,10 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
         const Real m4[4] = {th - r + p + y, th - r - p - y, th + r - p + y, th + r + p - y};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const Real x = clampr_(m4[k], Real(0), Real(65535)) / Real(65535) * Real(60);
+            const Real x = F32 ? clampr_(m4[k], Real(0), Real(65535)) * Real(60.0 / 65535)
+                               : clampr_(m4[k], Real(0), Real(65535)) / Real(65535) * Real(60);
             const Real volts = Real(-0.0006239) * x * x + Real(0.088) * x;
-            Real pct = volts / Real(3);
+            Real pct = F32 ? volts * Real(1.0 / 3) : volts / Real(3);
             if (pct > Real(1)) pct = Real(1);
             pwm[k] = pct * Real(65535);
         }
@@ -543,7 +567,8 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
     for (int k = 0; k < 4; ++k) {
         Real t = th[3 - k] + noise[k];
         if (t < Real(0)) t = Real(0);
-        Real mp = (sqrt_(t / Real(1) / Real(3.16e-10)) - Real(4070.3)) / Real(0.2685);
+        Real mp = F32 ? (sqrt_(t * Real(1.0 / 3.16e-10)) - Real(4070.3)) * Real(1.0 / 0.2685)
+                      : (sqrt_(t / Real(1) / Real(3.16e-10)) - Real(4070.3)) / Real(0.2685);
         mp = clampr_(mp, Real(20000), Real(65535));
         d.prev[k] = d.rpm[k];
         d.rpm[k] = Real(0.2685) * mp + Real(4070.3);
@@ -592,7 +617,7 @@ __device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDron
             for (int i = 0; i < 4; ++i) {
                 Real h = d.pos.z + R.a20 * C.px[i] + R.a21 * C.py[i] + R.a22 * C.pz[i];
                 h = h < C.gnd_clip ? C.gnd_clip : h;
-                const Real k = C.prop_r4 / h;
+                const Real k = C.prop_r4 * rcp_(h);
                 const Real g = C.gnd_kf * d.rpm[i] * d.rpm[i] * k * k;
                 sg += g;
                 G = G + v3(g * C.px[i], g * C.py[i], g * C.pz[i]);
@@ -610,13 +635,14 @@ __device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDron
         Fw = Fw + (GND ? dw : mul(Rs, mulT(R, dw)));
     }
     const Real ixx = d.inertia[0], iyy = d.inertia[1], izz = d.inertia[2];
+    (void)0;
     const V3<Real> wb = mulT(R, d.w);
     const V3<Real> Iw = v3(ixx * wb.x, iyy * wb.y, izz * wb.z);
     const Real kw = Real(0.04) + Real(0.04) * sqrt_(dot(wb, wb));
     const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
-    const V3<Real> wdot = mul(R, v3(rhs.x / ixx, rhs.y / iyy, rhs.z / izz));
+    const V3<Real> wdot = mul(R, v3(rhs.x * d.inv_i[0], rhs.y * d.inv_i[1], rhs.z * d.inv_i[2]));
     const Real kv = Real(0.04) + Real(0.04) * sqrt_(dot(d.vel, d.vel));
-    const V3<Real> acc = (Real(1) / d.mass) * Fw - kv * d.vel;
+    const V3<Real> acc = d.inv_mass * Fw - kv * d.vel;
     d.w = v3(clamp100r(d.w.x + C.dt * wdot.x), clamp100r(d.w.y + C.dt * wdot.y), clamp100r(d.w.z + C.dt * wdot.z));
     d.vel = v3(clamp100r(d.vel.x + C.dt * acc.x), clamp100r(d.vel.y + C.dt * acc.y), clamp100r(d.vel.z + C.dt * acc.z));
     // forwardKinematics of this step caches the pre-integration pose
@@ -626,7 +652,7 @@ __device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDron
     Real ang = sqrt_(dot(d.w, d.w));
     if (ang > C.ang_max) ang = C.ang_max;
     Real sh, ch;
-    sincos_(Real(0.5) * ang * C.dt, &sh, &ch);
+    small_sincos(Real(0.5) * ang * C.dt, &sh, &ch);   // argument <= ANGULAR_MOTION_THRESHOLD / 2 = pi / 8
     const Real sc = ang < Real(0.001) ? Real(0.5) * C.dt - (C.dt * C.dt * C.dt) * Real(0.020833333333) * ang * ang
                                       : sh / ang;
     const V3<Real> ax = sc * d.w;
@@ -671,7 +697,8 @@ __device__ __forceinline__ void race_dyn_substep(const RaceConst<Real>& C, RDron
     if (!(wn <= Real(1e-8))) {
         const Real th = wn * C.dt * Real(0.5);
         Real s, c;
-        sincos_(th, &s, &c);
+        if (th <= Real(0.39269908169872414)) small_sincos(th, &s, &c);
+        else sincos_(th, &s, &c);
         const Real k = s / wn;
         const Q4<Real> q = d.q;
         d.q = {c * q.x + k * (w.z * q.y - w.y * q.z + w.x * q.w), c * q.y + k * (-w.z * q.x + w.x * q.z + w.y * q.w),
@@ -857,6 +884,23 @@ __device__ __noinline__ void race_reset_lane(const RaceArgs<Real>& a, const Race
 template <typename Real, int PH, int G>
 __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a) {
     const RaceConst<Real>& C = *a.c;
+    // register copy of the constants the sub-step loop reads (uniform -> SGPRs; no reloads
+    // behind the state stores, which the compiler cannot prove do not alias a.c)
+    RaceConst<Real> H;
+    H.S = C.S; H.link_lag = C.link_lag; H.disturbances = C.disturbances;
+    H.dt = C.dt; H.gravity = C.gravity; H.kf = C.kf; H.km = C.km;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { H.px[i] = C.px[i]; H.py[i] = C.py[i]; H.pz[i] = C.pz[i]; }
+    H.gnd_kf = C.gnd_kf; H.prop_r4 = C.prop_r4; H.gnd_clip = C.gnd_clip;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        H.drag[i] = C.drag[i]; H.dist_lo[i] = C.dist_lo[i]; H.dist_hi[i] = C.dist_hi[i];
+        H.dyn_i[i] = C.dyn_i[i]; H.dyn_inv_i[i] = C.dyn_inv_i[i];
+    }
+    H.dw1 = C.dw1; H.dw2 = C.dw2; H.dw3 = C.dw3; H.prop_r = C.prop_r;
+    H.dyn_mass = C.dyn_mass; H.dyn_inv_mass = C.dyn_inv_mass; H.dyn_arm = C.dyn_arm;
+    H.coll_hh = C.coll_hh; H.coll_r = C.coll_r; H.coll_zoff = C.coll_zoff; H.ang_max = C.ang_max;
+    H.noise_std = C.noise_std;
     const int lane = blockIdx.x * kRaceBlock + threadIdx.x;
     const int e_raw = lane / G, d_raw = lane % G;
     const int N = C.N;
@@ -894,11 +938,11 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
         lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
         lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
     }
-    for (int s = 0; s < C.S; ++s) {
+    for (int s = 0; s < H.S; ++s) {
         const uint32_t idx = uint32_t(sc0 + s);
         if (PH != ADRP_PHYS_PYB) d.kpos = d.pos;          // KIN_PHYSICS read-back
         if constexpr (PH == ADRP_PHYS_DYN) {
-            race_dyn_substep(C, d);
+            race_dyn_substep(H, d);
         } else {
             V3<Real> Fx = v3(Real(0), Real(0), Real(0)), Tx = v3(Real(0), Real(0), Real(0));
             if constexpr (PH == ADRP_PHYS_PYB_DW || PH == ADRP_PHYS_PYB_GND_DRAG_DW) {
@@ -909,24 +953,24 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                     const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
                     const Real dxy = sqrt_(dx * dx + dy * dy);
                     if (dz > Real(0) && dxy < Real(10)) {
-                        const Real kk = C.prop_r / (Real(4) * dz);
-                        const Real alpha = C.dw1 * kk * kk, beta = C.dw2 * dz + C.dw3;
+                        const Real kk = H.prop_r / (Real(4) * dz);
+                        const Real alpha = H.dw1 * kk * kk, beta = H.dw2 * dz + H.dw3;
                         fz -= alpha * exp_(Real(-0.5) * (dxy / beta) * (dxy / beta));
                     }
                 }
-                const M3<Real> Rs = C.link_lag && !(PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? rot(d.ql) : rot(d.q);
+                const M3<Real> Rs = H.link_lag && !(PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? rot(d.ql) : rot(d.q);
                 Fx = fz * col2(Rs);
             }
-            if (C.disturbances) {   // world-frame force on link 4 at posObj = self.pos (532-544)
+            if (H.disturbances) {   // world-frame force on link 4 at posObj = self.pos (532-544)
                 const U4 u = draw(a.seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), idx);
-                const V3<Real> fd = v3(C.dist_lo[0] + (C.dist_hi[0] - C.dist_lo[0]) * Real(u01(u.a)),
-                                       C.dist_lo[1] + (C.dist_hi[1] - C.dist_lo[1]) * Real(u01(u.b)),
-                                       C.dist_lo[2] + (C.dist_hi[2] - C.dist_lo[2]) * Real(u01(u.c)));
+                const V3<Real> fd = v3(H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * Real(u01(u.a)),
+                                       H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * Real(u01(u.b)),
+                                       H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * Real(u01(u.c)));
                 const V3<Real> lo = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? d.pos : d.lpos;
                 Fx = Fx + fd;
                 Tx = cross(d.kpos - lo, fd);
             }
-            race_pyb_substep<Real, PH>(C, d, Fx, Tx);
+            race_pyb_substep<Real, PH>(H, d, Fx, Tx);
         }
         d.kpos = d.pos;
         if (d.flags & 1) {      // eliminated: motors off (233-235)
@@ -934,7 +978,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
             for (int k = 0; k < 4; ++k) d.rpm[k] = d.prev[k] = Real(0);
         } else {
             Real noise[4] = {Real(0), Real(0), Real(0), Real(0)};
-            if (C.disturbances) {
+            if (H.disturbances) {
                 const U4 u = draw(a.seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
                 const uint32_t x[4] = {u.a, u.b, u.c, u.d};
 #pragma unroll
@@ -944,8 +988,8 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                     const Real r = sqrt_(Real(-2) * log(u1));
                     Real sn, cs;
                     sincos_(Real(6.283185307179586) * u2, &sn, &cs);
-                    noise[2 * p] = r * cs * C.noise_std;
-                    noise[2 * p + 1] = r * sn * C.noise_std;
+                    noise[2 * p] = r * cs * H.noise_std;
+                    noise[2 * p + 1] = r * sn * H.noise_std;
                 }
             }
             mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz(d.q), noise);

@@ -61,6 +61,13 @@ def _load():
     lib.orc_shape_distance.argtypes = [P, P]
     lib.orc_shape_distance.restype = D
     lib.orc_lpf_coeffs.argtypes = [D, D, P]
+    lib.orc_race_obs_assemble.argtypes = [P, I, I, P, P, P, P, P, I, P]
+    lib.orc_race_terminated.argtypes = [P, I, P, P, P, P, P]
+    lib.orc_race_truncated.argtypes = [P, I]
+    lib.orc_race_rays.argtypes = [P, I, P, P]
+    lib.orc_race_progress.argtypes = [I, I, P, P, P, P]
+    lib.orc_race_reward.argtypes = [P, P, P, P, I, I]
+    lib.orc_race_reward.restype = D
     return lib
 
 
@@ -235,3 +242,55 @@ def lpf_coeffs(fs, fc):
     o = np.zeros(5)
     lib().orc_lpf_coeffs(fs, fc, _ptr(o))
     return o
+
+
+def race_obs_assemble(cfg, i, kin, gate_act, gate_in, obst_act, obst_in, current_gate):
+    """MultiRaceAviary._computeObs assembly for drone i given the range-test outcomes"""
+    N = kin.shape[0]
+    D = 49 + (6 * (N - 1) if cfg.race_mode == 1 else 0)
+    row = np.zeros(D)
+    rc = lib().orc_race_obs_assemble(ctypes.byref(cfg), N, i, _ptr(np.ascontiguousarray(kin, float)),
+                                     _ptr(np.ascontiguousarray(gate_act, float)), _ptr(np.ascontiguousarray(gate_in, np.uint8)),
+                                     _ptr(np.ascontiguousarray(obst_act, float)), _ptr(np.ascontiguousarray(obst_in, np.uint8)),
+                                     int(current_gate), _ptr(row))
+    assert rc == 0
+    return row
+
+
+def race_terminated(cfg, pos, angv, contact, elim, fin):
+    """-> (terminated, updated eliminated flags)"""
+    e = np.ascontiguousarray(elim, np.uint8).copy()
+    t = lib().orc_race_terminated(ctypes.byref(cfg), len(e), _ptr(np.ascontiguousarray(pos, float)),
+                                  _ptr(np.ascontiguousarray(angv, float)), _ptr(np.ascontiguousarray(contact, np.uint8)),
+                                  _ptr(e), _ptr(np.ascontiguousarray(fin, np.uint8)))
+    return bool(t), e.astype(bool)
+
+
+def race_truncated(cfg, step_counter):
+    return bool(lib().orc_race_truncated(ctypes.byref(cfg), int(step_counter)))
+
+
+def race_rays(gate_xyyaw, gate_type):
+    fr = np.zeros((7, 3)); to = np.zeros((7, 3))
+    lib().orc_race_rays(_ptr(np.ascontiguousarray(gate_xyyaw, float)), int(gate_type), _ptr(fr), _ptr(to))
+    return fr, to
+
+
+def race_progress(num_gates, self_id, hit_id, hit_frac, gate):
+    g = ctypes.c_int(int(gate)); f = ctypes.c_int(0)
+    lib().orc_race_progress(int(num_gates), int(self_id), _ptr(np.ascontiguousarray(hit_id, np.int32)),
+                            _ptr(np.ascontiguousarray(hit_frac, float)), ctypes.byref(g), ctypes.byref(f))
+    return g.value, bool(f.value)
+
+
+class RewardWrapperState:
+    """RewardWrapper internal state (current_gate_id, current_target, previous_pos)"""
+
+    def __init__(self, obs0_row):
+        self.gate = ctypes.c_int(int(obs0_row[48]))
+        self.target = np.ascontiguousarray(obs0_row[12:15], float).copy()
+        self.prev = np.ascontiguousarray(obs0_row[:3], float).copy()
+
+    def step(self, row0, term, completed):
+        return lib().orc_race_reward(ctypes.byref(self.gate), _ptr(self.target), _ptr(self.prev),
+                                     _ptr(np.ascontiguousarray(row0, float)), int(term), int(completed))

@@ -497,6 +497,44 @@ static void gate_pose(const renv_t* re, int g, v3* origin, m33* R) {
     *R = rot_z(re->gate[g][3]);   /* loadURDF(..., getQuaternionFromEuler([0, 0, yaw])) */
 }
 
+/* _computeObs assembly (MultiRaceAviary.py:597-661) for drone i from the drones' kinematic
+   rows kin[k] = [pos, rpy, vel, ang_v], the actual gate (x,y,z,yaw) / obstacle (x,y,z) poses
+   and the getClosestPoints(..., VISIBILITY_RANGE) outcomes */
+static void race_obs_assemble(const adrp_config* c, int N, int i, const double (*kin)[12], const double gate_act[][4],
+                              const uint8_t* gate_in, const double obst_act[][3], const uint8_t* obst_in,
+                              int current_gate, double* row) {
+    const adrp_track* t = &c->track;
+    memset(row, 0, sizeof(double) * race_obs_dim(c));
+    memcpy(row, kin[i], sizeof(double) * 12);
+    for (int g = 0; g < t->num_gates; ++g) {
+        if (gate_in[g]) { for (int j = 0; j < 4; ++j) row[12 + 4 * g + j] = gate_act[g][j]; }
+        else { row[12 + 4 * g] = t->gates[g][0]; row[13 + 4 * g] = t->gates[g][1]; row[14 + 4 * g] = t->gates[g][2]; row[15 + 4 * g] = t->gates[g][5]; }
+        row[28 + g] = gate_in[g] ? 1 : 0;
+    }
+    for (int k = 0; k < t->num_obstacles; ++k) {
+        for (int j = 0; j < 3; ++j) row[32 + 3 * k + j] = obst_in[k] ? obst_act[k][j] : t->obstacles[k][j];
+        row[44 + k] = obst_in[k] ? 1 : 0;
+    }
+    row[48] = current_gate;
+    if (c->race_mode == ADRP_RACE_COMPETE) {
+        int idx = 0;
+        for (int k = 0; k < N; ++k) {
+            if (k == i) continue;
+            double* p = row + 49 + 6 * idx;
+            for (int j = 0; j < 6; ++j) p[j] = kin[k][j];
+            ++idx;
+        }
+    }
+}
+
+static void race_kin_row(const orc_t* o, const body_t* b, double* k12) {
+    double rpy[3];
+    body_rpy(b, rpy);
+    v3 w = body_ang_v(o, b);
+    double v[12] = {b->pos.x, b->pos.y, b->pos.z, rpy[0], rpy[1], rpy[2], b->vel.x, b->vel.y, b->vel.z, w.x, w.y, w.z};
+    memcpy(k12, v, sizeof v);
+}
+
 /* _computeObs (MultiRaceAviary.py:566-661) of drone i in env e, float64 row */
 static void race_obs_row(const orc_t* o, int e, int i, double* row) {
     const adrp_config* c = &o->cfg;
@@ -504,42 +542,23 @@ static void race_obs_row(const orc_t* o, int e, int i, double* row) {
     const int N = o->N;
     const body_t* bs = &o->b[(size_t)e * N];
     const renv_t* re = &o->re[e];
-    const body_t* b = &bs[i];
-    double rpy[3];
-    body_rpy(b, rpy);
-    v3 w = body_ang_v(o, b);
-    double k12[12] = {b->pos.x, b->pos.y, b->pos.z, rpy[0], rpy[1], rpy[2], b->vel.x, b->vel.y, b->vel.z, w.x, w.y, w.z};
-    memset(row, 0, sizeof(double) * o->D);
-    memcpy(row, k12, sizeof k12);
-    shape_t ds = drone_shape(o, b);
+    double kin[ADRP_MAX_DRONES][12];
+    for (int k = 0; k < N; ++k) race_kin_row(o, &bs[k], kin[k]);
+    shape_t ds = drone_shape(o, &bs[i]);
     part_t parts[5];
+    uint8_t gin[ADRP_MAX_GATES] = {0}, oin[ADRP_MAX_OBSTACLES] = {0};
     for (int g = 0; g < t->num_gates; ++g) {
         v3 org; m33 Rg;
         gate_pose(re, g, &org, &Rg);
         int np = gate_parts(t->gates[g][6] > 0, parts);
-        int in = body_distance(&ds, parts, np, org, Rg) < VISIBILITY_RANGE;
-        if (in) { row[12 + 4 * g] = re->gate[g][0]; row[13 + 4 * g] = re->gate[g][1]; row[14 + 4 * g] = re->gate[g][2]; row[15 + 4 * g] = re->gate[g][3]; }
-        else { row[12 + 4 * g] = t->gates[g][0]; row[13 + 4 * g] = t->gates[g][1]; row[14 + 4 * g] = t->gates[g][2]; row[15 + 4 * g] = t->gates[g][5]; }
-        row[28 + g] = in;
+        gin[g] = body_distance(&ds, parts, np, org, Rg) < VISIBILITY_RANGE;
     }
     for (int k = 0; k < t->num_obstacles; ++k) {
         int np = obstacle_parts(parts);
-        int in = body_distance(&ds, parts, np, V(re->obst[k][0], re->obst[k][1], re->obst[k][2]), m_eye()) < VISIBILITY_RANGE;
-        for (int j = 0; j < 3; ++j) row[32 + 3 * k + j] = in ? re->obst[k][j] : t->obstacles[k][j];
-        row[44 + k] = in;
+        oin[k] = body_distance(&ds, parts, np, V(re->obst[k][0], re->obst[k][1], re->obst[k][2]), m_eye()) < VISIBILITY_RANGE;
     }
-    row[48] = o->rd[(size_t)e * N + i].gate;
-    if (c->race_mode == ADRP_RACE_COMPETE) {
-        int idx = 0;
-        for (int k = 0; k < N; ++k) {
-            if (k == i) continue;
-            double r2[3];
-            body_rpy(&bs[k], r2);
-            double* p = row + 49 + 6 * idx;
-            p[0] = bs[k].pos.x; p[1] = bs[k].pos.y; p[2] = bs[k].pos.z; p[3] = r2[0]; p[4] = r2[1]; p[5] = r2[2];
-            ++idx;
-        }
-    }
+    race_obs_assemble(c, N, i, (const double(*)[12])kin, (const double(*)[4])re->gate, gin,
+                      (const double(*)[3])re->obst, oin, o->rd[(size_t)e * N + i].gate, row);
 }
 
 static void race_write_obs(const orc_t* o, int e, float* obs_env, double* row0) {
@@ -677,31 +696,87 @@ static int race_contact(const orc_t* o, int e, int i) {   /* _collision (552-562
     return 0;
 }
 
+/* the 7 vertical rays of _gate_progress (MultiRaceAviary.py:484-494), reference order:
+   centre, then +-i * 0.05 (cos yaw, sin yaw) for i = 1, 2, 3 */
+static void race_rays(const double gate_xyyaw[3], int type, double from[7][3], double to[7][3]) {
+    const double x = gate_xyyaw[0], y = gate_xyyaw[1], rot = gate_xyyaw[2];
+    const double h = type == 0 ? 1.0 : 0.525, half = 0.1875;   /* Z_HIGH / Z_LOW (URDF dependent) */
+    const double dx = 0.05 * cos(rot), dy = 0.05 * sin(rot);
+    for (int r = 0; r < 7; ++r) {
+        const int m = r == 0 ? 0 : ((r + 1) / 2) * (r % 2 ? 1 : -1);
+        from[r][0] = to[r][0] = x + m * dx;
+        from[r][1] = to[r][1] = y + m * dy;
+        from[r][2] = h - half;
+        to[r][2] = h + half;
+    }
+}
+/* decision part of _gate_progress (502-506): rays' first-hit ids and fractions */
+static void race_progress_decide(int num_gates, int self_id, const int hit_id[7], const double hit_frac[7],
+                                 int* gate, int* fin) {
+    const int g = *gate;
+    if (num_gates > 0 && g < num_gates) {
+        int passed = 0;
+        for (int r = 0; r < 7; ++r) passed |= (hit_frac[r] < 0.9999 && hit_id[r] == self_id);
+        if (passed) *gate = g + 1;
+    }
+    if (g >= num_gates) *fin = 1;
+}
+
 /* _gate_progress (471-506) for drone i */
 static void race_gate_progress(orc_t* o, int e, int i) {
     const adrp_track* t = &o->cfg.track;
     const int N = o->N;
     rdrone_t* d = &o->rd[(size_t)e * N + i];
     const renv_t* re = &o->re[e];
-    int gate = d->gate;
-    if (t->num_gates > 0 && gate < t->num_gates) {
-        double x = re->gate[gate][0], y = re->gate[gate][1], rot = re->gate[gate][3];
-        double h = t->gates[gate][6] == 0 ? 1.0 : 0.525, half = 0.1875;
-        double dx = 0.05 * cos(rot), dy = 0.05 * sin(rot);
-        int passed = 0;
-        for (int r = -3; r <= 3 && !passed; ++r) {
-            v3 p0 = V(x + r * dx, y + r * dy, h - half), p1 = V(x + r * dx, y + r * dy, h + half);
-            double best = 2; int who = -1;
+    int hit_id[7] = {-1, -1, -1, -1, -1, -1, -1};
+    double hit_frac[7] = {1, 1, 1, 1, 1, 1, 1};
+    if (t->num_gates > 0 && d->gate < t->num_gates) {
+        double from[7][3], to[7][3], g3[3] = {re->gate[d->gate][0], re->gate[d->gate][1], re->gate[d->gate][3]};
+        race_rays(g3, t->gates[d->gate][6] > 0, from, to);
+        for (int r = 0; r < 7; ++r) {
             for (int k = 0; k < N; ++k) {   /* first hit among the drones (gates/obstacles lie off the rays) */
                 shape_t sk = drone_shape(o, &o->b[(size_t)e * N + k]);
-                double f = ray_cylinder(&sk, p0, p1);
-                if (f < best) { best = f; who = k; }
+                double f = ray_cylinder(&sk, V(from[r][0], from[r][1], from[r][2]), V(to[r][0], to[r][1], to[r][2]));
+                if (f < hit_frac[r] && f <= 1) { hit_frac[r] = f; hit_id[r] = k; }
             }
-            if (who == i && best < 0.9999) passed = 1;
         }
-        if (passed) d->gate += 1;
     }
-    if (gate >= t->num_gates) d->fin = 1;
+    race_progress_decide(t->num_gates, i, hit_id, hit_frac, &d->gate, &d->fin);
+}
+
+/* _computeTerminated (674-698): updates elim[], returns terminated */
+static int race_terminated(const adrp_track* t, int N, const double (*pos)[3], const double (*angv)[3],
+                           const uint8_t* contact, uint8_t* elim, const uint8_t* fin) {
+    int all_done = 1;
+    for (int i = 0; i < N; ++i) {
+        int oob = fabs(pos[i][0]) > t->bounds_hi[0] || fabs(pos[i][1]) > t->bounds_hi[1] || fabs(pos[i][2]) > t->bounds_hi[2];
+        int unstable = fabs(angv[i][0]) > 20 || fabs(angv[i][1]) > 20 || fabs(angv[i][2]) > 20;
+        elim[i] = (uint8_t)(elim[i] || oob || unstable || contact[i]);
+        all_done &= (elim[i] || fin[i]);
+    }
+    return all_done;
+}
+/* _computeTruncated (702-709), evaluated before step_counter += S */
+static int race_truncated(const adrp_config* c, int step_counter) {
+    return (double)step_counter / c->pyb_freq > c->track.episode_len_sec;
+}
+/* RewardWrapper._compute_reward (utils/wrapper.py:121-186) on drone 0's obs row */
+static double race_reward_wrapper(int* wr_gate, double target[3], double prev[3], const double* row0, int term,
+                                  int completed) {
+    int gate_id = (int)row0[48];
+    double r_passed = 0;
+    if (gate_id > *wr_gate % 4) {
+        *wr_gate = gate_id;
+        if (gate_id < 4)   /* gate_positions has keys 0..3 (KeyError otherwise) */
+            for (int k = 0; k < 3; ++k) target[k] = row0[12 + 4 * gate_id + k];
+        r_passed = 5;
+    }
+    double r_col = (term && !completed) ? -1 : 0, r_lab = (term && completed) ? 10 : 0;
+    double pxy = sqrt((target[0] - prev[0]) * (target[0] - prev[0]) + (target[1] - prev[1]) * (target[1] - prev[1]));
+    double cxy = sqrt((target[0] - row0[0]) * (target[0] - row0[0]) + (target[1] - row0[1]) * (target[1] - row0[1]));
+    double pz = fabs(target[2] - prev[2]), cz = fabs(target[2] - row0[2]);
+    for (int k = 0; k < 3; ++k) prev[k] = row0[k];
+    return (pxy - cxy) + (pz - cz) + r_passed + r_col + r_lab;
 }
 
 static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, float* rew, uint8_t* term,
@@ -766,38 +841,25 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
     for (int i = 0; i < N; ++i) race_gate_progress(o, e, i);
     double row0[64 + 6 * ADRP_MAX_DRONES];
     race_write_obs(o, e, obs_env, row0);
-    int all_done = 1, all_fin = 1;
-    for (int i = 0; i < N; ++i) {              /* _computeTerminated (674-698) */
-        rdrone_t* d = &ds[i];
+    double pos[ADRP_MAX_DRONES][3], angv[ADRP_MAX_DRONES][3];
+    uint8_t contact[ADRP_MAX_DRONES], elim[ADRP_MAX_DRONES], fin[ADRP_MAX_DRONES];
+    for (int i = 0; i < N; ++i) {
         v3 w = body_ang_v(o, &bs[i]);
-        int oob = fabs(bs[i].pos.x) > t->bounds_hi[0] || fabs(bs[i].pos.y) > t->bounds_hi[1] ||
-                  fabs(bs[i].pos.z) > t->bounds_hi[2];
-        int unstable = fabs(w.x) > 20 || fabs(w.y) > 20 || fabs(w.z) > 20;
-        d->elim = d->elim || oob || unstable || race_contact(o, e, i);
-        all_done &= (d->elim || d->fin);
-        all_fin &= d->fin;
+        pos[i][0] = bs[i].pos.x; pos[i][1] = bs[i].pos.y; pos[i][2] = bs[i].pos.z;
+        angv[i][0] = w.x; angv[i][1] = w.y; angv[i][2] = w.z;
+        contact[i] = (uint8_t)race_contact(o, e, i);
+        elim[i] = (uint8_t)ds[i].elim; fin[i] = (uint8_t)ds[i].fin;
     }
-    *term = (uint8_t)all_done;
-    *trunc = (uint8_t)((double)o->step_counter[e] / c->pyb_freq > t->episode_len_sec);   /* (702-709) */
+    int all_fin = 1;
+    *term = (uint8_t)race_terminated(t, N, (const double(*)[3])pos, (const double(*)[3])angv, contact, elim, fin);
+    for (int i = 0; i < N; ++i) { ds[i].elim = elim[i]; all_fin &= fin[i]; }
+    *trunc = (uint8_t)race_truncated(c, o->step_counter[e]);
     double r = 0;
-    if (t->reward_wrapper) {                   /* RewardWrapper._compute_reward (wrapper.py:121-186) */
+    if (t->reward_wrapper) {
         renv_t* re = &o->re[e];
-        int gate_id = (int)row0[48];
-        double r_passed = 0;
-        if (gate_id > re->wr_gate % 4) {
-            re->wr_gate = gate_id;
-            if (gate_id < 4)                   /* gate_positions has keys 0..3 (KeyError otherwise) */
-                for (int k = 0; k < 3; ++k) re->wr_target[k] = row0[12 + 4 * gate_id + k];
-            r_passed = 5;
-        }
         /* info["task_completed"] does not exist in the reference (KeyError, Q23):
            defined here as "every drone finished" */
-        double r_col = (*term && !all_fin) ? -1 : 0, r_lab = (*term && all_fin) ? 10 : 0;
-        double pxy = hypot(re->wr_target[0] - re->wr_prev[0], re->wr_target[1] - re->wr_prev[1]);
-        double cxy = hypot(re->wr_target[0] - row0[0], re->wr_target[1] - row0[1]);
-        double pz = fabs(re->wr_target[2] - re->wr_prev[2]), cz = fabs(re->wr_target[2] - row0[2]);
-        r = (pxy - cxy) + (pz - cz) + r_passed + r_col + r_lab;
-        for (int k = 0; k < 3; ++k) re->wr_prev[k] = row0[k];
+        r = race_reward_wrapper(&re->wr_gate, re->wr_target, re->wr_prev, row0, *term, all_fin);
     }
     *rew = (float)r;
     o->step_counter[e] += o->S;                /* (268) */
@@ -927,4 +989,28 @@ double orc_shape_distance(const double* a, const double* b) {
 void orc_lpf_coeffs(double fs, double fc, double out[5]) {
     lpf_t l = lpf_coeffs((float)fs, (float)fc);
     out[0] = l.b0; out[1] = l.b1; out[2] = l.b2; out[3] = l.a1; out[4] = l.a2;
+}
+
+/* ---- decision-logic entry points (golden tests against the reference's Python) ------- */
+int orc_race_obs_assemble(const adrp_config* cfg, int N, int i, const double* kin, const double* gate_act,
+                          const uint8_t* gate_in, const double* obst_act, const uint8_t* obst_in, int current_gate,
+                          double* row) {
+    if (N < 1 || N > ADRP_MAX_DRONES || i < 0 || i >= N) return fail("drone index");
+    race_obs_assemble(cfg, N, i, (const double(*)[12])kin, (const double(*)[4])gate_act, gate_in,
+                      (const double(*)[3])obst_act, obst_in, current_gate, row);
+    return ADRP_OK;
+}
+int orc_race_terminated(const adrp_config* cfg, int N, const double* pos, const double* angv, const uint8_t* contact,
+                        uint8_t* elim, const uint8_t* fin) {
+    return race_terminated(&cfg->track, N, (const double(*)[3])pos, (const double(*)[3])angv, contact, elim, fin);
+}
+int orc_race_truncated(const adrp_config* cfg, int step_counter) { return race_truncated(cfg, step_counter); }
+void orc_race_rays(const double gate_xyyaw[3], int type, double* from, double* to) {
+    race_rays(gate_xyyaw, type, (double(*)[3])from, (double(*)[3])to);
+}
+void orc_race_progress(int num_gates, int self_id, const int* hit_id, const double* hit_frac, int* gate, int* fin) {
+    race_progress_decide(num_gates, self_id, hit_id, hit_frac, gate, fin);
+}
+double orc_race_reward(int* wr_gate, double* target, double* prev, const double* row0, int term, int completed) {
+    return race_reward_wrapper(wr_gate, target, prev, row0, term, completed);
 }

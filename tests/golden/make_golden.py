@@ -489,6 +489,174 @@ def mellinger_fixtures(pb, m):
     return out
 
 
+# --------------------------------------------------------------------------------------
+# MultiRaceAviary decision logic: obs assembly, termination, truncation, gate progress
+# (rays), RewardWrapper -- with the Bullet queries answered from scripted tables
+# --------------------------------------------------------------------------------------
+class _Conn:
+    def send(self, x): pass
+    def recv(self): return np.zeros(4)
+    def close(self): pass
+
+
+class _Proc:
+    def __init__(self, *a, **k): pass
+    def start(self): pass
+    def join(self): pass
+
+
+RACE_CFG = {   # config/level3.yaml track with the two SURVEY §8(d) extension drones
+    "bounds": [[-3, -3, 0], [3, 3, 2]], "episode_len_sec": 33, "done_on_completion": True,
+    "init_states": {f"drone{k}": {"pos": p, "vel": [0, 0, 0], "rpy": [0, 0, 0], "pqr": [0, 0, 0]}
+                    for k, p in enumerate([[0.9, 0.9, 0.05], [1.1, 1.1, 0.05], [0.7, 0.9, 0.05], [1.3, 1.1, 0.05]])},
+    "gates": [[0.45, -1.0, 0.525, 0, 0, 2.35, 1], [1.0, -1.55, 1.0, 0, 0, -0.78, 0],
+              [0.0, 0.5, 0.525, 0, 0, 0, 1], [-0.5, -0.5, 1.0, 0, 0, 3.14, 0]],
+    "obstacles": [[1.0, -0.5, 0.525, 0, 0, 0], [0.5, -1.5, 0.525, 0, 0, 0], [-0.5, 0, 0.525, 0, 0, 0],
+                  [0, 1.0, 0.525, 0, 0, 0]],
+    "random_gates_obstacles": False, "random_drone_state": False, "random_drone_inertia": False,
+    "disturbances": False,
+}
+
+
+def race_fixtures(pb, m):
+    E = m.enums
+    MR = m.MultiRace
+    MR.mp = types.SimpleNamespace(Pipe=lambda: (_Conn(), _Conn()), Process=_Proc)   # no controller processes
+    cfg = sys.modules["munch"].munchify(RACE_CFG)
+    rng = np.random.default_rng(21)
+    out = {}
+    for mode_name, mode in (("compete", E.RaceMode.COMPETE), ("compare", E.RaceMode.COMPARE)):
+        N = 4 if mode_name == "compete" else 2
+        env = MR.MultiRaceAviary(race_config=cfg, num_drones=N, racemode=mode)
+        env.reset()
+        gates_nom = np.array(env.gates_nominal, float)
+        obst_nom = np.array(env.obstacles_nominal, float)
+        # (a) _computeObs with scripted getClosestPoints answers
+        n = 96
+        D = env._computeObs().shape[1]
+        kin = np.zeros((n, N, 12)); gact = np.zeros((n, 4, 4)); oact = np.zeros((n, 4, 3))
+        gin = np.zeros((n, N, 4), np.uint8); oin = np.zeros((n, N, 4), np.uint8)
+        cur = np.zeros((n, N), np.int64); obs = np.zeros((n, N, D))
+        for k in range(n):
+            for i in range(N):
+                pos, quat, vel, ang = random_state(rng, center=(0, 0, 1), tilt=0.4)
+                set_drone_state(pb, env, i, pos, quat, vel, ang)
+            env._updateAndStoreKinematicInformation()
+            ga = gates_nom.copy(); ga[:, [0, 1, 5]] += rng.uniform(-0.15, 0.15, (4, 3))
+            oa = obst_nom.copy(); oa[:, :2] += rng.uniform(-0.15, 0.15, (4, 2))
+            env.gates_actual = ga.tolist(); env.obstacles_actual = oa.tolist()
+            env.current_gate = rng.integers(0, 5, N).astype(float)
+            gi = rng.random((N, 4)) < 0.5; oi = rng.random((N, 4)) < 0.5
+            pb.closest = {}
+            for i in range(N):
+                for g in range(4):
+                    pb.closest[(env.gates_urdf[g], env.DRONE_IDS[i])] = bool(gi[i, g])
+                    pb.closest[(env.obstacles_urdf[g], env.DRONE_IDS[i])] = bool(oi[i, g])
+            obs[k] = env._computeObs()
+            kin[k] = np.hstack([env.pos, env.rpy, env.vel, env.ang_v])
+            gact[k] = ga[:, [0, 1, 2, 5]]; oact[k] = oa[:, :3]
+            gin[k] = gi; oin[k] = oi; cur[k] = env.current_gate
+        out.update({f"{mode_name}_obs_kin": kin, f"{mode_name}_obs_gact": gact, f"{mode_name}_obs_oact": oact,
+                    f"{mode_name}_obs_gin": gin, f"{mode_name}_obs_oin": oin, f"{mode_name}_obs_cur": cur,
+                    f"{mode_name}_obs": obs})
+        # (b) _computeTerminated with scripted getContactPoints answers
+        env.collision_objects = env.gates_urdf + env.obstacles_urdf + [env.PLANE_ID]
+        if mode == E.RaceMode.COMPETE:
+            env.collision_objects += env.DRONE_IDS.tolist()
+        n = 128
+        tpos = np.zeros((n, N, 3)); tang = np.zeros((n, N, 3)); tcon = np.zeros((n, N), np.uint8)
+        telim0 = np.zeros((n, N), np.uint8); telim = np.zeros((n, N), np.uint8); tfin = np.zeros((n, N), np.uint8)
+        tterm = np.zeros(n, bool)
+        for k in range(n):
+            for i in range(N):
+                pos = rng.uniform(-3.3, 3.3, 3); pos[2] = rng.uniform(-0.2, 2.3)
+                ang = rng.uniform(-25, 25, 3) * (rng.random() < 0.3) + rng.uniform(-1, 1, 3)
+                set_drone_state(pb, env, i, pos, np.array([0, 0, 0, 1.0]), np.zeros(3), ang)
+            env._updateAndStoreKinematicInformation()
+            pb.contacts = {}
+            con = rng.random(N) < 0.2
+            for i in range(N):
+                if con[i]:
+                    obj = env.collision_objects[int(rng.integers(0, len(env.collision_objects)))]
+                    pb.contacts[(obj, env.DRONE_IDS[i])] = True
+            e0 = rng.random(N) < 0.2
+            f0 = rng.random(N) < 0.3
+            env.drones_eliminated = e0.copy(); env.drones_finished = f0.copy()
+            tterm[k] = env._computeTerminated()
+            tpos[k] = env.pos; tang[k] = env.ang_v
+            tcon[k] = [any(pb.contacts.get((o, env.DRONE_IDS[i]), False) for o in env.collision_objects) for i in range(N)]
+            telim0[k] = e0; telim[k] = env.drones_eliminated; tfin[k] = f0
+        out.update({f"{mode_name}_term_pos": tpos, f"{mode_name}_term_angv": tang, f"{mode_name}_term_contact": tcon,
+                    f"{mode_name}_term_elim0": telim0, f"{mode_name}_term_elim": telim,
+                    f"{mode_name}_term_fin": tfin, f"{mode_name}_term": tterm})
+    # (c) _computeTruncated around 33 s x 500 Hz
+    counters = np.array([0, 20, 16480, 16499, 16500, 16501, 16520, 16540, 20000])
+    tr = []
+    for sc in counters:
+        env.step_counter = int(sc)
+        tr.append(env._computeTruncated())
+    out.update(trunc_counter=counters, trunc=np.array(tr))
+    # (d) _gate_progress with scripted rayTestBatch answers
+    N = env.NUM_DRONES
+    n = 160
+    pg_gate0 = np.zeros((n, N), np.int64); pg_gate = np.zeros((n, N), np.int64); pg_fin = np.zeros((n, N), np.uint8)
+    pg_gact = np.zeros((n, 4, 6)); pg_from = np.zeros((n, N, 7, 3)); pg_to = np.zeros((n, N, 7, 3))
+    pg_id = np.zeros((n, N, 7), np.int64); pg_frac = np.zeros((n, N, 7))
+    for k in range(n):
+        ga = gates_nom.copy(); ga[:, [0, 1, 5]] += rng.uniform(-0.15, 0.15, (4, 3))
+        env.gates_actual = ga.tolist()
+        g0 = rng.integers(0, 5, N)
+        env.current_gate = g0.astype(float)
+        env.drones_finished = np.zeros(N, bool)
+        for i in range(N):
+            ids = rng.choice(list(env.DRONE_IDS) + [-1], 7)
+            fr = np.where(rng.random(7) < 0.15, 0.99995, rng.uniform(0, 1.0, 7))
+            fr[ids == -1] = 1.0
+            pb.ray_result = [(int(ids[r]), -1, float(fr[r]), (0, 0, 0), (0, 0, 1)) for r in range(7)]
+            pb.rays = None
+            env._gate_progress(i)
+            if pb.rays is not None:
+                pg_from[k, i], pg_to[k, i] = pb.rays
+            pg_id[k, i] = [list(env.DRONE_IDS).index(x) if x in list(env.DRONE_IDS) else -1 for x in ids]
+            pg_frac[k, i] = fr
+        pg_gate0[k] = g0; pg_gate[k] = env.current_gate; pg_fin[k] = env.drones_finished; pg_gact[k] = ga
+    out.update(pg_gate0=pg_gate0, pg_gate=pg_gate, pg_fin=pg_fin, pg_gact=pg_gact, pg_from=pg_from, pg_to=pg_to,
+               pg_id=pg_id, pg_frac=pg_frac)
+    # (e) RewardWrapper on a scripted episode (info["task_completed"] supplied: the env has none)
+    T = 40
+
+    class _Scripted(sys.modules["gymnasium"].Env):
+        def __init__(self, seq, obs0):
+            self.seq, self.obs0, self.k = seq, obs0, 0
+        def reset(self, *a, **k):
+            return self.obs0, {}
+        def step(self, action):
+            r = self.seq[self.k]
+            self.k += 1
+            return r
+    obs_seq = np.zeros((T + 1, 2, 49))
+    obs_seq[:, :, :12] = rng.uniform(-1, 1, (T + 1, 2, 12))
+    obs_seq[:, :, 12:28] = np.tile(np.array(RACE_CFG["gates"])[:, [0, 1, 2, 5]].ravel(), (T + 1, 2, 1))
+    g = 0
+    for t in range(T + 1):
+        if t > 0 and rng.random() < 0.2 and g < 4:
+            g += 1
+        obs_seq[t, :, 48] = g
+    term_seq = np.zeros(T, bool); term_seq[[15, 31, 39]] = True
+    comp_seq = np.zeros(T, bool); comp_seq[31] = True
+    seq = [(obs_seq[t + 1], 0, bool(term_seq[t]), False, {"task_completed": bool(comp_seq[t])}) for t in range(T)]
+    w = m.wrapper.RewardWrapper(_Scripted(seq, obs_seq[0]))
+    w.reset()
+    rewards = []
+    for t in range(T):
+        if obs_seq[t + 1, 0, 48] >= 4 and obs_seq[t + 1, 0, 48] > w.current_gate_id % 4:
+            # the reference raises KeyError (gate_positions has keys 0..3); stop the script here
+            break
+        rewards.append(w.step(np.zeros((2, 4)))[1])
+    out.update(rw_obs=obs_seq, rw_term=term_seq, rw_completed=comp_seq, rw_reward=np.array(rewards))
+    return out
+
+
 def main():
     os.chdir(REF)   # MultiRaceAviary resolves URDF_DIR relative to the cwd (read only)
     pb = install_stubs()
@@ -501,6 +669,10 @@ def main():
     path = os.path.join(HERE, "hover_golden.npz")
     np.savez_compressed(path, **fx)
     print("wrote", path, len(fx), "arrays")
+    rx = race_fixtures(pb, m)
+    path = os.path.join(HERE, "race_golden.npz")
+    np.savez_compressed(path, **rx)
+    print("wrote", path, len(rx), "arrays")
 
 
 if __name__ == "__main__":
