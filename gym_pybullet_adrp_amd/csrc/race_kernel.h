@@ -176,6 +176,12 @@ __device__ __noinline__ Real gjk_distance(const Shape<Real>& A, const Shape<Real
             V3<Real> bv = v, b0 = W0, b1 = W1, b2 = W2;
             int bm = 0;
             bool outside = false;
+            // a flat (degenerate) tetrahedron -- two level discs at one height -- encloses
+            // nothing: every face is then a candidate
+            const V3<Real> e1 = W1 - W0, e2 = W2 - W0, e3 = W3 - W0;
+            const Real vol = dot(e1, cross(e2, e3));
+            const Real scl = sqrt_(dot(e1, e1) * dot(e2, e2) * dot(e3, e3));
+            const bool flat = fabs_(vol) <= (sizeof(Real) == 4 ? Real(1e-5) : Real(1e-12)) * scl;
 #pragma unroll
             for (int f = 0; f < 4; ++f) {
                 const V3<Real> p0 = f == 3 ? W1 : W0;
@@ -184,7 +190,7 @@ __device__ __noinline__ Real gjk_distance(const Shape<Real>& A, const Shape<Real
                 const V3<Real> po = f == 0 ? W3 : (f == 1 ? W1 : (f == 2 ? W2 : W0));
                 const V3<Real> nrm = cross(p1 - p0, p2 - p0);
                 const Real so = -dot(nrm, p0), sd = dot(nrm, po - p0);
-                if (so * sd < Real(0)) {
+                if (flat || so * sd < Real(0)) {
                     outside = true;
                     V3<Real> q0, q1, q2;
                     int m;
@@ -422,7 +428,9 @@ __device__ __forceinline__ float lpf_apply(const Lpf& l, float& d1, float& d2, f
 }
 
 // FULLSTATE setpoint modes (MellingerControl.py:510-543): x,y,z,quat abs; rates 0
-template <typename Real>
+// FAST (fp32 kernel): hardware reciprocals for the firmware's divisions; the fp64 kernel
+// keeps the C float divisions bit-for-bit
+template <typename Real, bool FAST = (sizeof(Real) == 4)>
 __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3], float xc_x, float xc_y,
                                              const float gyro[3], const float pos[3], const float vel[3],
                                              const float Rm[9]) {
@@ -441,12 +449,18 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
     const float Ry0 = Rm[1], Ry1 = Rm[4], Ry2 = Rm[7];
     const float Rz0 = Rm[2], Rz1 = Rm[5], Rz2 = Rm[8];
     const float current_thrust = tx * Rz0 + ty * Rz1 + tz * Rz2;
-    const float tn = sqrtf(tx * tx + ty * ty + tz * tz);
-    const float zd0 = tx / tn, zd1 = ty / tn, zd2 = tz / tn;
+    const float tn = FAST ? __builtin_amdgcn_sqrtf(tx * tx + ty * ty + tz * tz) : sqrtf(tx * tx + ty * ty + tz * tz);
+    const float itn = FAST ? __builtin_amdgcn_rcpf(tn) : 0.0f;
+    const float zd0 = FAST ? tx * itn : tx / tn, zd1 = FAST ? ty * itn : ty / tn, zd2 = FAST ? tz * itn : tz / tn;
     // y_des = normalize(z_des x x_c), x_c = (cos yaw, sin yaw, 0)
     float yd0 = zd1 * 0.0f - zd2 * xc_y, yd1 = zd2 * xc_x - zd0 * 0.0f, yd2 = zd0 * xc_y - zd1 * xc_x;
-    const float yn = sqrtf(yd0 * yd0 + yd1 * yd1 + yd2 * yd2);
-    yd0 /= yn; yd1 /= yn; yd2 /= yn;
+    const float yn = FAST ? __builtin_amdgcn_sqrtf(yd0 * yd0 + yd1 * yd1 + yd2 * yd2) : sqrtf(yd0 * yd0 + yd1 * yd1 + yd2 * yd2);
+    if (FAST) {
+        const float iyn = __builtin_amdgcn_rcpf(yn);
+        yd0 *= iyn; yd1 *= iyn; yd2 *= iyn;
+    } else {
+        yd0 /= yn; yd1 /= yn; yd2 /= yn;
+    }
     const float xd0 = yd1 * zd2 - yd2 * zd1, xd1 = yd2 * zd0 - yd0 * zd2, xd2 = yd0 * zd1 - yd1 * zd0;
     const float eRx = (zd0 * Ry0 + zd1 * Ry1 + zd2 * Ry2) - (Rz0 * yd0 + Rz1 * yd1 + Rz2 * yd2);
     const float eRy = -((xd0 * Rz0 + xd1 * Rz1 + xd2 * Rz2) - (Rx0 * zd0 + Rx1 * zd1 + Rx2 * zd2));
@@ -455,8 +469,10 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
     const float ewx = radf_(0.0f) - rate_roll, ewy = -radf_(0.0f) - rate_pitch, ewz = radf_(0.0f) - rate_yaw;
     float err_d_roll = 0, err_d_pitch = 0;
     if (d.pw_roll == d.pw_roll) {
-        err_d_roll = ((radf_(0.0f) - d.psp_roll) - (rate_roll - d.pw_roll)) / dt;
-        err_d_pitch = (-(radf_(0.0f) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) / dt;
+        err_d_roll = FAST ? ((radf_(0.0f) - d.psp_roll) - (rate_roll - d.pw_roll)) * 500.0f
+                          : ((radf_(0.0f) - d.psp_roll) - (rate_roll - d.pw_roll)) / dt;
+        err_d_pitch = FAST ? (-(radf_(0.0f) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) * 500.0f
+                           : (-(radf_(0.0f) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) / dt;
     }
     d.pw_roll = rate_roll;
     d.pw_pitch = rate_pitch;
@@ -567,7 +583,7 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
     for (int k = 0; k < 4; ++k) {
         Real t = th[3 - k] + noise[k];
         if (t < Real(0)) t = Real(0);
-        Real mp = F32 ? (sqrt_(t * Real(1.0 / 3.16e-10)) - Real(4070.3)) * Real(1.0 / 0.2685)
+        Real mp = F32 ? (hsqrt_(t * Real(1.0 / 3.16e-10)) - Real(4070.3)) * Real(1.0 / 0.2685)
                       : (sqrt_(t / Real(1) / Real(3.16e-10)) - Real(4070.3)) / Real(0.2685);
         mp = clampr_(mp, Real(20000), Real(65535));
         d.prev[k] = d.rpm[k];
@@ -638,10 +654,10 @@ __device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDron
     (void)0;
     const V3<Real> wb = mulT(R, d.w);
     const V3<Real> Iw = v3(ixx * wb.x, iyy * wb.y, izz * wb.z);
-    const Real kw = Real(0.04) + Real(0.04) * sqrt_(dot(wb, wb));
+    const Real kw = Real(0.04) + Real(0.04) * hsqrt_(dot(wb, wb));
     const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
     const V3<Real> wdot = mul(R, v3(rhs.x * d.inv_i[0], rhs.y * d.inv_i[1], rhs.z * d.inv_i[2]));
-    const Real kv = Real(0.04) + Real(0.04) * sqrt_(dot(d.vel, d.vel));
+    const Real kv = Real(0.04) + Real(0.04) * hsqrt_(dot(d.vel, d.vel));
     const V3<Real> acc = d.inv_mass * Fw - kv * d.vel;
     d.w = v3(clamp100r(d.w.x + C.dt * wdot.x), clamp100r(d.w.y + C.dt * wdot.y), clamp100r(d.w.z + C.dt * wdot.z));
     d.vel = v3(clamp100r(d.vel.x + C.dt * acc.x), clamp100r(d.vel.y + C.dt * acc.y), clamp100r(d.vel.z + C.dt * acc.z));
@@ -649,12 +665,12 @@ __device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDron
     d.ql = d.q;
     d.lpos = d.pos;
     d.pos = d.pos + C.dt * d.vel;
-    Real ang = sqrt_(dot(d.w, d.w));
+    Real ang = hsqrt_(dot(d.w, d.w));
     if (ang > C.ang_max) ang = C.ang_max;
     Real sh, ch;
     small_sincos(Real(0.5) * ang * C.dt, &sh, &ch);   // argument <= ANGULAR_MOTION_THRESHOLD / 2 = pi / 8
     const Real sc = ang < Real(0.001) ? Real(0.5) * C.dt - (C.dt * C.dt * C.dt) * Real(0.020833333333) * ang * ang
-                                      : sh / ang;
+                                      : sh * rcp_(ang);
     const V3<Real> ax = sc * d.w;
     const Q4<Real> q0 = d.q;
     const Q4<Real> q1 = {ch * q0.x + ax.x * q0.w + ax.y * q0.z - ax.z * q0.y,
@@ -664,7 +680,7 @@ __device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDron
     const Real inv = rsqrt_(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
     d.q = {q1.x * inv, q1.y * inv, q1.z * inv, q1.w * inv};
     const M3<Real> Rn = rot(d.q);
-    const Real low = d.pos.z + C.coll_zoff - C.coll_hh * fabs_(Rn.a22) - C.coll_r * sqrt_(Rn.a02 * Rn.a02 + Rn.a12 * Rn.a12);
+    const Real low = d.pos.z + C.coll_zoff - C.coll_hh * fabs_(Rn.a22) - C.coll_r * hsqrt_(Rn.a02 * Rn.a02 + Rn.a12 * Rn.a12);
     if (low < Real(0)) {
         d.pos.z -= low;
         if (d.vel.z < Real(0)) d.vel.z = Real(0);
@@ -693,13 +709,13 @@ __device__ __forceinline__ void race_dyn_substep(const RaceConst<Real>& C, RDron
     d.w = rr + C.dt * rdd;
     d.pos = d.pos + C.dt * d.vel;
     const V3<Real> w = d.w;
-    const Real wn = sqrt_(dot(w, w));
+    const Real wn = hsqrt_(dot(w, w));
     if (!(wn <= Real(1e-8))) {
         const Real th = wn * C.dt * Real(0.5);
         Real s, c;
         if (th <= Real(0.39269908169872414)) small_sincos(th, &s, &c);
         else sincos_(th, &s, &c);
-        const Real k = s / wn;
+        const Real k = s * rcp_(wn);
         const Q4<Real> q = d.q;
         d.q = {c * q.x + k * (w.z * q.y - w.y * q.z + w.x * q.w), c * q.y + k * (-w.z * q.x + w.x * q.z + w.y * q.w),
                c * q.z + k * (w.y * q.x - w.x * q.y + w.z * q.w), c * q.w + k * (-w.x * q.x - w.y * q.y - w.z * q.z)};
@@ -951,7 +967,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                 for (int k = 0; k < N; ++k) {
                     const Real ox = shfl_(d.pos.x, k, G), oy = shfl_(d.pos.y, k, G), oz = shfl_(d.pos.z, k, G);
                     const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
-                    const Real dxy = sqrt_(dx * dx + dy * dy);
+                    const Real dxy = hsqrt_(dx * dx + dy * dy);
                     if (dz > Real(0) && dxy < Real(10)) {
                         const Real kk = H.prop_r / (Real(4) * dz);
                         const Real alpha = H.dw1 * kk * kk, beta = H.dw2 * dz + H.dw3;

@@ -348,10 +348,15 @@ static int simplex_closest(v3* W, int* n, v3* out) {
         *out = vadd(a, vadd(vscale(ab, v), vscale(ac, w)));
         return 0;
     }
-    /* tetrahedron: origin inside?  else the closest of the faces that see the origin */
+    /* tetrahedron: origin inside?  else the closest of the faces that see the origin.  A
+       degenerate (flat) tetrahedron -- e.g. two level discs at the same height -- encloses
+       nothing: then every face is a candidate. */
     v3 a = W[0], b = W[1], c = W[2], d = W[3];
     v3 faces[4][3] = {{a, b, c}, {a, c, d}, {a, d, b}, {b, d, c}};
     v3 opp[4] = {d, b, c, a};
+    double vol = vdot(vsub(b, a), vcross(vsub(c, a), vsub(d, a)));
+    double scale = vnorm(vsub(b, a)) * vnorm(vsub(c, a)) * vnorm(vsub(d, a));
+    int flat = fabs(vol) <= 1e-12 * scale;
     double best = INFINITY;
     v3 bestW[3], bestv = V(0, 0, 0);
     int bestn = 0, outside = 0;
@@ -359,7 +364,7 @@ static int simplex_closest(v3* W, int* n, v3* out) {
         v3 p0 = faces[f][0], p1 = faces[f][1], p2 = faces[f][2];
         v3 nrm = vcross(vsub(p1, p0), vsub(p2, p0));
         double so = -vdot(nrm, p0), sd = vdot(nrm, vsub(opp[f], p0));
-        if (so * sd < 0) {   /* origin and the opposite vertex on different sides */
+        if (flat || so * sd < 0) {   /* origin and the opposite vertex on different sides */
             outside = 1;
             v3 Wf[3] = {p0, p1, p2};
             int nf = 3;

@@ -107,6 +107,19 @@ def test_gjk_separating_distance_is_tight():
     assert O.shape_distance(cyl, box) == 0
 
 
+def test_gjk_coplanar_discs():
+    """two level drone cylinders at one height: the support points are coplanar (flat
+    tetrahedra); the distance is the rim gap"""
+    I = np.eye(3)
+    for gap in (0.0035, 0.02, 0.1):
+        a = _cyl([0.0, 0.0, 0.5], I, 0.06, 0.0125)
+        b = _cyl([0.12 + gap, 0.0, 0.5], I, 0.06, 0.0125)
+        assert abs(O.shape_distance(a, b) - gap) < 1e-9
+        b = _cyl([(0.12 + gap) / np.sqrt(2), (0.12 + gap) / np.sqrt(2), 0.5], _rot([0, 0, 0.3]), 0.06, 0.0125)
+        assert abs(O.shape_distance(a, b) - gap) < 1e-9
+    assert O.shape_distance(_cyl([0, 0, 0.5], I, 0.06, 0.0125), _cyl([0.11, 0, 0.5], I, 0.06, 0.0125)) == 0
+
+
 def test_gate_distance_geometry():
     c = race_cfg()
     ident = [0, 0, 0, 1]
