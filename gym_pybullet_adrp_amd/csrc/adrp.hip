@@ -8,6 +8,7 @@
 
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -32,6 +33,7 @@ struct adrp_handle {
     int32_t* counters = nullptr;  // device diagnostics (ground-model hits)
     void* cblk = nullptr;         // device HoverConst<Real> + HoverReset<Real>
     bool cf2x = false;            // compiled-in constants (hover_step_kernel<..., DEF=true>)
+    bool stage_rows = true;       // LDS-staged obs rows when E % 64 == 0 (ADRP_STAGE_ROWS=0 disables)
     int diagnostics = 0;
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -384,6 +386,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
         hipMemset(h->ist, 0, h->ni * EN * sizeof(int32_t)) != hipSuccess ||
         hipMemset(h->counters, 0, 64 * sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return cleanup(seterr(h, ADRP_ERR_DEVICE, "initialisation failed"));
+    if (const char* env = getenv("ADRP_STAGE_ROWS")) h->stage_rows = atoi(env) != 0;
     const int rc = race ? (h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h))
                         : (h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h));
     if (rc != ADRP_OK) return cleanup(seterr(h, rc, "constant block upload failed"));
@@ -425,16 +428,16 @@ static void launch(K kernel, dim3 grid, dim3 blk, hipStream_t s, const HoverArgs
     }
 }
 
-template <typename Real, int A, int B, bool DEF>
+template <typename Real, int A, int B, bool DEF, bool STG = false>
 static void launch_step_ph(const HoverArgs<Real>& a, int physics, dim3 grid, hipStream_t s, adrp_t* h) {
     const dim3 blk(kBlock);
     switch (physics) {
-        case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B, DEF>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B, DEF>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_GND: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B, DEF>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_DRAG: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B, DEF>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_DW: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B, DEF>, grid, blk, s, a, h); break;
-        default: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B, DEF>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B, DEF, STG>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B, DEF, STG>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_GND: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B, DEF, STG>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_DRAG: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B, DEF, STG>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_DW: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B, DEF, STG>, grid, blk, s, a, h); break;
+        default: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B, DEF, STG>, grid, blk, s, a, h); break;
     }
 }
 
@@ -446,9 +449,13 @@ static int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8
     const dim3 grid((h->E + kBlock - 1) / kBlock);
     const int ph = h->cfg.physics;
     // compiled-in constants exist for the reference default (CF2X @ 240/30 Hz, B = 15)
+    const bool stg = h->stage_rows && h->E % kBlock == 0;
     if (h->cf2x && h->B == 15) {
         if (h->A == 1) launch_step_ph<Real, 1, 15, true>(a, ph, grid, s, h);
+        else if (stg) launch_step_ph<Real, 4, 15, true, true>(a, ph, grid, s, h);
         else launch_step_ph<Real, 4, 15, true>(a, ph, grid, s, h);
+    } else if (h->A == 4 && h->B == 15 && stg) {
+        launch_step_ph<Real, 4, 15, false, true>(a, ph, grid, s, h);
     } else if (h->A == 1) {
         if (h->B == 15) launch_step_ph<Real, 1, 15, false>(a, ph, grid, s, h);
         else launch_step_ph<Real, 1, 0, false>(a, ph, grid, s, h);

@@ -400,8 +400,27 @@ __device__ __forceinline__ void store_body(const HoverArgs<Real>& a, int e, cons
 // env.step kernel: lane = env; B (ring length) is a template parameter so the ring lives
 // in registers
 // ------------------------------------------------------------------------------------------
-// B == 0: runtime ring length a.B;  SC > 0: compile-time sub-step count (loop fully unrolled)
-template <typename Real, int PH, int A, int B, int SC>
+// obs rows staged in LDS, then written as one contiguous, fully coalesced block of
+// 64 rows (the row-per-lane float4 stores leave partial 64-B lines: +18 % write traffic)
+constexpr int kRowF4 = 18;        // 72 floats = 18 float4 per obs row (A = 4, B = 15)
+constexpr int kRowPad = 19;       // LDS row stride in float4 (bank spread)
+
+template <int A, int B>
+__device__ __forceinline__ void stage_row(float4* lds_row, const float o12[12], const float (&ring)[B][A], int head1) {
+    lds_row[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
+    lds_row[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
+    lds_row[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
+#pragma unroll
+    for (int p = 0; p < B; ++p) {
+        int k = p - head1;
+        k += k < 0 ? B : 0;
+        lds_row[3 + k] = make_float4(ring[p][0], ring[p][1], ring[p][2], ring[p][3]);
+    }
+}
+
+// B == 0: runtime ring length a.B;  SC > 0: compile-time sub-step count (loop fully unrolled);
+// STG: LDS-staged obs rows (needs A == 4, B == 15 and every lane of the block live)
+template <typename Real, int PH, int A, int B, int SC, bool STG = false>
 __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const HoverConst<Real>& C) {
     constexpr int BR = B > 0 ? B : 1;
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
@@ -509,8 +528,23 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         hover_reset_state(a, C, e, b, sc, ep);
         hover_obs12(C, b, o12);
     }
-    if constexpr (B > 0) write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
-    else write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
+    if constexpr (STG) {
+        static_assert(A == 4 && B == 15, "staged rows: 72-float rows only");
+        __shared__ float4 rows[kStepBlock * kRowPad];
+        stage_row<A, B>(rows + threadIdx.x * kRowPad, o12, ring, head1);
+        __syncthreads();
+        float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
+#pragma unroll
+        for (int k = 0; k < kRowF4; ++k) {
+            const int idx = threadIdx.x + kStepBlock * k;   // float4 index inside the block's rows
+            const int r = idx / kRowF4, c = idx - r * kRowF4;
+            dst[idx] = rows[r * kRowPad + c];
+        }
+    } else if constexpr (B > 0) {
+        write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
+    } else {
+        write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
+    }
     store_body(a, e, b, lag, DRAG, DYN);
     a.ist[HI_STEP * E + e] = sc;
     a.ist[HI_EPISODE * E + e] = ep;
@@ -533,8 +567,9 @@ struct HoverTail {
 };
 
 // DEF: compiled-in cf2x_consts (the reference default) instead of the device block.
+// STG: LDS-staged coalesced obs rows (host: only when E % kStepBlock == 0).
 // Launch with kStepBlock threads per workgroup.
-template <typename Real, int PH, int A, int B, bool DEF>
+template <typename Real, int PH, int A, int B, bool DEF, bool STG = false>
 __global__ void __launch_bounds__(256) hover_step_kernel(Real* f, float* ring, int32_t* ist, const float* act,
                                                          float* obs, float* rew, int E, HoverTail<Real> t) {
     HoverArgs<Real> a;
@@ -545,9 +580,9 @@ __global__ void __launch_bounds__(256) hover_step_kernel(Real* f, float* ring, i
     a.E = E; a.B = t.B; a.D = t.D; a.autoreset = t.autoreset;
     if constexpr (DEF) {
         constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
-        hover_step_body<Real, PH, A, B, C.S>(a, C);
+        hover_step_body<Real, PH, A, B, C.S, STG>(a, C);
     } else {
-        hover_step_body<Real, PH, A, B, 0>(a, *a.c);
+        hover_step_body<Real, PH, A, B, 0, STG>(a, *a.c);
     }
 }
 
