@@ -15,7 +15,7 @@ import torch  # noqa: F401  (binds the shared HIP runtime before libadrp loads)
 from .utils import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libadrp.so")
+LIB_PATH = os.environ.get("ADRP_LIB", os.path.join(HERE, "libadrp.so"))   # override: build experiments
 
 _lib = None
 

@@ -506,7 +506,8 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     else
 #pragma unroll
         for (int j = 0; j < A; ++j) a.ring[(size_t(head) * E + e) * A + j] = act[j];
-    const int head1 = head + 1 == B ? 0 : head + 1;
+    const int BB = B > 0 ? B : a.B;                    // ring length (runtime for the generic kernel)
+    const int head1 = head + 1 == BB ? 0 : head + 1;
     // ---- obs / reward / terminated / truncated (HoverAviary.py:68-117) ----
     float o12[12];
     const V3<Real> rpy = hover_obs12(C, b, o12);

@@ -239,3 +239,30 @@ def test_full_size_properties():
     fg = env.get_state()[0][:, sub].double().cpu().numpy()
     fo, _ = orc.get_state()
     np.testing.assert_allclose(fg[:13], fo[:13], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("ctrl_freq", [240, 60])
+def test_generic_ring_length(ctrl_freq):
+    """ctrl_freq != 30: ring length ctrl_freq // 2 != 15 and S = 240 / ctrl_freq -> the
+    generic (runtime ring length, device-constant) kernel"""
+    E = 128
+    env, orc = pair(E, ctrl_freq=ctrl_freq, autoreset=False, seed=3, initial_xyzs=[0, 0, 1.0],
+                    init_noise={"xyz": 0.1, "rpy": 0.1, "vel": 0.2, "omega": 0.5})
+    obs_g, _ = env.reset()
+    obs_o = orc.reset()
+    np.testing.assert_allclose(obs_g.cpu().numpy(), obs_o, atol=1e-6)
+    rng = np.random.default_rng(4)
+    B = ctrl_freq // 2
+    for k in range(B + 3):          # past the ring wrap-around
+        act = rng.uniform(-1, 1, (E, 1, 4)).astype(np.float32)
+        obs_o, rew_o, te_o, tr_o, _ = orc.step(act)
+        obs_g, rew_g, te_g, tr_g, _ = env.step(torch.from_numpy(act).to(env.device))
+        torch.cuda.synchronize()
+        if k % 10 == 0 or k >= B - 2:
+            compare_state(env, orc, 1e-4, active_fields(Physics.PYB))
+        np.testing.assert_array_equal(obs_g.cpu().numpy()[..., 12:], obs_o[..., 12:])
+        f, i = orc.get_state()
+        f = f.astype(np.float32).astype(np.float64)
+        orc.set_state(f, i)
+        env.set_state(torch.from_numpy(f.astype(np.float32)), torch.from_numpy(i))
+    env.close()
