@@ -342,16 +342,31 @@ __device__ __forceinline__ void write_row(float* row, const float o12[12], const
 // generic-B variant: the ring part is copied from HBM in logical order (slot head1 = oldest);
 // the newest entry (logical B-1) is this step's action
 template <int A>
-__device__ __forceinline__ void write_row_generic(float* row, const float o12[12], const float* ring, int B, int E,
-                                                  int e, int head1, const float act[A], bool act_is_newest) {
+__device__ __forceinline__ void write_row_generic(float* __restrict__ row, const float o12[12],
+                                                  const float* __restrict__ ring, int B, int E, int e, int head1,
+                                                  const float act[A], bool act_is_newest) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) row[k] = o12[k];
+    // chunks of 8 slots: all loads of a chunk in flight before its stores
+    constexpr int CH = 8;
     int slot = head1;
-    for (int k = 0; k < B; ++k) {
+    for (int k0 = 0; k0 < B; k0 += CH) {
+        float v[CH][A];
 #pragma unroll
-        for (int j = 0; j < A; ++j)
-            row[12 + k * A + j] = (act_is_newest && k == B - 1) ? act[j] : ring[(size_t(slot) * E + e) * A + j];
-        slot = slot + 1 == B ? 0 : slot + 1;
+        for (int c = 0; c < CH; ++c) {
+            const int k = k0 + c;
+#pragma unroll
+            for (int j = 0; j < A; ++j)
+                v[c][j] = k < B ? ((act_is_newest && k == B - 1) ? act[j] : ring[(size_t(slot) * E + e) * A + j]) : 0.0f;
+            slot = slot + 1 == B ? 0 : slot + 1;
+        }
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int k = k0 + c;
+            if (k < B)
+#pragma unroll
+                for (int j = 0; j < A; ++j) row[12 + k * A + j] = v[c][j];
+        }
     }
 }
 
