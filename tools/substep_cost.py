@@ -8,8 +8,9 @@ import torch
 sys.path.insert(0, ".")
 from gym_pybullet_adrp_amd.envs.hover import HoverAviary  # noqa: E402
 
-for ctrl in (240, 120, 60, 30):
-    env = HoverAviary(num_envs=4096, pyb_freq=240, ctrl_freq=ctrl, initial_xyzs=[0, 0, 1.0],
+for pyb in (120, 240, 480, 960):
+    ctrl = 30          # ring length 15 everywhere; S = pyb / 30 sub-steps
+    env = HoverAviary(num_envs=4096, pyb_freq=pyb, ctrl_freq=ctrl, initial_xyzs=[0, 0, 1.0],
                       init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1})
     env.reset()
     acts = torch.rand((8, 4096, 1, 4), device=env.device) * 2 - 1
@@ -20,6 +21,7 @@ for ctrl in (240, 120, 60, 30):
     for k in range(400):
         env.step(acts[k % 8])
     ms = env.h.profile_end(400)
-    print(json.dumps({"substeps": 240 // ctrl, "kernel_us": float(np.mean(ms)) * 1e3,
+    from gym_pybullet_adrp_amd import _lib
+    print(json.dumps({"substeps": pyb // ctrl, "kernel": _lib.kernel_name(env.cfg), "kernel_us": float(np.mean(ms)) * 1e3,
                       "kernel_us_median": float(np.median(ms)) * 1e3}), flush=True)
     env.close()
