@@ -1,10 +1,11 @@
-"""Summarise rocprofv3 --pmc passes of the HoverAviary step kernel into per-launch HBM bytes.
+"""Summarise rocprofv3 --pmc passes of a step kernel into per-launch HBM bytes.
 
 usage: python tools/pmc_summary.py OUT.json KEY FETCH_DIR WRITE_DIR [KEY FETCH_DIR WRITE_DIR ...]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is
-taken as is.  The first 8 dispatches (cold caches, first-touch) are skipped; the median of
+taken as is.  Keys starting with ``race_`` select race_step_kernel, the others
+hover_step_kernel.  The first 8 dispatches (cold caches, first-touch) are skipped; the median of
 the rest is reported.
 """
 import csv
@@ -14,16 +15,16 @@ import statistics
 import sys
 
 
-def counter(d, name):
+def counter(d, name, kernel):
     vals = []
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "hover_step_kernel" in r.get("Kernel_Name", "") and r["Counter_Name"] == name:
+            if kernel in r.get("Kernel_Name", "") and r["Counter_Name"] == name:
                 vals.append((int(r.get("Dispatch_Id", len(vals))), float(r["Counter_Value"])))
     vals = [v for _, v in sorted(vals)]
     steady = vals[8:] if len(vals) > 16 else vals
     if not steady:
-        raise SystemExit(f"no {name} rows for hover_step_kernel under {d}")
+        raise SystemExit(f"no {name} rows for {kernel} under {d}")
     return statistics.median(steady), len(vals)
 
 
@@ -35,11 +36,12 @@ def main():
         rec = {}
     for i in range(0, len(rest), 3):
         key, fdir, wdir = rest[i:i + 3]
-        fetch_kib, nf = counter(fdir, "FETCH_SIZE")
-        write_kib, nw = counter(wdir, "WRITE_SIZE")
+        kernel = "race_step_kernel" if key.startswith("race_") else "hover_step_kernel"
+        fetch_kib, nf = counter(fdir, "FETCH_SIZE", kernel)
+        write_kib, nw = counter(wdir, "WRITE_SIZE", kernel)
         rd = fetch_kib * 1024 * 2
         wr = write_kib * 1024
-        rec[key] = {"hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
+        rec[key] = {"kernel": kernel, "hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
                     "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib,
                     "dispatches": [nf, nw],
                     "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes; FETCH_SIZE x2 "
