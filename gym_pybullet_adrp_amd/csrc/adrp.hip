@@ -710,6 +710,20 @@ extern "C" int adrp_set_diagnostics(adrp_t* h, int enable) {
     return ADRP_OK;
 }
 
+#ifdef ADRP_RACE_TIMING
+// timing build only (not declared in include/adrp.h): per-phase s_memtime sums of
+// race_step_kernel -- [setup, physics, controller, rays, obs, contacts, tail, total, waves, -]
+extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_race_phase), 10 * sizeof(unsigned long long)) != hipSuccess)
+        return ADRP_ERR_DEVICE;
+    if (reset) {
+        static const unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_race_phase), z, sizeof z) != hipSuccess) return ADRP_ERR_DEVICE;
+    }
+    return ADRP_OK;
+}
+#endif
+
 extern "C" int adrp_diagnostic_contact_count(adrp_t* h, int reset) {
     if (!h) return ADRP_ERR_INVALID;
     int32_t v = 0;

@@ -80,6 +80,34 @@ __device__ __forceinline__ void small_sincos(float x, float* s, float* c) {
 }
 __device__ __forceinline__ void small_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 
+// fast fp32 transcendentals for the latency-bound sub-step loop (the fp64 overloads keep
+// libm). atan on [0,1] is an odd minimax polynomial (|err| <= 1.1e-7 rad, fitted by IRLS on
+// Chebyshev nodes, checked in fp32 Horner), after octant reduction with a hardware reciprocal.
+__device__ __forceinline__ float fatan2_(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    const float t = a * a;
+    float p = 0.0028487828094512224f;
+    p = p * t - 0.016064105555415154f;
+    p = p * t + 0.04268398508429527f;
+    p = p * t - 0.07503638416528702f;
+    p = p * t + 0.10640615969896317f;
+    p = p * t - 0.1420356035232544f;
+    p = p * t + 0.19992607831954956f;
+    p = p * t - 0.3333307206630707f;
+    p = p * t + 1.0f;
+    float r = a * p;
+    if (ay > ax) r = 1.57079632679489661923f - r;
+    if (x < 0.0f) r = 3.14159265358979323846f - r;
+    return copysignf(r, y);
+}
+__device__ __forceinline__ double fatan2_(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ float fasin_(float s) { return fatan2_(s, __builtin_amdgcn_sqrtf((1.0f - s) * (1.0f + s))); }
+__device__ __forceinline__ double fasin_(double s) { return asin(s); }
+__device__ __forceinline__ float fexp_(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ double fexp_(double x) { return exp(x); }
+
 // rotation matrix of a unit quaternion (body->world)
 template <typename Real>
 __device__ __forceinline__ M3<Real> rot(Q4<Real> q) {
@@ -120,6 +148,18 @@ __device__ __forceinline__ V3<Real> euler_xyz(Q4<Real> q) {
             atan2_(Real(2) * (q.x * q.y + q.w * q.z), squ + sqx - sqy - sqz)};
 }
 
+// euler_xyz with the fast fp32 atan2/asin (controller input inside the sub-step loop)
+template <typename Real>
+__device__ __forceinline__ V3<Real> euler_xyz_fast(Q4<Real> q) {
+    const Real sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
+    const Real sarg = Real(-2) * (q.x * q.z - q.w * q.y);
+    const Real half_pi = Real(1.57079632679489661923);
+    if (sarg <= Real(-0.99999)) return {Real(0), -half_pi, Real(2) * fatan2_(q.x, -q.y)};
+    if (sarg >= Real(0.99999)) return {Real(0), half_pi, Real(2) * fatan2_(-q.x, q.y)};
+    return {fatan2_(Real(2) * (q.y * q.z + q.w * q.x), squ - sqx - sqy + sqz), fasin_(sarg),
+            fatan2_(Real(2) * (q.x * q.y + q.w * q.z), squ + sqx - sqy - sqz)};
+}
+
 // getQuaternionFromEuler (rpy extrinsic xyz)
 template <typename Real>
 __device__ __forceinline__ Q4<Real> quat_from_euler(Real r, Real p, Real y) {
@@ -150,6 +190,9 @@ __device__ __forceinline__ U4 philox4x32_10(U4 ctr, uint32_t k0, uint32_t k1) {
 }
 // uniform in [0,1) with 24 random bits: exact in float and double alike
 __device__ __forceinline__ double u01(uint32_t x) { return double(x >> 8) * (1.0 / 16777216.0); }
+// the same value in Real (a 24-bit integer times 2^-24 is exact in fp32 too)
+template <typename Real>
+__device__ __forceinline__ Real u01r(uint32_t x) { return Real(x >> 8) * Real(1.0 / 16777216.0); }
 
 // counter layout (shared by specification with the oracle):
 //   {global env id (low 32 bits), episode, tag, index}, key = {seed lo, seed hi}

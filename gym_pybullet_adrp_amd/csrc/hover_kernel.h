@@ -258,11 +258,6 @@ __device__ __forceinline__ void dyn_substep(const HoverConst<Real>& a, Body<Real
     b.angv = mul(R, b.w);   // resetBaseVelocity(vel, rotation @ rpy_rates)
 }
 
-template <typename Real>
-__device__ __forceinline__ Real u01r(uint32_t x) {
-    return Real(x >> 8) * Real(1.0 / 16777216.0);
-}
-
 // BaseAviary.reset -> _housekeeping (+ the optional init_noise extension), Real precision
 template <typename Real>
 __device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& args, const HoverConst<Real>& C, int e,

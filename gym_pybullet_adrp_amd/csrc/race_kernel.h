@@ -23,6 +23,17 @@ constexpr uint32_t TAG_RACE_NOISE = 0x524e0000u;
 constexpr uint32_t TAG_RACE_DIST = 0x52460000u;
 constexpr int kRaceBlock = 64;
 
+// phase timing (build with -DADRP_RACE_TIMING; tools/race_phases.py): lane 0 of every wave
+// adds its s_memtime deltas per phase of race_step_kernel
+#ifdef ADRP_RACE_TIMING
+__device__ unsigned long long g_race_phase[10];
+#define RACE_MARK(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define RACE_ACC(i, dt) atomicAdd(&g_race_phase[i], (unsigned long long)(dt))
+#else
+#define RACE_MARK(var)
+#define RACE_ACC(i, dt)
+#endif
+
 // per-drone SoA fields ([field][E*N]); env fields are replicated in every drone slot
 enum RaceField {
     RF_POS = 0, RF_QUAT = 3, RF_VEL = 7, RF_OMEGA = 10, RF_RPM = 13, RF_PREV_RPM = 17, RF_ANGV = 21,
@@ -76,6 +87,8 @@ struct RaceArgs {
 __device__ __forceinline__ float clampf_(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 template <typename Real>
 __device__ __forceinline__ Real clampr_(Real v, Real lo, Real hi) { return v < lo ? lo : (v > hi ? hi : v); }
+template <typename Real>
+__device__ __forceinline__ Real fmaxr_(Real a, Real b) { return a > b ? a : b; }
 __device__ __forceinline__ float radf_(float d) { return (3.14159265358979323846f / 180.0f) * d; }
 __device__ __forceinline__ float degf_(float r) { return (180.0f / 3.14159265358979323846f) * r; }
 
@@ -143,7 +156,7 @@ __device__ __forceinline__ V3<Real> tri_closest(V3<Real> a, V3<Real> b, V3<Real>
 // Euclidean distance of two convex shapes (0 if they overlap); GJK with the simplex kept
 // in named registers (no dynamic indexing -> no scratch)
 template <typename Real>
-__device__ __noinline__ Real gjk_distance(const Shape<Real>& A, const Shape<Real>& B) {
+__device__ __forceinline__ Real gjk_distance(const Shape<Real>& A, const Shape<Real>& B) {
     const Real eps = sizeof(Real) == 4 ? Real(1e-6) : Real(1e-13);
     V3<Real> W0, W1, W2, W3;
     int n = 0;
@@ -268,50 +281,6 @@ template <typename Real>
 __device__ __forceinline__ void obst_part(int k, V3<Real>& off, V3<Real>& h, Real& r, int& cyl) {
     if (k == 0) { off = v3(Real(0), Real(0), Real(0)); h = v3(Real(0), Real(0), Real(0.4)); r = Real(0.05); cyl = 1; }
     else { off = v3(Real(0), Real(0), Real(-0.4)); h = v3(Real(0.075), Real(0.075), Real(0.125)); r = Real(0); cyl = 0; }
-}
-
-// min distance drone <-> gate g or obstacle; parts whose bounding sphere is farther than
-// `cut` are skipped (their distance is then reported as >= cut)
-template <typename Real>
-__device__ __noinline__ Real gate_distance(const Shape<Real>& ds, V3<Real> org, Real yaw, int low, Real cut) {
-    const M3<Real> Rg = rotz_(yaw);
-    const Real dr = sqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
-    Real best = Real(3.0e38);
-    for (int k = 0; k < 5; ++k) {
-        V3<Real> off, h;
-        M3<Real> R;
-        Real r;
-        int cyl;
-        gate_part(k, low, off, R, h, r, cyl);
-        Shape<Real> s{org + mul(Rg, off), mmul_(Rg, R), h, r, cyl};
-        const Real pr = cyl ? sqrt_(r * r + h.z * h.z) : sqrt_(dot(h, h));
-        const V3<Real> dc = s.c - ds.c;
-        const Real lb = sqrt_(dot(dc, dc)) - pr - dr;
-        if (lb >= cut) { if (lb < best) best = lb; continue; }
-        const Real dd = gjk_distance(ds, s);
-        if (dd < best) best = dd;
-    }
-    return best;
-}
-template <typename Real>
-__device__ __noinline__ Real obst_distance(const Shape<Real>& ds, V3<Real> org, Real cut) {
-    const M3<Real> I = {Real(1), Real(0), Real(0), Real(0), Real(1), Real(0), Real(0), Real(0), Real(1)};
-    const Real dr = sqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
-    Real best = Real(3.0e38);
-    for (int k = 0; k < 2; ++k) {
-        V3<Real> off, h;
-        Real r;
-        int cyl;
-        obst_part(k, off, h, r, cyl);
-        Shape<Real> s{org + off, I, h, r, cyl};
-        const Real pr = cyl ? sqrt_(r * r + h.z * h.z) : sqrt_(dot(h, h));
-        const V3<Real> dc = s.c - ds.c;
-        const Real lb = sqrt_(dot(dc, dc)) - pr - dr;
-        if (lb >= cut) { if (lb < best) best = lb; continue; }
-        const Real dd = gjk_distance(ds, s);
-        if (dd < best) best = dd;
-    }
-    return best;
 }
 
 template <typename Real>
@@ -724,12 +693,135 @@ __device__ __forceinline__ void race_dyn_substep(const RaceConst<Real>& C, RDron
 }
 
 // ---------------------------------------------------------------------------------------
+// drone <-> track queries: getClosestPoints(distance=0.45) in-range flags (_computeObs 591-651)
+// and contacts (_collision 552-562) as decisions "min part distance < cut".
+//
+// Exact bounds decide almost every (drone, part) pair without GJK. With p the centre of the
+// drone's collision cylinder and dr its bounding radius, dist(p, part) - dr <= dist(drone,
+// part) <= dist(p, part); dist(p, part) to a box / cylinder is closed form. Only pairs whose
+// bounds straddle a cut (by more than the rounding guard) are queued; each lane then walks
+// its own queue, so a wave runs max-over-lanes GJKs instead of one per part any lane needs.
+// ---------------------------------------------------------------------------------------
+template <typename Real>
+__device__ __forceinline__ Real point_part_dist(V3<Real> lp, V3<Real> h, Real r, int cyl) {
+    if (cyl) {
+        const Real dr = fmaxr_(hsqrt_(lp.x * lp.x + lp.y * lp.y) - r, Real(0));
+        const Real dz = fmaxr_(fabs_(lp.z) - h.z, Real(0));
+        return hsqrt_(dr * dr + dz * dz);
+    }
+    const Real dx = fmaxr_(fabs_(lp.x) - h.x, Real(0)), dy = fmaxr_(fabs_(lp.y) - h.y, Real(0)),
+               dz = fmaxr_(fabs_(lp.z) - h.z, Real(0));
+    return hsqrt_(dx * dx + dy * dy + dz * dz);
+}
+
+constexpr int kGateParts = 5, kObstParts = 2, kObstBit0 = ADRP_MAX_GATES * kGateParts;
+
+// placed collision shape of queue bit b (gate b / 5, part b % 5; obstacle bits from kObstBit0)
+template <typename Real>
+__device__ __forceinline__ Shape<Real> track_part_shape(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
+                                                        int b) {
+    V3<Real> off, h;
+    Real r;
+    int cyl;
+    if (b < kObstBit0) {
+        const int g = b / kGateParts, k = b - g * kGateParts;
+        M3<Real> R;
+        gate_part(k, C.gate_type[g] > 0, off, R, h, r, cyl);
+        const V3<Real> org = v3(ld(f, RF_GATE + 4 * g, EN, slot), ld(f, RF_GATE + 4 * g + 1, EN, slot),
+                                ld(f, RF_GATE + 4 * g + 2, EN, slot));
+        const M3<Real> Rg = rotz_(ld(f, RF_GATE + 4 * g + 3, EN, slot));
+        return Shape<Real>{org + mul(Rg, off), mmul_(Rg, R), h, r, cyl};
+    }
+    const int o = (b - kObstBit0) / kObstParts, k = (b - kObstBit0) - o * kObstParts;
+    obst_part(k, off, h, r, cyl);
+    const V3<Real> org = v3(ld(f, RF_OBST + 3 * o, EN, slot), ld(f, RF_OBST + 3 * o + 1, EN, slot),
+                            ld(f, RF_OBST + 3 * o + 2, EN, slot));
+    const M3<Real> I = {Real(1), Real(0), Real(0), Real(0), Real(1), Real(0), Real(0), Real(0), Real(1)};
+    return Shape<Real>{org + off, I, h, r, cyl};
+}
+
+// in-range bits (gate g -> bit g, obstacle k -> bit k) for `cut`; returns the contact
+// decision (distance < ccut) when want_contact
+template <typename Real>
+__device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
+                                            const Shape<Real>& ds, Real cut, bool want_contact, Real ccut,
+                                            uint32_t& gin, uint32_t& oin) {
+    const Real tol = sizeof(Real) == 4 ? Real(1e-5) : Real(1e-10);
+    const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
+    const V3<Real> p = ds.c;
+    uint32_t amb = 0;   // queued pairs
+    gin = 0; oin = 0;
+#pragma unroll
+    for (int g = 0; g < ADRP_MAX_GATES; ++g) {
+        if (g < C.num_gates) {
+            const V3<Real> dp = p - v3(ld(f, RF_GATE + 4 * g, EN, slot), ld(f, RF_GATE + 4 * g + 1, EN, slot),
+                                       ld(f, RF_GATE + 4 * g + 2, EN, slot));
+            Real sn, cs;
+            sincos_(ld(f, RF_GATE + 4 * g + 3, EN, slot), &sn, &cs);
+            const V3<Real> lg = v3(cs * dp.x + sn * dp.y, -sn * dp.x + cs * dp.y, dp.z);   // Rz(yaw)^T dp
+            const int low = C.gate_type[g] > 0;
+            bool in = false;
+            uint32_t gamb = 0, camb = 0;
+#pragma unroll
+            for (int k = 0; k < kGateParts; ++k) {
+                V3<Real> off, h;
+                M3<Real> R;
+                Real r;
+                int cyl;
+                gate_part(k, low, off, R, h, r, cyl);
+                const Real pd = point_part_dist(mulT(R, lg - off), h, r, cyl);
+                in |= pd < cut - tol;
+                if (pd - dr < cut + tol) gamb |= 1u << k;
+                if (want_contact && pd - dr < ccut + tol) camb |= 1u << k;
+            }
+            if (in) gin |= 1u << g;
+            amb |= ((in ? 0u : gamb) | camb) << (g * kGateParts);
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < ADRP_MAX_OBSTACLES; ++o) {
+        if (o < C.num_obstacles) {
+            const V3<Real> dp = p - v3(ld(f, RF_OBST + 3 * o, EN, slot), ld(f, RF_OBST + 3 * o + 1, EN, slot),
+                                       ld(f, RF_OBST + 3 * o + 2, EN, slot));
+            bool in = false;
+            uint32_t gamb = 0, camb = 0;
+#pragma unroll
+            for (int k = 0; k < kObstParts; ++k) {
+                V3<Real> off, h;
+                Real r;
+                int cyl;
+                obst_part(k, off, h, r, cyl);
+                const Real pd = point_part_dist(dp - off, h, r, cyl);
+                in |= pd < cut - tol;
+                if (pd - dr < cut + tol) gamb |= 1u << k;
+                if (want_contact && pd - dr < ccut + tol) camb |= 1u << k;
+            }
+            if (in) oin |= 1u << o;
+            amb |= ((in ? 0u : gamb) | camb) << (kObstBit0 + o * kObstParts);
+        }
+    }
+    bool contact = false;
+    while (amb) {
+        const int b = __builtin_ctz(amb);
+        amb &= amb - 1;
+        const Shape<Real> s = track_part_shape(C, f, EN, slot, b);
+        const Real dd = gjk_distance(ds, s);
+        if (dd < ccut) contact = true;
+        if (dd < cut) {
+            if (b < kObstBit0) gin |= 1u << (b / kGateParts);
+            else oin |= 1u << ((b - kObstBit0) / kObstParts);
+        }
+    }
+    return want_contact && contact;
+}
+
+// ---------------------------------------------------------------------------------------
 // obs row (MultiRaceAviary._computeObs, 566-661) written straight to global memory
 // ---------------------------------------------------------------------------------------
 template <typename Real>
 __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
                                              V3<Real> pos, Q4<Real> q, V3<Real> vel, V3<Real> w, int gate,
-                                             float* row, bool write, Real* row0) {
+                                             float* row, bool write, Real* row0, uint32_t gin, uint32_t oin) {
     const V3<Real> rpy = euler_xyz(q);
     const Real k12[12] = {pos.x, pos.y, pos.z, rpy.x, rpy.y, rpy.z, vel.x, vel.y, vel.z, w.x, w.y, w.z};
     if (write)
@@ -738,7 +830,7 @@ __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Rea
     if (row0)
 #pragma unroll
         for (int k = 0; k < 3; ++k) row0[k] = k12[k];
-    const Shape<Real> ds = drone_shape(C, pos, q);
+#pragma unroll
     for (int g = 0; g < ADRP_MAX_GATES; ++g) {
         Real v4[4] = {Real(0), Real(0), Real(0), Real(0)};
         Real in = 0;
@@ -746,7 +838,7 @@ __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Rea
             const V3<Real> org = v3(ld(f, RF_GATE + 4 * g, EN, slot), ld(f, RF_GATE + 4 * g + 1, EN, slot),
                                     ld(f, RF_GATE + 4 * g + 2, EN, slot));
             const Real yaw = ld(f, RF_GATE + 4 * g + 3, EN, slot);
-            in = gate_distance(ds, org, yaw, C.gate_type[g] > 0, Real(0.45)) < Real(0.45) ? Real(1) : Real(0);
+            in = (gin >> g) & 1u ? Real(1) : Real(0);
             if (in > Real(0)) { v4[0] = org.x; v4[1] = org.y; v4[2] = org.z; v4[3] = yaw; }
             else {
 #pragma unroll
@@ -762,13 +854,14 @@ __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Rea
 #pragma unroll
             for (int j = 0; j < 3; ++j) row0[3 + 3 * g + j] = v4[j];
     }
+#pragma unroll
     for (int k = 0; k < ADRP_MAX_OBSTACLES; ++k) {
         Real v3_[3] = {Real(0), Real(0), Real(0)};
         Real in = 0;
         if (k < C.num_obstacles) {
             const V3<Real> org = v3(ld(f, RF_OBST + 3 * k, EN, slot), ld(f, RF_OBST + 3 * k + 1, EN, slot),
                                     ld(f, RF_OBST + 3 * k + 2, EN, slot));
-            in = obst_distance(ds, org, Real(0.45)) < Real(0.45) ? Real(1) : Real(0);
+            in = (oin >> k) & 1u ? Real(1) : Real(0);
             if (in > Real(0)) { v3_[0] = org.x; v3_[1] = org.y; v3_[2] = org.z; }
             else {
 #pragma unroll
@@ -824,7 +917,9 @@ __device__ __noinline__ void race_reset_lane(const RaceArgs<Real>& a, const Race
     const Q4<Real> nq = quat_from_euler(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
     Real row0[15];
     const V3<Real> zero = v3(Real(0), Real(0), Real(0));
-    race_obs_row(C, f, EN, slot, npos, nq, zero, zero, 0, obs_row, obs_row != nullptr, row0);
+    uint32_t gin, oin;
+    track_query(C, f, EN, slot, drone_shape(C, npos, nq), Real(0.45), false, Real(0), gin, oin);
+    race_obs_row(C, f, EN, slot, npos, nq, zero, zero, 0, obs_row, obs_row != nullptr, row0, gin, oin);
     if (C.compete && obs_row) {   // other drones' nominal pos + rpy
         int idx = 0;
         for (int k = 0; k < C.N; ++k) {
@@ -899,6 +994,7 @@ __device__ __noinline__ void race_reset_lane(const RaceArgs<Real>& a, const Race
 // ---------------------------------------------------------------------------------------
 template <typename Real, int PH, int G>
 __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a) {
+    RACE_MARK(t0);
     const RaceConst<Real>& C = *a.c;
     // register copy of the constants the sub-step loop reads (uniform -> SGPRs; no reloads
     // behind the state stores, which the compiler cannot prove do not alias a.c)
@@ -954,7 +1050,14 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
         lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
         lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
     }
+    RACE_MARK(t1);
+#ifdef ADRP_RACE_TIMING
+    uint64_t acc_phys = 0;
+#endif
     for (int s = 0; s < H.S; ++s) {
+#ifdef ADRP_RACE_TIMING
+        RACE_MARK(ta);
+#endif
         const uint32_t idx = uint32_t(sc0 + s);
         if (PH != ADRP_PHYS_PYB) d.kpos = d.pos;          // KIN_PHYSICS read-back
         if constexpr (PH == ADRP_PHYS_DYN) {
@@ -964,14 +1067,17 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
             if constexpr (PH == ADRP_PHYS_PYB_DW || PH == ADRP_PHYS_PYB_GND_DRAG_DW) {
                 // _downwash (BaseAviary.py:792-818): every other drone above, LINK_FRAME on link 4
                 Real fz = 0;
-                for (int k = 0; k < N; ++k) {
+                constexpr bool F32 = sizeof(Real) == 4;
+#pragma unroll
+                for (int k = 0; k < G; ++k) {   // all shuffles in flight at once
                     const Real ox = shfl_(d.pos.x, k, G), oy = shfl_(d.pos.y, k, G), oz = shfl_(d.pos.z, k, G);
                     const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
                     const Real dxy = hsqrt_(dx * dx + dy * dy);
-                    if (dz > Real(0) && dxy < Real(10)) {
-                        const Real kk = H.prop_r / (Real(4) * dz);
+                    if (k < N && dz > Real(0) && dxy < Real(10)) {
+                        const Real kk = F32 ? H.prop_r * rcp_(Real(4) * dz) : H.prop_r / (Real(4) * dz);
                         const Real alpha = H.dw1 * kk * kk, beta = H.dw2 * dz + H.dw3;
-                        fz -= alpha * exp_(Real(-0.5) * (dxy / beta) * (dxy / beta));
+                        const Real q = F32 ? dxy * rcp_(beta) : dxy / beta;
+                        fz -= alpha * fexp_(Real(-0.5) * q * q);
                     }
                 }
                 const M3<Real> Rs = H.link_lag && !(PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? rot(d.ql) : rot(d.q);
@@ -979,15 +1085,19 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
             }
             if (H.disturbances) {   // world-frame force on link 4 at posObj = self.pos (532-544)
                 const U4 u = draw(a.seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), idx);
-                const V3<Real> fd = v3(H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * Real(u01(u.a)),
-                                       H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * Real(u01(u.b)),
-                                       H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * Real(u01(u.c)));
+                const V3<Real> fd = v3(H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * u01r<Real>(u.a),
+                                       H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * u01r<Real>(u.b),
+                                       H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * u01r<Real>(u.c));
                 const V3<Real> lo = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? d.pos : d.lpos;
                 Fx = Fx + fd;
                 Tx = cross(d.kpos - lo, fd);
             }
             race_pyb_substep<Real, PH>(H, d, Fx, Tx);
         }
+#ifdef ADRP_RACE_TIMING
+        RACE_MARK(tb);
+        acc_phys += tb - ta;
+#endif
         d.kpos = d.pos;
         if (d.flags & 1) {      // eliminated: motors off (233-235)
 #pragma unroll
@@ -1001,16 +1111,23 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                 for (int p = 0; p < 2; ++p) {
                     const Real u1 = (Real(x[2 * p] >> 8) + Real(1)) * Real(1.0 / 16777216.0);
                     const Real u2 = Real(x[2 * p + 1] >> 8) * Real(1.0 / 16777216.0);
-                    const Real r = sqrt_(Real(-2) * log(u1));
-                    Real sn, cs;
-                    sincos_(Real(6.283185307179586) * u2, &sn, &cs);
+                    Real r, sn, cs;
+                    if constexpr (sizeof(Real) == 4) {   // v_log_f32 is log2; v_sin/v_cos take turns
+                        r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+                        sn = __builtin_amdgcn_sinf(u2);
+                        cs = __builtin_amdgcn_cosf(u2);
+                    } else {
+                        r = sqrt_(Real(-2) * log(u1));
+                        sincos_(Real(6.283185307179586) * u2, &sn, &cs);
+                    }
                     noise[2 * p] = r * cs * H.noise_std;
                     noise[2 * p + 1] = r * sn * H.noise_std;
                 }
             }
-            mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz(d.q), noise);
+            mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz_fast(d.q), noise);
         }
     }
+    RACE_MARK(t2);
     // ---- _gate_progress (471-506): rays of my current gate vs every drone of the env ----
     V3<Real> gpos[ADRP_MAX_DRONES];
     Q4<Real> gq[ADRP_MAX_DRONES];
@@ -1027,15 +1144,28 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
         Real sn, cs;
         sincos_(rotg, &sn, &cs);
         const Real dx = Real(0.05) * cs, dy = Real(0.05) * sn;
+        // the 7 rays span the rectangle {g + t u + z e_z : |t| <= 0.15, |z - h| <= half};
+        // drones whose bounding sphere (about pos: |z offset| + cylinder radius) misses it
+        // cannot be hit, and a pass needs this lane's own drone to be hit
+        const Real br = fabs_(C.coll_zoff) + hsqrt_(C.coll_r * C.coll_r + C.coll_hh * C.coll_hh) +
+                        (sizeof(Real) == 4 ? Real(1e-5) : Real(1e-10));
+        uint32_t near = 0;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const Real ex = gpos[k].x - gx, ey = gpos[k].y - gy;
+            const Real ta = fmaxr_(fabs_(cs * ex + sn * ey) - Real(0.15), Real(0)), tb = -sn * ex + cs * ey;
+            const Real tz = fmaxr_(fabs_(gpos[k].z - h) - half, Real(0));
+            if (k < N && ta * ta + tb * tb + tz * tz < br * br) near |= 1u << k;
+        }
         bool passed = false;
-        for (int r = -3; r <= 3 && !passed; ++r) {
+        for (int r = -3; r <= 3 && !passed && ((near >> dn) & 1u); ++r) {
             const V3<Real> p0 = v3(gx + Real(r) * dx, gy + Real(r) * dy, h - half);
             const V3<Real> p1 = v3(gx + Real(r) * dx, gy + Real(r) * dy, h + half);
             Real best = Real(2);
             int who = -1;
 #pragma unroll
             for (int k = 0; k < G; ++k) {
-                if (k < N) {
+                if ((near >> k) & 1u) {
                     const Shape<Real> sk = drone_shape(C, gpos[k], gq[k]);
                     const Real fr = ray_cylinder(sk, p0, p1);
                     if (fr < best) { best = fr; who = k; }
@@ -1046,11 +1176,15 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
         if (passed) d.gate += 1;
     }
     if (gate0 >= C.num_gates) d.flags |= 2;
+    RACE_MARK(t3);
     // ---- obs row, elimination (674-698) ----
     const V3<Real> wv = PH == ADRP_PHYS_DYN ? d.angv : d.w;
     float* row = a.obs + slot * size_t(C.D);
     Real row0[15];
-    race_obs_row(C, a.f, EN, slot, d.pos, d.q, d.vel, wv, d.gate, row, active, row0);
+    const Shape<Real> ds = drone_shape(C, d.pos, d.q);
+    uint32_t gin, oin;
+    bool crashed = track_query(C, a.f, EN, slot, ds, Real(0.45), true, Real(1e-6), gin, oin);
+    race_obs_row(C, a.f, EN, slot, d.pos, d.q, d.vel, wv, d.gate, row, active, row0, gin, oin);
     if (C.compete && active) {   // other drones' pos + rpy (653-659)
         int idx = 0;
 #pragma unroll
@@ -1064,19 +1198,8 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
             }
         }
     }
-    bool crashed = false;
+    RACE_MARK(t4);
     {
-        const Shape<Real> ds = drone_shape(C, d.pos, d.q);
-        for (int g = 0; g < C.num_gates && !crashed; ++g) {
-            const V3<Real> org = v3(ld(a.f, RF_GATE + 4 * g, EN, slot), ld(a.f, RF_GATE + 4 * g + 1, EN, slot),
-                                    ld(a.f, RF_GATE + 4 * g + 2, EN, slot));
-            crashed = gate_distance(ds, org, ld(a.f, RF_GATE + 4 * g + 3, EN, slot), C.gate_type[g] > 0, Real(1e-6)) < Real(1e-6);
-        }
-        for (int k = 0; k < C.num_obstacles && !crashed; ++k) {
-            const V3<Real> org = v3(ld(a.f, RF_OBST + 3 * k, EN, slot), ld(a.f, RF_OBST + 3 * k + 1, EN, slot),
-                                    ld(a.f, RF_OBST + 3 * k + 2, EN, slot));
-            crashed = obst_distance(ds, org, Real(1e-6)) < Real(1e-6);
-        }
         const M3<Real>& R = ds.R;
         const Real low = ds.c.z - ds.h.z * fabs_(R.a22) - ds.r * sqrt_(R.a02 * R.a02 + R.a12 * R.a12);
         if (low <= Real(1e-6)) crashed = true;
@@ -1084,12 +1207,18 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
 #pragma unroll
             for (int k = 0; k < G; ++k) {
                 if (k < N && k != dn && !crashed) {
-                    const Shape<Real> sk = drone_shape(C, gpos[k], gq[k]);
-                    crashed = gjk_distance(ds, sk) < Real(1e-6);
+                    // bounding spheres first: GJK only for drones closer than 2 dr
+                    const V3<Real> dc = gpos[k] - d.pos;
+                    const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
+                    if (dot(dc, dc) < (Real(2) * dr + Real(1e-4)) * (Real(2) * dr + Real(1e-4))) {
+                        const Shape<Real> sk = drone_shape(C, gpos[k], gq[k]);
+                        crashed = gjk_distance(ds, sk) < Real(1e-6);
+                    }
                 }
             }
         }
     }
+    RACE_MARK(t5);
     const bool oob = fabs_(d.pos.x) > C.bounds[0] || fabs_(d.pos.y) > C.bounds[1] || fabs_(d.pos.z) > C.bounds[2];
     const bool unstable = fabs_(wv.x) > Real(20) || fabs_(wv.y) > Real(20) || fabs_(wv.z) > Real(20);
     if (oob || unstable || crashed) d.flags |= 1;
@@ -1124,6 +1253,13 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
         if (active)
             for (int k = 0; k < 3; ++k) { st(a.f, RF_WR_TARGET + k, EN, slot, tgt[k]); st(a.f, RF_WR_PREV + k, EN, slot, row0[k]); }
     }
+#ifdef ADRP_RACE_TIMING
+    RACE_MARK(t6);
+    if (threadIdx.x == 0) {
+        RACE_ACC(0, t1 - t0); RACE_ACC(1, acc_phys); RACE_ACC(2, (t2 - t1) - acc_phys); RACE_ACC(3, t3 - t2);
+        RACE_ACC(4, t4 - t3); RACE_ACC(5, t5 - t4); RACE_ACC(6, t6 - t5); RACE_ACC(7, t6 - t0); RACE_ACC(8, 1);
+    }
+#endif
     if (!active) return;
     if (dn == 0) {
         a.rew[e] = reward;

@@ -1,0 +1,55 @@
+"""Per-phase cost of race_step_kernel (needs the timing build: make -C gym_pybullet_adrp_amd/csrc timing).
+
+usage: ADRP_LIB=gym_pybullet_adrp_amd/libadrp_timing.so python tools/race_phases.py [LEVEL DRONES PHYSICS MODE E]
+Prints, per configuration, the mean s_memtime cycles per wave spent in each phase and the
+kernel time from dispatch events.
+"""
+import ctypes
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from gym_pybullet_adrp_amd import _lib  # noqa: E402
+from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary  # noqa: E402
+from gym_pybullet_adrp_amd.utils.enums import Physics, RaceMode  # noqa: E402
+
+PHASES = ["setup", "physics", "controller", "rays", "obs", "contacts", "tail", "total"]
+CONFIGS = [("level0", 2, "PYB", "COMPARE", 2048), ("level3", 4, "PYB_DW", "COMPETE", 4096),
+           ("level3", 4, "PYB_DW", "COMPARE", 4096), ("level0", 4, "PYB", "COMPARE", 4096)]
+if len(sys.argv) > 5:
+    CONFIGS = [(sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]))]
+
+lib = ctypes.CDLL(_lib.LIB_PATH)
+lib.adrp_race_phase_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+buf = (ctypes.c_ulonglong * 10)()
+
+for level, n, phys, mode, E in CONFIGS:
+    env = MultiRaceAviary(level, num_drones=n, physics=Physics[phys], racemode=RaceMode[mode], num_envs=E, seed=7)
+    obs0, _ = env.reset()
+    gen = torch.Generator(device=env.device)
+    gen.manual_seed(3)
+    off = torch.rand((16, E, n, 3), generator=gen, device=env.device) * 0.6 - 0.3
+    tgt = obs0[..., :3].unsqueeze(0) + off
+    tgt[..., 2] = tgt[..., 2].clamp(0.2, 1.5)
+    acts = torch.cat([tgt, torch.zeros((16, E, n, 1), device=env.device)], -1).contiguous()
+    for k in range(100):
+        env.step(acts[k % 16])
+    torch.cuda.synchronize()
+    lib.adrp_race_phase_read(buf, 1)
+    nk = 100
+    env.h.profile_begin(nk)
+    for k in range(nk):
+        env.step(acts[k % 16])
+    ms = env.h.profile_end(nk)
+    lib.adrp_race_phase_read(buf, 1)
+    v = np.array(list(buf), dtype=np.float64)
+    waves = v[8]
+    per = {p: v[i] / waves for i, p in enumerate(PHASES)}
+    print(json.dumps({"config": f"{level} N={n} {phys} {mode} E={E}", "kernel": _lib.kernel_name(env.cfg),
+                      "kernel_us": float(np.mean(ms)) * 1e3,
+                      "cycles_per_wave": {k: round(x) for k, x in per.items()},
+                      "share": {k: round(per[k] / per["total"], 3) for k in PHASES[:-1]}}), flush=True)
+    env.close()
