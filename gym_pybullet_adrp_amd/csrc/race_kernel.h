@@ -26,12 +26,24 @@ constexpr int kRaceBlock = 64;
 // phase timing (build with -DADRP_RACE_TIMING; tools/race_phases.py): lane 0 of every wave
 // adds its s_memtime deltas per phase of race_step_kernel
 #ifdef ADRP_RACE_TIMING
-__device__ unsigned long long g_race_phase[10];
+__device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-phase max, [20..] controller parts
 #define RACE_MARK(var) const uint64_t var = __builtin_amdgcn_s_memtime()
-#define RACE_ACC(i, dt) atomicAdd(&g_race_phase[i], (unsigned long long)(dt))
+#define RACE_ACC(i, dt) do { atomicAdd(&g_race_phase[i], (unsigned long long)(dt)); \
+        atomicMax(&g_race_phase[10 + (i)], (unsigned long long)(dt)); } while (0)
 #else
 #define RACE_MARK(var)
 #define RACE_ACC(i, dt)
+#endif
+#ifdef ADRP_RACE_TIMING
+#define RACE_SUB(i, from, to) do { if (threadIdx.x == 0) atomicAdd(&g_race_phase[20 + (i)], (unsigned long long)((to) - (from))); } while (0)
+#else
+#define RACE_SUB(i, from, to)
+#endif
+#ifdef ADRP_RACE_TIMING
+#define GJK_STAT(n) do { atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
+        atomicMax(&g_race_phase[19], (unsigned long long)(n)); } while (0)
+#else
+#define GJK_STAT(n)
 #endif
 
 // per-drone SoA fields ([field][E*N]); env fields are replicated in every drone slot
@@ -153,23 +165,34 @@ __device__ __forceinline__ V3<Real> tri_closest(V3<Real> a, V3<Real> b, V3<Real>
     return a + (vb * den) * ab + (vc * den) * ac;
 }
 
-// Euclidean distance of two convex shapes (0 if they overlap); GJK with the simplex kept
-// in named registers (no dynamic indexing -> no scratch)
+// "distance(A, B) < cut" for two convex shapes, by GJK with the simplex kept in named
+// registers (no dynamic indexing -> no scratch). Every iterate v is a point of the
+// Minkowski difference, so |v| >= distance, and v.w / |v| <= distance for the support point
+// w: the loop stops as soon as either bound decides against `cut`, else on convergence.
 template <typename Real>
-__device__ __forceinline__ Real gjk_distance(const Shape<Real>& A, const Shape<Real>& B) {
-    const Real eps = sizeof(Real) == 4 ? Real(1e-6) : Real(1e-13);
+__device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Real>& B0, Real cut) {
+    // in A's centre frame: support points stay O(shape size), so the fp32 termination test
+    // is not swamped by rounding of world coordinates (which stalled convergence)
+    Shape<Real> A = A0, B = B0;
+    B.c = B0.c - A0.c;
+    A.c = v3(Real(0), Real(0), Real(0));
+    const Real eps = sizeof(Real) == 4 ? Real(4e-6) : Real(1e-13);
     V3<Real> W0, W1, W2, W3;
     int n = 0;
     V3<Real> v = A.c - B.c;
+    const Real cut2 = cut * cut;
     if (dot(v, v) < Real(1e-20)) v = v3(Real(1), Real(0), Real(0));
     for (int it = 0; it < 48; ++it) {
         const V3<Real> w = support(A, Real(-1) * v) - support(B, v);
-        const Real vv = dot(v, v);
-        if (vv - dot(v, w) <= eps * vv) break;
+        const Real vv = dot(v, v), vw = dot(v, w);
+        if (vw > Real(0) && vw * vw >= cut2 * vv) { GJK_STAT(it + 1); return false; }   // lower bound
+        if (vv - vw <= eps * vv) { GJK_STAT(it + 1); return vv < cut2; }
         const V3<Real> dw0 = W0 - w, dw1 = W1 - w, dw2 = W2 - w;
         if ((n > 0 && dot(dw0, dw0) < Real(1e-20)) || (n > 1 && dot(dw1, dw1) < Real(1e-20)) ||
-            (n > 2 && dot(dw2, dw2) < Real(1e-20)))
-            break;
+            (n > 2 && dot(dw2, dw2) < Real(1e-20))) {
+            GJK_STAT(it + 1);
+            return vv < cut2;
+        }
         if (n == 0) { W0 = w; n = 1; v = w; }
         else if (n == 1) {
             W1 = w;
@@ -212,12 +235,13 @@ __device__ __forceinline__ Real gjk_distance(const Shape<Real>& A, const Shape<R
                     if (dd < best) { best = dd; bv = vf; b0 = q0; b1 = q1; b2 = q2; bm = m; }
                 }
             }
-            if (!outside) return Real(0);
+            if (!outside) { GJK_STAT(it + 1); return true; }
             v = bv; W0 = b0; W1 = b1; W2 = b2; n = bm;
         }
-        if (dot(v, v) < Real(1e-20)) return Real(0);
+        if (dot(v, v) < cut2) { GJK_STAT(it + 1); return true; }   // upper bound
     }
-    return sqrt_(dot(v, v));
+    GJK_STAT(48);
+    return dot(v, v) < cut2;
 }
 
 // entry fraction of the segment p0 -> p1 into a cylinder, > 1 on a miss
@@ -471,6 +495,7 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
                                                   float xc_y, V3<Real> rpy, const Real noise[4]) {
 #pragma clang fp contract(off)   // numpy / C arithmetic of the reference wrapper and firmware
     constexpr bool F32 = sizeof(Real) == 4;   // fp32 kernel: reciprocal multiplies; fp64: numpy's divisions
+    RACE_MARK(c0);
     const Real fdt = Real(0.002);
     const Real r2d = Real(57.29577951308232);
     Real rates[3];
@@ -490,6 +515,8 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
 #pragma unroll
     for (int k = 0; k < 3; ++k) gyro[k] = lpf_apply(lpf, d.lpf1[k], d.lpf2[k], float(rates[k] * r2d));
     Real pwm[4];
+    RACE_MARK(c1);
+    RACE_SUB(2, c0, c1);
     if (float(acc_z) < -0.5f) d.tumble += 1; else d.tumble = 0;
     if (d.tumble >= 30) {
         d.tick += 1;
@@ -541,6 +568,8 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
             pwm[k] = pct * Real(65535);
         }
     }
+    RACE_MARK(c2);
+    RACE_SUB(3, c1, c2);
     // clip -> thrust -> reorder [3,2,1,0] -> + noise -> _thr2pwm -> rpm (246-262)
     Real th[4];
 #pragma unroll
@@ -558,6 +587,8 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
         d.prev[k] = d.rpm[k];
         d.rpm[k] = Real(0.2685) * mp + Real(4070.3);
     }
+    RACE_MARK(c3);
+    RACE_SUB(4, c2, c3);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -749,7 +780,7 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real
     const Real tol = sizeof(Real) == 4 ? Real(1e-5) : Real(1e-10);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
     const V3<Real> p = ds.c;
-    uint32_t amb = 0;   // queued pairs
+    uint32_t amb = 0, camb_all = 0;   // queued pairs; those queued for the contact cut
     gin = 0; oin = 0;
 #pragma unroll
     for (int g = 0; g < ADRP_MAX_GATES; ++g) {
@@ -776,6 +807,7 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real
             }
             if (in) gin |= 1u << g;
             amb |= ((in ? 0u : gamb) | camb) << (g * kGateParts);
+            camb_all |= camb << (g * kGateParts);
         }
     }
 #pragma unroll
@@ -798,17 +830,20 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real
             }
             if (in) oin |= 1u << o;
             amb |= ((in ? 0u : gamb) | camb) << (kObstBit0 + o * kObstParts);
+            camb_all |= camb << (kObstBit0 + o * kObstParts);
         }
     }
+    // a contact-queued pair has its drone centre within dr of the part, so its body is
+    // already in range by the upper bound: each queued pair needs exactly one of the cuts
     bool contact = false;
     while (amb) {
         const int b = __builtin_ctz(amb);
         amb &= amb - 1;
+        const bool for_contact = (camb_all >> b) & 1u;
         const Shape<Real> s = track_part_shape(C, f, EN, slot, b);
-        const Real dd = gjk_distance(ds, s);
-        if (dd < ccut) contact = true;
-        if (dd < cut) {
-            if (b < kObstBit0) gin |= 1u << (b / kGateParts);
+        if (gjk_within(ds, s, for_contact ? ccut : cut)) {
+            if (for_contact) contact = true;
+            else if (b < kObstBit0) gin |= 1u << (b / kGateParts);
             else oin |= 1u << ((b - kObstBit0) / kObstParts);
         }
     }
@@ -882,7 +917,7 @@ __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Rea
 // (MultiRaceAviary.reset 127-167, _addObstacles 347-403, _drone_init 407-467)
 // ---------------------------------------------------------------------------------------
 template <typename Real>
-__device__ __noinline__ void race_reset_lane(const RaceArgs<Real>& a, const RaceConst<Real>& C, int e, int dn, size_t EN,
+__device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const RaceConst<Real>& C, int e, int dn, size_t EN,
                                 size_t slot, int episode, float* obs_row) {
     const uint64_t gid = uint64_t(a.env_offset + e);
     const uint32_t ep = uint32_t(episode);
@@ -1103,6 +1138,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
 #pragma unroll
             for (int k = 0; k < 4; ++k) d.rpm[k] = d.prev[k] = Real(0);
         } else {
+            RACE_MARK(n0);
             Real noise[4] = {Real(0), Real(0), Real(0), Real(0)};
             if (H.disturbances) {
                 const U4 u = draw(a.seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
@@ -1124,7 +1160,12 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                     noise[2 * p + 1] = r * sn * H.noise_std;
                 }
             }
-            mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz_fast(d.q), noise);
+            RACE_MARK(n1);
+            RACE_SUB(0, n0, n1);
+            const V3<Real> rpy_in = euler_xyz_fast(d.q);
+            RACE_MARK(n2);
+            RACE_SUB(1, n1, n2);
+            mellinger_compute(d, lpf, sp, xc_x, xc_y, rpy_in, noise);
         }
     }
     RACE_MARK(t2);
@@ -1212,7 +1253,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
                     if (dot(dc, dc) < (Real(2) * dr + Real(1e-4)) * (Real(2) * dr + Real(1e-4))) {
                         const Shape<Real> sk = drone_shape(C, gpos[k], gq[k]);
-                        crashed = gjk_distance(ds, sk) < Real(1e-6);
+                        crashed = gjk_within(ds, sk, Real(1e-6));
                     }
                 }
             }

@@ -1,8 +1,9 @@
 """Per-phase cost of race_step_kernel (needs the timing build: make -C gym_pybullet_adrp_amd/csrc timing).
 
 usage: ADRP_LIB=gym_pybullet_adrp_amd/libadrp_timing.so python tools/race_phases.py [LEVEL DRONES PHYSICS MODE E]
-Prints, per configuration, the mean s_memtime cycles per wave spent in each phase and the
-kernel time from dispatch events.
+Prints, per configuration, the s_memtime cycles per wave spent in each phase (mean over
+waves, and the slowest wave per launch averaged over launches) and the kernel time from
+dispatch events.
 """
 import ctypes
 import json
@@ -24,7 +25,7 @@ if len(sys.argv) > 5:
 
 lib = ctypes.CDLL(_lib.LIB_PATH)
 lib.adrp_race_phase_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-buf = (ctypes.c_ulonglong * 10)()
+buf = (ctypes.c_ulonglong * 32)()
 
 for level, n, phys, mode, E in CONFIGS:
     env = MultiRaceAviary(level, num_drones=n, physics=Physics[phys], racemode=RaceMode[mode], num_envs=E, seed=7)
@@ -40,16 +41,28 @@ for level, n, phys, mode, E in CONFIGS:
     torch.cuda.synchronize()
     lib.adrp_race_phase_read(buf, 1)
     nk = 100
+    sums = np.zeros(32)
+    mx = np.zeros(8)
+    gjk_max = 0
     env.h.profile_begin(nk)
     for k in range(nk):
         env.step(acts[k % 16])
+        torch.cuda.synchronize()
+        lib.adrp_race_phase_read(buf, 1)
+        v = np.array(list(buf), dtype=np.float64)
+        sums += v
+        mx += v[10:18]
+        gjk_max = max(gjk_max, v[19])
     ms = env.h.profile_end(nk)
-    lib.adrp_race_phase_read(buf, 1)
-    v = np.array(list(buf), dtype=np.float64)
-    waves = v[8]
-    per = {p: v[i] / waves for i, p in enumerate(PHASES)}
+    waves = sums[8]
+    mean = {p: sums[i] / waves for i, p in enumerate(PHASES)}
+    slow = {p: mx[i] / nk for i, p in enumerate(PHASES)}
     print(json.dumps({"config": f"{level} N={n} {phys} {mode} E={E}", "kernel": _lib.kernel_name(env.cfg),
                       "kernel_us": float(np.mean(ms)) * 1e3,
-                      "cycles_per_wave": {k: round(x) for k, x in per.items()},
-                      "share": {k: round(per[k] / per["total"], 3) for k in PHASES[:-1]}}), flush=True)
+                      "mean_cycles_per_wave": {k: round(x) for k, x in mean.items()},
+                      "max_cycles_per_launch": {k: round(x) for k, x in slow.items()},
+                      "controller_parts": dict(zip(["noise", "euler", "wrapper_lpf", "firmware", "pwm_chain"],
+                                                   [round(x) for x in sums[20:25] / waves])),
+                      "gjk": {"calls_per_launch": sums[9] / nk, "mean_iters": sums[18] / max(sums[9], 1),
+                              "max_iters": gjk_max}}), flush=True)
     env.close()
