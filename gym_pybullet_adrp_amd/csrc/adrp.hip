@@ -713,8 +713,7 @@ extern "C" int adrp_set_diagnostics(adrp_t* h, int enable) {
 #ifdef ADRP_RACE_TIMING
 // timing build only (not declared in include/adrp.h): per-phase s_memtime sums of
 // race_step_kernel -- [setup, physics, controller, rays, obs, contacts, tail, total, waves, -] sums
-// over waves, the same phases' max over waves at [10..17], GJK calls/iterations at 9/18/19, and
-// controller parts [noise, euler, wrapper+lpf, schedule+firmware, pwm chain] at [20..24]
+// over waves, the same phases' max over waves at [10..17], GJK calls/iterations at 9/18/19
 extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_race_phase), 32 * sizeof(unsigned long long)) != hipSuccess)
         return ADRP_ERR_DEVICE;

@@ -26,7 +26,7 @@ constexpr int kRaceBlock = 64;
 // phase timing (build with -DADRP_RACE_TIMING; tools/race_phases.py): lane 0 of every wave
 // adds its s_memtime deltas per phase of race_step_kernel
 #ifdef ADRP_RACE_TIMING
-__device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-phase max, [20..] controller parts
+__device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-phase max, 9/18/19 GJK
 #define RACE_MARK(var) const uint64_t var = __builtin_amdgcn_s_memtime()
 #define RACE_ACC(i, dt) do { atomicAdd(&g_race_phase[i], (unsigned long long)(dt)); \
         atomicMax(&g_race_phase[10 + (i)], (unsigned long long)(dt)); } while (0)
@@ -34,11 +34,7 @@ __device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-p
 #define RACE_MARK(var)
 #define RACE_ACC(i, dt)
 #endif
-#ifdef ADRP_RACE_TIMING
-#define RACE_SUB(i, from, to) do { if (threadIdx.x == 0) atomicAdd(&g_race_phase[20 + (i)], (unsigned long long)((to) - (from))); } while (0)
-#else
-#define RACE_SUB(i, from, to)
-#endif
+
 #ifdef ADRP_RACE_TIMING
 #define GJK_STAT(n) do { atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
         atomicMax(&g_race_phase[19], (unsigned long long)(n)); } while (0)
@@ -495,7 +491,6 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
                                                   float xc_y, V3<Real> rpy, const Real noise[4]) {
 #pragma clang fp contract(off)   // numpy / C arithmetic of the reference wrapper and firmware
     constexpr bool F32 = sizeof(Real) == 4;   // fp32 kernel: reciprocal multiplies; fp64: numpy's divisions
-    RACE_MARK(c0);
     const Real fdt = Real(0.002);
     const Real r2d = Real(57.29577951308232);
     Real rates[3];
@@ -515,8 +510,6 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
 #pragma unroll
     for (int k = 0; k < 3; ++k) gyro[k] = lpf_apply(lpf, d.lpf1[k], d.lpf2[k], float(rates[k] * r2d));
     Real pwm[4];
-    RACE_MARK(c1);
-    RACE_SUB(2, c0, c1);
     if (float(acc_z) < -0.5f) d.tumble += 1; else d.tumble = 0;
     if (d.tumble >= 30) {
         d.tick += 1;
@@ -568,8 +561,6 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
             pwm[k] = pct * Real(65535);
         }
     }
-    RACE_MARK(c2);
-    RACE_SUB(3, c1, c2);
     // clip -> thrust -> reorder [3,2,1,0] -> + noise -> _thr2pwm -> rpm (246-262)
     Real th[4];
 #pragma unroll
@@ -587,8 +578,6 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
         d.prev[k] = d.rpm[k];
         d.rpm[k] = Real(0.2685) * mp + Real(4070.3);
     }
-    RACE_MARK(c3);
-    RACE_SUB(4, c2, c3);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1138,7 +1127,6 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
 #pragma unroll
             for (int k = 0; k < 4; ++k) d.rpm[k] = d.prev[k] = Real(0);
         } else {
-            RACE_MARK(n0);
             Real noise[4] = {Real(0), Real(0), Real(0), Real(0)};
             if (H.disturbances) {
                 const U4 u = draw(a.seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
@@ -1160,12 +1148,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                     noise[2 * p + 1] = r * sn * H.noise_std;
                 }
             }
-            RACE_MARK(n1);
-            RACE_SUB(0, n0, n1);
-            const V3<Real> rpy_in = euler_xyz_fast(d.q);
-            RACE_MARK(n2);
-            RACE_SUB(1, n1, n2);
-            mellinger_compute(d, lpf, sp, xc_x, xc_y, rpy_in, noise);
+            mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz_fast(d.q), noise);
         }
     }
     RACE_MARK(t2);

@@ -61,8 +61,6 @@ for level, n, phys, mode, E in CONFIGS:
                       "kernel_us": float(np.mean(ms)) * 1e3,
                       "mean_cycles_per_wave": {k: round(x) for k, x in mean.items()},
                       "max_cycles_per_launch": {k: round(x) for k, x in slow.items()},
-                      "controller_parts": dict(zip(["noise", "euler", "wrapper_lpf", "firmware", "pwm_chain"],
-                                                   [round(x) for x in sums[20:25] / waves])),
                       "gjk": {"calls_per_launch": sums[9] / nk, "mean_iters": sums[18] / max(sums[9], 1),
                               "max_iters": gjk_max}}), flush=True)
     env.close()
