@@ -15,46 +15,15 @@
 #include <string>
 #include <vector>
 
-#include "../../include/adrp.h"
-#include "hover_kernel.h"
-#include "race_kernel.h"
-
-using namespace adrp;
-
-struct adrp_handle {
-    adrp_config cfg;
-    int device = 0;
-    int E = 0, N = 0, A = 0, D = 0, S = 0, B = 0;
-    int nf_base = 0, ni = 0;
-    size_t real_size = 4;
-    void* f = nullptr;        // Real [nf_base][E*N]
-    float* ring = nullptr;    // [B*A][E]
-    int32_t* ist = nullptr;   // [ni][E*N]
-    int32_t* counters = nullptr;  // device diagnostics (ground-model hits)
-    void* cblk = nullptr;         // device HoverConst<Real> + HoverReset<Real>
-    bool cf2x = false;            // compiled-in constants (hover_step_kernel<..., DEF=true>)
-    bool stage_rows = true;       // LDS-staged obs rows when E % 64 == 0 (ADRP_STAGE_ROWS=0 disables)
-    int diagnostics = 0;
-    // kernel timing (adrp_profile_begin/end)
-    std::vector<hipEvent_t> ev_start, ev_stop;
-    int prof_cap = 0, prof_n = 0;
-    std::string err;
-};
+#include "adrp_internal.h"
 
 static thread_local std::string g_err;
 
-static int seterr(adrp_t* h, int code, const std::string& msg) {
+int seterr(adrp_t* h, int code, const std::string& msg) {
     if (h) h->err = msg;
     g_err = msg;
     return code;
 }
-
-#define HIPCHK(h, x)                                                                            \
-    do {                                                                                        \
-        hipError_t e_ = (x);                                                                    \
-        if (e_ != hipSuccess)                                                                   \
-            return seterr(h, ADRP_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));  \
-    } while (0)
 
 extern "C" int adrp_abi_version(void) { return ADRP_ABI_VERSION; }
 
@@ -197,24 +166,6 @@ static bool config_is_cf2x(const adrp_config& c) {
 }
 
 template <typename Real>
-static HoverArgs<Real> hover_args(const adrp_t* h) {
-    const adrp_config& c = h->cfg;
-    HoverArgs<Real> a;
-    memset(&a, 0, sizeof a);
-    a.c = (const HoverConst<Real>*)h->cblk;
-    a.r = (const HoverReset<Real>*)((const char*)h->cblk + sizeof(HoverConst<Real>));
-    a.E = h->E; a.B = h->B; a.D = h->D;
-    a.autoreset = c.autoreset;
-    a.seed = c.seed;
-    a.env_offset = c.env_offset;
-    a.f = (Real*)h->f;
-    a.ring = h->ring;
-    a.ist = h->ist;
-    a.contact_count = h->diagnostics ? h->counters : nullptr;
-    return a;
-}
-
-template <typename Real>
 static int upload_const(adrp_t* h) {
     const HoverConst<Real> k = hover_const<Real>(h->cfg);
     const HoverReset<Real> r = hover_reset_dist<Real>(h->cfg);
@@ -301,7 +252,6 @@ static int upload_race_const(adrp_t* h) {
     return ADRP_OK;
 }
 
-static int race_group(int n) { return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : 8; }
 
 extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
     static thread_local char buf[96];
@@ -407,137 +357,6 @@ extern "C" void adrp_destroy(adrp_t* h) {
 extern "C" int adrp_obs_dim(const adrp_t* h) { return h ? h->D : ADRP_ERR_INVALID; }
 extern "C" int adrp_act_dim(const adrp_t* h) { return h ? h->A : ADRP_ERR_INVALID; }
 
-// ---------------------------------------------------------------------------------------------
-// launch dispatch
-// ---------------------------------------------------------------------------------------------
-constexpr int kBlock = kStepBlock;
-
-// launch with optional start/stop events recorded by the dispatch itself
-template <typename K, typename Real>
-static void launch(K kernel, dim3 grid, dim3 blk, hipStream_t s, const HoverArgs<Real>& a, adrp_t* h) {
-    HoverTail<Real> t;
-    memset(&t, 0, sizeof t);
-    t.c = a.c; t.r = a.r; t.term = a.term; t.trunc = a.trunc; t.tobs = a.tobs; t.contact_count = a.contact_count;
-    t.seed = a.seed; t.env_offset = a.env_offset; t.B = a.B; t.D = a.D; t.autoreset = a.autoreset;
-    if (h->prof_n < h->prof_cap) {
-        hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0,
-                              a.f, a.ring, a.ist, a.act, a.obs, a.rew, a.E, t);
-        ++h->prof_n;
-    } else {
-        hipLaunchKernelGGL(kernel, grid, blk, 0, s, a.f, a.ring, a.ist, a.act, a.obs, a.rew, a.E, t);
-    }
-}
-
-template <typename Real, int A, int B, bool DEF, bool STG = false>
-static void launch_step_ph(const HoverArgs<Real>& a, int physics, dim3 grid, hipStream_t s, adrp_t* h) {
-    const dim3 blk(kBlock);
-    switch (physics) {
-        case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B, DEF, STG>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B, DEF, STG>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_GND: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B, DEF, STG>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_DRAG: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B, DEF, STG>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_DW: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B, DEF, STG>, grid, blk, s, a, h); break;
-        default: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B, DEF, STG>, grid, blk, s, a, h); break;
-    }
-}
-
-template <typename Real>
-static int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
-                      float* tobs, hipStream_t s) {
-    HoverArgs<Real> a = hover_args<Real>(h);
-    a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
-    const dim3 grid((h->E + kBlock - 1) / kBlock);
-    const int ph = h->cfg.physics;
-    // compiled-in constants exist for the reference default (CF2X @ 240/30 Hz, B = 15)
-    const bool stg = h->stage_rows && h->E % kBlock == 0;
-    if (h->cf2x && h->B == 15) {
-        if (h->A == 1) launch_step_ph<Real, 1, 15, true>(a, ph, grid, s, h);
-        else if (stg) launch_step_ph<Real, 4, 15, true, true>(a, ph, grid, s, h);
-        else launch_step_ph<Real, 4, 15, true>(a, ph, grid, s, h);
-    } else if (h->A == 4 && h->B == 15 && stg) {
-        launch_step_ph<Real, 4, 15, false, true>(a, ph, grid, s, h);
-    } else if (h->A == 1) {
-        if (h->B == 15) launch_step_ph<Real, 1, 15, false>(a, ph, grid, s, h);
-        else launch_step_ph<Real, 1, 0, false>(a, ph, grid, s, h);
-    } else {
-        if (h->B == 15) launch_step_ph<Real, 4, 15, false>(a, ph, grid, s, h);
-        else launch_step_ph<Real, 4, 0, false>(a, ph, grid, s, h);
-    }
-    HIPCHK(h, hipGetLastError());
-    return ADRP_OK;
-}
-
-template <typename Real>
-static int hover_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s) {
-    HoverArgs<Real> a = hover_args<Real>(h);
-    a.mask = mask; a.obs = obs;
-    const dim3 grid((h->E + kBlock - 1) / kBlock);
-    if (h->A == 1) hipLaunchKernelGGL((hover_reset_kernel<Real, 1>), grid, dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((hover_reset_kernel<Real, 4>), grid, dim3(kBlock), 0, s, a);
-    HIPCHK(h, hipGetLastError());
-    return ADRP_OK;
-}
-
-template <typename Real>
-static RaceArgs<Real> race_args(const adrp_t* h) {
-    RaceArgs<Real> a;
-    memset(&a, 0, sizeof a);
-    a.c = (const RaceConst<Real>*)h->cblk;
-    a.f = (Real*)h->f;
-    a.ist = h->ist;
-    a.seed = h->cfg.seed;
-    a.env_offset = h->cfg.env_offset;
-    a.E = h->E;
-    return a;
-}
-
-template <typename Real, int PH>
-static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
-    const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G + kRaceBlock - 1) / kRaceBlock));
-    auto go = [&](auto kernel) {
-        if (h->prof_n < h->prof_cap) {
-            hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
-            ++h->prof_n;
-        } else {
-            hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
-        }
-    };
-    switch (G) {
-        case 1: go(race_step_kernel<Real, PH, 1>); break;
-        case 2: go(race_step_kernel<Real, PH, 2>); break;
-        case 4: go(race_step_kernel<Real, PH, 4>); break;
-        default: go(race_step_kernel<Real, PH, 8>); break;
-    }
-}
-
-template <typename Real>
-static int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
-                     float* tobs, hipStream_t s) {
-    RaceArgs<Real> a = race_args<Real>(h);
-    a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
-    const int G = race_group(h->N);
-    switch (h->cfg.physics) {
-        case ADRP_PHYS_PYB: launch_race_g<Real, ADRP_PHYS_PYB>(a, G, s, h); break;
-        case ADRP_PHYS_DYN: launch_race_g<Real, ADRP_PHYS_DYN>(a, G, s, h); break;
-        case ADRP_PHYS_PYB_GND: launch_race_g<Real, ADRP_PHYS_PYB_GND>(a, G, s, h); break;
-        case ADRP_PHYS_PYB_DRAG: launch_race_g<Real, ADRP_PHYS_PYB_DRAG>(a, G, s, h); break;
-        case ADRP_PHYS_PYB_DW: launch_race_g<Real, ADRP_PHYS_PYB_DW>(a, G, s, h); break;
-        default: launch_race_g<Real, ADRP_PHYS_PYB_GND_DRAG_DW>(a, G, s, h); break;
-    }
-    HIPCHK(h, hipGetLastError());
-    return ADRP_OK;
-}
-
-template <typename Real>
-static int race_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s) {
-    RaceArgs<Real> a = race_args<Real>(h);
-    a.mask = mask; a.obs = obs;
-    const dim3 grid((unsigned)((size_t(h->E) * h->N + kRaceBlock - 1) / kRaceBlock));
-    hipLaunchKernelGGL((race_reset_kernel<Real>), grid, dim3(kRaceBlock), 0, s, a);
-    HIPCHK(h, hipGetLastError());
-    return ADRP_OK;
-}
-
 extern "C" int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev, void* stream) {
     if (!h || !obs_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_reset: NULL argument");
     HIPCHK(h, hipSetDevice(h->device));
@@ -561,6 +380,33 @@ extern "C" int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float*
     return h->real_size == 8 ? hover_step<double>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s)
                              : hover_step<float>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s);
 }
+
+namespace adrp {
+// snapshot <-> internal ring: user fields ring_{s}_{j} = [B*A][E] (physical slot s, per-env
+// ring_head); internal [B][E][A].  Both keep the same physical slots and heads.
+__global__ void ring_get_kernel(const float* __restrict__ ring, void* dst, int is_double, int B, int A, int E) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    for (int s = 0; s < B; ++s)
+        for (int j = 0; j < A; ++j) {
+            const float v = ring[(size_t(s) * E + e) * A + j];
+            const size_t o = size_t(s * A + j) * E + e;
+            if (is_double) static_cast<double*>(dst)[o] = v;
+            else static_cast<float*>(dst)[o] = v;
+        }
+}
+__global__ void ring_set_kernel(float* __restrict__ ring, const void* src, int is_double, int B, int A, int E) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    for (int s = 0; s < B; ++s)
+        for (int j = 0; j < A; ++j) {
+            const size_t o = size_t(s * A + j) * E + e;
+            ring[(size_t(s) * E + e) * A + j] =
+                is_double ? float(static_cast<const double*>(src)[o]) : static_cast<const float*>(src)[o];
+        }
+}
+
+}  // namespace adrp
 
 // ---------------------------------------------------------------------------------------------
 // state snapshot
@@ -711,15 +557,22 @@ extern "C" int adrp_set_diagnostics(adrp_t* h, int enable) {
 }
 
 #ifdef ADRP_RACE_TIMING
-// timing build only (not declared in include/adrp.h): per-phase s_memtime sums of
-// race_step_kernel -- [setup, physics, controller, rays, obs, contacts, tail, total, waves, -] sums
-// over waves, the same phases' max over waves at [10..17], GJK calls/iterations at 9/18/19
+// timing build only (not declared in include/adrp.h): per-phase s_memtime sums of the step
+// kernels -- race: [setup, physics, controller, rays, obs, contacts, tail, total, waves, -]
+// sums over waves, the same phases' max over waves at [10..17], GJK calls/iterations at
+// 9/18/19; hover: tools/hover_phases.py.  Summed over the four kernel code objects.
 extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_race_phase), 32 * sizeof(unsigned long long)) != hipSuccess)
-        return ADRP_ERR_DEVICE;
-    if (reset) {
-        static const unsigned long long z[32] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_race_phase), z, sizeof z) != hipSuccess) return ADRP_ERR_DEVICE;
+    int (*readers[4])(unsigned long long*, int) = {phase_read_hover_f32, phase_read_hover_f64, phase_read_race_f32,
+                                                  phase_read_race_f64};
+    for (int k = 0; k < 32; ++k) out[k] = 0;
+    for (auto rd : readers) {
+        unsigned long long v[32];
+        const int rc = rd(v, reset);
+        if (rc != ADRP_OK) return rc;
+        for (int k = 0; k < 32; ++k) {
+            const bool is_max = (k >= 10 && k <= 17) || k == 19;
+            out[k] = is_max ? std::max(out[k], v[k]) : out[k] + v[k];
+        }
     }
     return ADRP_OK;
 }

@@ -10,6 +10,19 @@
 
 namespace adrp {
 
+// phase timing (build with -DADRP_RACE_TIMING; tools/race_phases.py, tools/hover_phases.py):
+// lane 0 of every wave adds its s_memtime deltas per phase of the step kernel
+#ifdef ADRP_RACE_TIMING
+__device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-phase max, 9/18/19 GJK
+#define RACE_MARK(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define RACE_ACC(i, dt) do { atomicAdd(&g_race_phase[i], (unsigned long long)(dt)); \
+        atomicMax(&g_race_phase[10 + (i)], (unsigned long long)(dt)); } while (0)
+#else
+#define RACE_MARK(var)
+#define RACE_ACC(i, dt)
+#endif
+
+
 template <typename Real>
 struct V3 {
     Real x, y, z;

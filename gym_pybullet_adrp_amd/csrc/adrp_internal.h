@@ -1,0 +1,114 @@
+// adrp_internal.h — host-side handle and launch plumbing shared by the libadrp translation
+// units (adrp.hip: the C-ABI; hover_f32/f64.hip, race_f32/f64.hip: kernel instantiations and
+// their launchers, compiled in parallel).
+#pragma once
+
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/adrp.h"
+#include "hover_kernel.h"
+#include "race_kernel.h"
+
+using namespace adrp;
+
+int seterr(adrp_t* h, int code, const std::string& msg);
+
+struct adrp_handle {
+    adrp_config cfg;
+    int device = 0;
+    int E = 0, N = 0, A = 0, D = 0, S = 0, B = 0;
+    int nf_base = 0, ni = 0;
+    size_t real_size = 4;
+    void* f = nullptr;        // Real [nf_base][E*N]
+    float* ring = nullptr;    // [B*A][E]
+    int32_t* ist = nullptr;   // [ni][E*N]
+    int32_t* counters = nullptr;  // device diagnostics (ground-model hits)
+    void* cblk = nullptr;         // device HoverConst<Real> + HoverReset<Real>
+    bool cf2x = false;            // compiled-in constants (hover_step_kernel<..., DEF=true>)
+    bool stage_rows = true;       // LDS-staged obs rows when E % 64 == 0 (ADRP_STAGE_ROWS=0 disables)
+    int diagnostics = 0;
+    // kernel timing (adrp_profile_begin/end)
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    int prof_cap = 0, prof_n = 0;
+    std::string err;
+};
+
+
+
+#define HIPCHK(h, x)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess)                                                                   \
+            return seterr(h, ADRP_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));  \
+    } while (0)
+
+constexpr int kBlock = kStepBlock;
+
+inline int race_group(int n) { return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : 8; }
+
+template <typename Real>
+inline HoverArgs<Real> hover_args(const adrp_t* h) {
+    const adrp_config& c = h->cfg;
+    HoverArgs<Real> a;
+    memset(&a, 0, sizeof a);
+    a.c = (const HoverConst<Real>*)h->cblk;
+    a.r = (const HoverReset<Real>*)((const char*)h->cblk + sizeof(HoverConst<Real>));
+    a.E = h->E; a.B = h->B; a.D = h->D;
+    a.autoreset = c.autoreset;
+    a.seed = c.seed;
+    a.env_offset = c.env_offset;
+    a.f = (Real*)h->f;
+    a.ring = h->ring;
+    a.ist = h->ist;
+    a.contact_count = h->diagnostics ? h->counters : nullptr;
+    return a;
+}
+
+template <typename Real>
+inline RaceArgs<Real> race_args(const adrp_t* h) {
+    RaceArgs<Real> a;
+    memset(&a, 0, sizeof a);
+    a.c = (const RaceConst<Real>*)h->cblk;
+    a.f = (Real*)h->f;
+    a.ist = h->ist;
+    a.seed = h->cfg.seed;
+    a.env_offset = h->cfg.env_offset;
+    a.E = h->E;
+    return a;
+}
+
+// launchers (one translation unit per task x precision)
+template <typename Real>
+int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc, float* tobs,
+               hipStream_t s);
+template <typename Real>
+int hover_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s);
+template <typename Real>
+int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc, float* tobs,
+              hipStream_t s);
+template <typename Real>
+int race_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s);
+
+#ifdef ADRP_RACE_TIMING
+// each kernel translation unit is its own code object with its own g_race_phase
+int phase_read_hover_f32(unsigned long long* out, int reset);
+int phase_read_hover_f64(unsigned long long* out, int reset);
+int phase_read_race_f32(unsigned long long* out, int reset);
+int phase_read_race_f64(unsigned long long* out, int reset);
+#define ADRP_PHASE_READER(name)                                                                  \
+    int name(unsigned long long* out, int reset) {                                               \
+        if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_race_phase), 32 * sizeof(unsigned long long)) != hipSuccess) \
+            return ADRP_ERR_DEVICE;                                                              \
+        if (reset) {                                                                             \
+            static const unsigned long long z[32] = {};                                          \
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_race_phase), z, sizeof z) != hipSuccess) return ADRP_ERR_DEVICE; \
+        }                                                                                        \
+        return ADRP_OK;                                                                          \
+    }
+#endif

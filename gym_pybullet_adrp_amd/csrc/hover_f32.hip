@@ -1,0 +1,10 @@
+// hover_f32.hip — hover kernels and launchers for Real = float (own translation unit so
+// the kernel instantiations compile in parallel)
+#include "hover_launch.h"
+
+template int hover_step<float>(adrp_t*, const float*, float*, float*, uint8_t*, uint8_t*, float*, hipStream_t);
+template int hover_reset<float>(adrp_t*, const uint8_t*, float*, hipStream_t);
+
+#ifdef ADRP_RACE_TIMING
+ADRP_PHASE_READER(phase_read_hover_f32)
+#endif

@@ -439,6 +439,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     const int E = a.E;
     const int D = B > 0 ? 12 + B * A : a.D;
     if (e >= E) return;
+    RACE_MARK(t0);
     // ---- issue every load up front: action, the whole ring, ints, state ----
     float act[A];
     if constexpr (A == 4) {
@@ -470,6 +471,11 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     for (int i = 0; i < 4; ++i) rpm[i] = C.hover_rpm * Real(rpm_gain(act[A == 1 ? 0 : i]));
     // ---- sub-step loop (BaseAviary.py:347-376) ----
     bool touched = false;
+#ifdef ADRP_RACE_TIMING
+    // loads landed: the rpm gains and the state are consumed by the first sub-step
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    RACE_MARK(t1);
     if constexpr (DYN) {
         if constexpr (SC > 0) {
 #pragma unroll
@@ -503,6 +509,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
             for (int s = 0; s < C.S; ++s) substep();
         }
     }
+    RACE_MARK(t2);
     if (touched && a.contact_count) atomicAdd(a.contact_count, 1);
     // ---- action ring: append this action at `head` (deque.append, BaseRLAviary.py:187) ----
 #pragma unroll
@@ -531,6 +538,10 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     a.term[e] = te;
     a.trunc[e] = tr;
     sc += C.S;
+    RACE_MARK(t3);
+#ifdef ADRP_RACE_TIMING
+    const unsigned long long dmask = __ballot(a.autoreset && (te || tr));
+#endif
     if (a.autoreset && (te || tr)) {
         if (a.tobs) {
             if constexpr (B > 0) write_row<A, B>(a.tobs + size_t(e) * D, o12, ring, head1);
@@ -539,6 +550,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         hover_reset_state(a, C, e, b, sc, ep);
         hover_obs12(C, b, o12);
     }
+    RACE_MARK(t4);
     if constexpr (STG) {
         static_assert(A == 4 && B == 15, "staged rows: 72-float rows only");
         __shared__ float4 rows[kStepBlock * kRowPad];
@@ -556,10 +568,20 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     } else {
         write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
     }
+    RACE_MARK(t5);
     store_body(a, e, b, lag, DRAG, DYN);
     a.ist[HI_STEP * E + e] = sc;
     a.ist[HI_EPISODE * E + e] = ep;
     a.ist[HI_RING_HEAD * E + e] = head1;
+#ifdef ADRP_RACE_TIMING
+    RACE_MARK(t6);
+    if (threadIdx.x == 0) {   // [loads, sub-steps, obs+flags, reset, obs row, state stores, total, -, waves]
+        RACE_ACC(0, t1 - t0); RACE_ACC(1, t2 - t1); RACE_ACC(2, t3 - t2); RACE_ACC(3, t4 - t3);
+        RACE_ACC(4, t5 - t4); RACE_ACC(5, t6 - t5); RACE_ACC(6, t6 - t0); RACE_ACC(8, 1);
+        RACE_ACC(7, __popcll(dmask));
+        if (dmask) atomicAdd(&g_race_phase[9], 1ull);
+    }
+#endif
 }
 
 // Arguments the step needs at wave start are separate scalars so the CP preloads them into
@@ -617,30 +639,6 @@ __global__ void __launch_bounds__(256) hover_reset_kernel(HoverArgs<Real> a) {
     hover_obs12(C, b, o12);
     const float none[A] = {};
     write_row_generic<A>(a.obs + size_t(e) * a.D, o12, a.ring, a.B, E, e, head, none, false);
-}
-
-// snapshot <-> internal ring: user fields ring_{s}_{j} = [B*A][E] (physical slot s, per-env
-// ring_head); internal [B][E][A].  Both keep the same physical slots and heads.
-__global__ void ring_get_kernel(const float* __restrict__ ring, void* dst, int is_double, int B, int A, int E) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
-    for (int s = 0; s < B; ++s)
-        for (int j = 0; j < A; ++j) {
-            const float v = ring[(size_t(s) * E + e) * A + j];
-            const size_t o = size_t(s * A + j) * E + e;
-            if (is_double) static_cast<double*>(dst)[o] = v;
-            else static_cast<float*>(dst)[o] = v;
-        }
-}
-__global__ void ring_set_kernel(float* __restrict__ ring, const void* src, int is_double, int B, int A, int E) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
-    for (int s = 0; s < B; ++s)
-        for (int j = 0; j < A; ++j) {
-            const size_t o = size_t(s * A + j) * E + e;
-            ring[(size_t(s) * E + e) * A + j] =
-                is_double ? float(static_cast<const double*>(src)[o]) : static_cast<const float*>(src)[o];
-        }
 }
 
 }  // namespace adrp

@@ -1,0 +1,10 @@
+// race_f64.hip — race kernels and launchers for Real = double (own translation unit so
+// the kernel instantiations compile in parallel)
+#include "race_launch.h"
+
+template int race_step<double>(adrp_t*, const float*, float*, float*, uint8_t*, uint8_t*, float*, hipStream_t);
+template int race_reset<double>(adrp_t*, const uint8_t*, float*, hipStream_t);
+
+#ifdef ADRP_RACE_TIMING
+ADRP_PHASE_READER(phase_read_race_f64)
+#endif

@@ -23,18 +23,6 @@ constexpr uint32_t TAG_RACE_NOISE = 0x524e0000u;
 constexpr uint32_t TAG_RACE_DIST = 0x52460000u;
 constexpr int kRaceBlock = 64;
 
-// phase timing (build with -DADRP_RACE_TIMING; tools/race_phases.py): lane 0 of every wave
-// adds its s_memtime deltas per phase of race_step_kernel
-#ifdef ADRP_RACE_TIMING
-__device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-phase max, 9/18/19 GJK
-#define RACE_MARK(var) const uint64_t var = __builtin_amdgcn_s_memtime()
-#define RACE_ACC(i, dt) do { atomicAdd(&g_race_phase[i], (unsigned long long)(dt)); \
-        atomicMax(&g_race_phase[10 + (i)], (unsigned long long)(dt)); } while (0)
-#else
-#define RACE_MARK(var)
-#define RACE_ACC(i, dt)
-#endif
-
 #ifdef ADRP_RACE_TIMING
 #define GJK_STAT(n) do { atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
         atomicMax(&g_race_phase[19], (unsigned long long)(n)); } while (0)

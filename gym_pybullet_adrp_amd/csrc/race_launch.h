@@ -1,0 +1,51 @@
+// race_launch.h — MultiRaceAviary step/reset launchers (instantiated by race_f32.hip / race_f64.hip)
+#pragma once
+
+#include "adrp_internal.h"
+
+template <typename Real, int PH>
+static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
+    const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G + kRaceBlock - 1) / kRaceBlock));
+    auto go = [&](auto kernel) {
+        if (h->prof_n < h->prof_cap) {
+            hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
+            ++h->prof_n;
+        } else {
+            hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
+        }
+    };
+    switch (G) {
+        case 1: go(race_step_kernel<Real, PH, 1>); break;
+        case 2: go(race_step_kernel<Real, PH, 2>); break;
+        case 4: go(race_step_kernel<Real, PH, 4>); break;
+        default: go(race_step_kernel<Real, PH, 8>); break;
+    }
+}
+
+template <typename Real>
+int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                     float* tobs, hipStream_t s) {
+    RaceArgs<Real> a = race_args<Real>(h);
+    a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
+    const int G = race_group(h->N);
+    switch (h->cfg.physics) {
+        case ADRP_PHYS_PYB: launch_race_g<Real, ADRP_PHYS_PYB>(a, G, s, h); break;
+        case ADRP_PHYS_DYN: launch_race_g<Real, ADRP_PHYS_DYN>(a, G, s, h); break;
+        case ADRP_PHYS_PYB_GND: launch_race_g<Real, ADRP_PHYS_PYB_GND>(a, G, s, h); break;
+        case ADRP_PHYS_PYB_DRAG: launch_race_g<Real, ADRP_PHYS_PYB_DRAG>(a, G, s, h); break;
+        case ADRP_PHYS_PYB_DW: launch_race_g<Real, ADRP_PHYS_PYB_DW>(a, G, s, h); break;
+        default: launch_race_g<Real, ADRP_PHYS_PYB_GND_DRAG_DW>(a, G, s, h); break;
+    }
+    HIPCHK(h, hipGetLastError());
+    return ADRP_OK;
+}
+
+template <typename Real>
+int race_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s) {
+    RaceArgs<Real> a = race_args<Real>(h);
+    a.mask = mask; a.obs = obs;
+    const dim3 grid((unsigned)((size_t(h->E) * h->N + kRaceBlock - 1) / kRaceBlock));
+    hipLaunchKernelGGL((race_reset_kernel<Real>), grid, dim3(kRaceBlock), 0, s, a);
+    HIPCHK(h, hipGetLastError());
+    return ADRP_OK;
+}
