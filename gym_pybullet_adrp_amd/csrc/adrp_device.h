@@ -184,6 +184,26 @@ __device__ __forceinline__ Q4<Real> quat_from_euler(Real r, Real p, Real y) {
             cr * cp * sy - sr * sp * cy, cr * cp * cy + sr * sp * sy};
 }
 
+// getQuaternionFromEuler with the half-angle sin/cos from the small-angle polynomial when all
+// three half angles are within pi/8 (exact in fp32, as small_sincos), else from libm; fp64
+// is always libm
+template <typename Real>
+__device__ __forceinline__ Q4<Real> quat_from_euler_fast(Real r, Real p, Real y) {
+    if constexpr (sizeof(Real) == 4) {
+        const Real hr = r * Real(0.5), hp = p * Real(0.5), hy = y * Real(0.5);
+        const Real lim = Real(0.39269908169872414);
+        if (fabs_(hr) <= lim && fabs_(hp) <= lim && fabs_(hy) <= lim) {
+            Real sr, cr, sp, cp, sy, cy;
+            small_sincos(hr, &sr, &cr);
+            small_sincos(hp, &sp, &cp);
+            small_sincos(hy, &sy, &cy);
+            return {sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy,
+                    cr * cp * sy - sr * sp * cy, cr * cp * cy + sr * sp * sy};
+        }
+    }
+    return quat_from_euler(r, p, y);
+}
+
 // ---- Philox4x32-10 (Salmon et al. SC'11) -------------------------------------------------
 struct U4 {
     uint32_t a, b, c, d;

@@ -279,7 +279,7 @@ __device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& args, c
     om[0] = a.n_om[0] * (Real(2) * u01r<Real>(w0[3]) - Real(1));
     om[1] = a.n_om[1] * (Real(2) * u01r<Real>(w1[3]) - Real(1));
     om[2] = a.n_om[2] * (Real(2) * u01r<Real>(w2[3]) - Real(1));
-    b.q = quat_from_euler<Real>(e_[0], e_[1], e_[2]);
+    b.q = quat_from_euler_fast<Real>(e_[0], e_[1], e_[2]);
     b.pos = v3(p[0], p[1], p[2]);
     b.ql = b.q;
     b.vel = v3(v[0], v[1], v[2]);
@@ -298,7 +298,7 @@ __device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& args, c
 
 template <typename Real>
 __device__ __forceinline__ V3<Real> hover_obs12(const HoverConst<Real>& a, const Body<Real>& b, float o[12]) {
-    const V3<Real> rpy = euler_xyz(b.q);
+    const V3<Real> rpy = euler_xyz_fast(b.q);
     const V3<Real> w = a.physics == ADRP_PHYS_DYN ? b.angv : b.w;
     o[0] = float(b.pos.x); o[1] = float(b.pos.y); o[2] = float(b.pos.z);
     o[3] = float(rpy.x);   o[4] = float(rpy.y);   o[5] = float(rpy.z);
@@ -413,7 +413,6 @@ __device__ __forceinline__ void store_body(const HoverArgs<Real>& a, int e, cons
 // obs rows staged in LDS, then written as one contiguous, fully coalesced block of
 // 64 rows (the row-per-lane float4 stores leave partial 64-B lines: +18 % write traffic)
 constexpr int kRowF4 = 18;        // 72 floats = 18 float4 per obs row (A = 4, B = 15)
-constexpr int kRowPad = 19;       // LDS row stride in float4 (bank spread)
 
 template <int A, int B>
 __device__ __forceinline__ void stage_row(float4* lds_row, const float o12[12], const float (&ring)[B][A], int head1) {
@@ -512,12 +511,6 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     RACE_MARK(t2);
     if (touched && a.contact_count) atomicAdd(a.contact_count, 1);
     // ---- action ring: append this action at `head` (deque.append, BaseRLAviary.py:187) ----
-#pragma unroll
-    for (int p = 0; p < B; ++p) {
-        const bool hit = p == head;
-#pragma unroll
-        for (int j = 0; j < A; ++j) ring[p][j] = hit ? act[j] : ring[p][j];
-    }
     if constexpr (A == 4)
         reinterpret_cast<float4*>(a.ring)[size_t(head) * E + e] = make_float4(act[0], act[1], act[2], act[3]);
     else
@@ -538,35 +531,82 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     a.term[e] = te;
     a.trunc[e] = tr;
     sc += C.S;
+    const bool done = a.autoreset && (te || tr);
     RACE_MARK(t3);
 #ifdef ADRP_RACE_TIMING
-    const unsigned long long dmask = __ballot(a.autoreset && (te || tr));
+    const unsigned long long dmask = __ballot(done);
 #endif
-    if (a.autoreset && (te || tr)) {
-        if (a.tobs) {
-            if constexpr (B > 0) write_row<A, B>(a.tobs + size_t(e) * D, o12, ring, head1);
-            else write_row_generic<A>(a.tobs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
-        }
-        hover_reset_state(a, C, e, b, sc, ep);
-        hover_obs12(C, b, o12);
-    }
-    RACE_MARK(t4);
     if constexpr (STG) {
+        // The obs row is assembled in LDS (18 float4 per lane, no padding: the copy-out
+        // reads contiguous float4s at immediate offsets) and leaves as one coalesced block.
         static_assert(A == 4 && B == 15, "staged rows: 72-float rows only");
-        __shared__ float4 rows[kStepBlock * kRowPad];
-        stage_row<A, B>(rows + threadIdx.x * kRowPad, o12, ring, head1);
+        __shared__ float4 rows[kStepBlock * kRowF4];
+        float4* my = rows + threadIdx.x * kRowF4;
+        // Every env appends once per env.step and resets keep the ring, so the ring head is
+        // the same for every env in practice: then the slot -> row position map is scalar
+        // and the appended action simply overwrites the newest position.
+        const int hu = __builtin_amdgcn_readfirstlane(head);
+        if (__all(head == hu)) {
+            const int h1 = hu + 1 == B ? 0 : hu + 1;
+#pragma unroll
+            for (int p = 0; p < B; ++p) {
+                const int k = p >= h1 ? p - h1 : p - h1 + B;
+                my[3 + k] = make_float4(ring[p][0], ring[p][1], ring[p][2], ring[p][3]);
+            }
+            my[3 + B - 1] = make_float4(act[0], act[1], act[2], act[3]);
+        } else {
+#pragma unroll
+            for (int p = 0; p < B; ++p) {
+                const bool hit = p == head;
+#pragma unroll
+                for (int j = 0; j < A; ++j) ring[p][j] = hit ? act[j] : ring[p][j];
+            }
+            stage_row<A, B>(my, o12, ring, head1);
+        }
+        my[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
+        my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
+        my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
+        if (done) {
+            if (a.tobs) {   // terminal obs = the row just staged (this lane's own LDS row)
+                float4 t[kRowF4];
+#pragma unroll
+                for (int k = 0; k < kRowF4; ++k) t[k] = my[k];
+                float4* trow = reinterpret_cast<float4*>(a.tobs + size_t(e) * D);
+#pragma unroll
+                for (int k = 0; k < kRowF4; ++k) trow[k] = t[k];
+            }
+            hover_reset_state(a, C, e, b, sc, ep);
+            hover_obs12(C, b, o12);      // the reset keeps the ring: only the kinematic part changes
+            my[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
+            my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
+            my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
+        }
+        RACE_MARK(t4);
         __syncthreads();
         float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
+        float4 v[kRowF4];
 #pragma unroll
-        for (int k = 0; k < kRowF4; ++k) {
-            const int idx = threadIdx.x + kStepBlock * k;   // float4 index inside the block's rows
-            const int r = idx / kRowF4, c = idx - r * kRowF4;
-            dst[idx] = rows[r * kRowPad + c];
-        }
-    } else if constexpr (B > 0) {
-        write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
+        for (int k = 0; k < kRowF4; ++k) v[k] = rows[threadIdx.x + kStepBlock * k];
+#pragma unroll
+        for (int k = 0; k < kRowF4; ++k) dst[threadIdx.x + kStepBlock * k] = v[k];
     } else {
-        write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
+#pragma unroll
+        for (int p = 0; p < B; ++p) {
+            const bool hit = p == head;
+#pragma unroll
+            for (int j = 0; j < A; ++j) ring[p][j] = hit ? act[j] : ring[p][j];
+        }
+        if (done) {
+            if (a.tobs) {
+                if constexpr (B > 0) write_row<A, B>(a.tobs + size_t(e) * D, o12, ring, head1);
+                else write_row_generic<A>(a.tobs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
+            }
+            hover_reset_state(a, C, e, b, sc, ep);
+            hover_obs12(C, b, o12);
+        }
+        RACE_MARK(t4);
+        if constexpr (B > 0) write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
+        else write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
     }
     RACE_MARK(t5);
     store_body(a, e, b, lag, DRAG, DYN);

@@ -834,7 +834,7 @@ template <typename Real>
 __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
                                              V3<Real> pos, Q4<Real> q, V3<Real> vel, V3<Real> w, int gate,
                                              float* row, bool write, Real* row0, uint32_t gin, uint32_t oin) {
-    const V3<Real> rpy = euler_xyz(q);
+    const V3<Real> rpy = euler_xyz_fast(q);
     const Real k12[12] = {pos.x, pos.y, pos.z, rpy.x, rpy.y, rpy.z, vel.x, vel.y, vel.z, w.x, w.y, w.z};
     if (write)
 #pragma unroll
@@ -926,7 +926,7 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
     // initial obs at the nominal (loadURDF) poses, at rest
     const Real d2r = Real(0.017453292519943295);
     const V3<Real> npos = v3(C.init_pos[dn][0], C.init_pos[dn][1], C.init_pos[dn][2]);
-    const Q4<Real> nq = quat_from_euler(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
+    const Q4<Real> nq = quat_from_euler_fast(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
     Real row0[15];
     const V3<Real> zero = v3(Real(0), Real(0), Real(0));
     uint32_t gin, oin;
@@ -936,14 +936,14 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
         int idx = 0;
         for (int k = 0; k < C.N; ++k) {
             if (k == dn) continue;
-            const V3<Real> orpy = euler_xyz(quat_from_euler(C.init_rpy[k][0] * d2r, C.init_rpy[k][1] * d2r, C.init_rpy[k][2] * d2r));
+            const V3<Real> orpy = euler_xyz_fast(quat_from_euler_fast(C.init_rpy[k][0] * d2r, C.init_rpy[k][1] * d2r, C.init_rpy[k][2] * d2r));
             float* p = obs_row + 49 + 6 * idx;
             p[0] = float(C.init_pos[k][0]); p[1] = float(C.init_pos[k][1]); p[2] = float(C.init_pos[k][2]);
             p[3] = float(orpy.x); p[4] = float(orpy.y); p[5] = float(orpy.z);
             ++idx;
         }
     }
-    const V3<Real> nrpy = euler_xyz(nq);
+    const V3<Real> nrpy = euler_xyz_fast(nq);
     // RewardWrapper.reset: current_target = obs[0, 12:15], previous_pos = obs[0, :3]
     for (int k = 0; k < 3; ++k) {   // per-env state, kept in drone 0's slot
         st(f, RF_WR_TARGET + k, EN, slot, dn == 0 && C.num_gates > 0 ? row0[3 + k] : Real(0));
@@ -987,7 +987,7 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
         }
     }
     d.pos = v3(npos.x + po[0], npos.y + po[1], npos.z + po[2]);
-    d.q = quat_from_euler(C.init_rpy[dn][0] + ro[0], C.init_rpy[dn][1] + ro[1], C.init_rpy[dn][2] + ro[2]);
+    d.q = quat_from_euler_fast(C.init_rpy[dn][0] + ro[0], C.init_rpy[dn][1] + ro[1], C.init_rpy[dn][2] + ro[2]);
     d.vel = v3(C.init_vel[dn][0], C.init_vel[dn][1], C.init_vel[dn][2]);
     d.w = v3(C.init_pqr[dn][0], C.init_pqr[dn][1], C.init_pqr[dn][2]);
     d.angv = d.w;
@@ -1202,7 +1202,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             if (k < N && k != dn) {
-                const V3<Real> orpy = euler_xyz(gq[k]);
+                const V3<Real> orpy = euler_xyz_fast(gq[k]);
                 float* p = row + 49 + 6 * idx;
                 p[0] = float(gpos[k].x); p[1] = float(gpos[k].y); p[2] = float(gpos[k].z);
                 p[3] = float(orpy.x); p[4] = float(orpy.y); p[5] = float(orpy.z);
