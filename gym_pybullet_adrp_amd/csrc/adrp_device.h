@@ -15,10 +15,12 @@ namespace adrp {
 #ifdef ADRP_RACE_TIMING
 __device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-phase max, 9/18/19 GJK
 #define RACE_MARK(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define RACE_SET(var) var = __builtin_amdgcn_s_memtime()
 #define RACE_ACC(i, dt) do { atomicAdd(&g_race_phase[i], (unsigned long long)(dt)); \
         atomicMax(&g_race_phase[10 + (i)], (unsigned long long)(dt)); } while (0)
 #else
 #define RACE_MARK(var)
+#define RACE_SET(var)
 #define RACE_ACC(i, dt)
 #endif
 

@@ -535,6 +535,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     RACE_MARK(t3);
 #ifdef ADRP_RACE_TIMING
     const unsigned long long dmask = __ballot(done);
+    uint64_t t4 = 0;
 #endif
     if constexpr (STG) {
         // The obs row is assembled in LDS (18 float4 per lane, no padding: the copy-out
@@ -581,7 +582,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
             my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
             my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
         }
-        RACE_MARK(t4);
+        RACE_SET(t4);
         __syncthreads();
         float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
         float4 v[kRowF4];
@@ -604,7 +605,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
             hover_reset_state(a, C, e, b, sc, ep);
             hover_obs12(C, b, o12);
         }
-        RACE_MARK(t4);
+        RACE_SET(t4);
         if constexpr (B > 0) write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
         else write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
     }
