@@ -136,6 +136,11 @@ static HoverConst<Real> hover_const(const adrp_config& c) {
     a.dyn_arm = Real(d.l / sqrt(2.0));
     a.coll_hh = Real(0.5 * d.collision_h); a.coll_r = Real(d.collision_r); a.coll_zoff = Real(d.collision_z_offset);
     for (int k = 0; k < 3; ++k) a.target[k] = Real(c.target_pos[k]);
+    a.pid_grav = Real(c.gravity * d.m);
+    a.pid_inv4kf = Real(1.0 / (4 * d.kf));
+    a.ctrl_dt = Real(1.0 / c.ctrl_freq);
+    a.ctrl_hz = Real(c.ctrl_freq);
+    a.speed_limit = float(0.03 * d.max_speed_kmh * (1000.0 / 3600));   // BaseRLAviary.py:95
     return a;
 }
 
@@ -263,7 +268,13 @@ extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
                  race_group(cfg->num_drones));
         return buf;
     }
-    const int A = cfg->act_type == ADRP_ACT_ONE_D_RPM ? 1 : 4;
+    const int A = hover_act_dim(cfg->act_type);
+    if (hover_has_pid(cfg->act_type)) {
+        static const char* ctl[] = {"", "", "", "PID", "VEL", "ONE_D_PID"};
+        snprintf(buf, sizeof buf, "hover_step<%s,%s,A%d,Bn,generic,%s>", cfg->precision ? "f64" : "f32", ph[p], A,
+                 ctl[cfg->act_type]);
+        return buf;
+    }
     snprintf(buf, sizeof buf, "hover_step<%s,%s,A%d,B%s,%s>", cfg->precision ? "f64" : "f32", ph[p], A,
              cfg->action_buffer_size == 15 ? "15" : "n", config_is_cf2x(*cfg) ? "cf2x" : "generic");
     return buf;
@@ -284,8 +295,8 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     if (c.precision != 0 && c.precision != 1) return seterr(nullptr, ADRP_ERR_INVALID, "precision must be 0 or 1");
     if (c.task == ADRP_TASK_HOVER) {
         if (c.num_drones != 1) return seterr(nullptr, ADRP_ERR_INVALID, "HoverAviary has exactly one drone");
-        if (c.act_type != ADRP_ACT_RPM && c.act_type != ADRP_ACT_ONE_D_RPM)
-            return seterr(nullptr, ADRP_ERR_INVALID, "HoverAviary act_type must be RPM or ONE_D_RPM");
+        if (c.act_type != ADRP_ACT_RPM && c.act_type != ADRP_ACT_ONE_D_RPM && !hover_has_pid(c.act_type))
+            return seterr(nullptr, ADRP_ERR_INVALID, "HoverAviary act_type must be RPM, ONE_D_RPM, PID, VEL or ONE_D_PID");
         if (c.action_buffer_size <= 0 || c.action_buffer_size > 4096)
             return seterr(nullptr, ADRP_ERR_INVALID, "action_buffer_size");
     } else if (c.task == ADRP_TASK_RACE) {
@@ -310,11 +321,11 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     h->device = device;
     h->E = c.num_envs; h->N = c.num_drones;
     const bool race = c.task == ADRP_TASK_RACE;
-    h->A = c.act_type == ADRP_ACT_ONE_D_RPM ? 1 : 4;
+    h->A = race ? 4 : hover_act_dim(c.act_type);
     h->B = race ? 0 : c.action_buffer_size;
     h->D = race ? 49 + (c.race_mode == ADRP_RACE_COMPETE ? 6 * (c.num_drones - 1) : 0) : 12 + h->B * h->A;
     h->S = c.pyb_freq / c.ctrl_freq;
-    h->nf_base = race ? RF_N : HF_NBASE;
+    h->nf_base = race ? RF_N : HF_NBASE + (hover_has_pid(c.act_type) ? HF_NPID : 0);
     h->ni = race ? RI_N : HI_N;
     h->real_size = c.precision ? 8 : 4;
     const size_t EN = size_t(h->E) * h->N;
@@ -416,6 +427,9 @@ static const char* k_hover_f[HF_NBASE] = {
     "omega_x", "omega_y", "omega_z", "last_rpm_0", "last_rpm_1", "last_rpm_2", "last_rpm_3",
     "angv_x", "angv_y", "angv_z", "link_quat_x", "link_quat_y", "link_quat_z", "link_quat_w"};
 static const char* k_hover_i[HI_N] = {"step_counter", "episode", "ring_head"};
+static const char* k_hover_pid[HF_NPID] = {"pid_last_rpy_x", "pid_last_rpy_y", "pid_last_rpy_z",
+                                           "pid_int_pos_x", "pid_int_pos_y", "pid_int_pos_z",
+                                           "pid_int_rpy_x", "pid_int_rpy_y", "pid_int_rpy_z"};
 
 extern "C" int adrp_state_layout(const adrp_t* h, int* nf, int* ni) {
     if (!h || !nf || !ni) return ADRP_ERR_INVALID;
@@ -453,7 +467,8 @@ extern "C" const char* adrp_state_field(const adrp_t* h, int is_int, int index) 
         return buf;
     }
     if (is_int) return index < h->ni ? k_hover_i[index] : nullptr;
-    if (index < h->nf_base) return k_hover_f[index];
+    if (index < HF_NBASE) return k_hover_f[index];
+    if (index < h->nf_base) return k_hover_pid[index - HF_NBASE];
     const int k = index - h->nf_base;
     if (k >= h->B * h->A) return nullptr;
     snprintf(buf, sizeof buf, "ring_%d_%d", k / h->A, k % h->A);
@@ -508,7 +523,7 @@ extern "C" int64_t adrp_step_bytes(const adrp_t* h) {
     const bool dyn = ph == ADRP_PHYS_DYN;
     const bool drag = ph == ADRP_PHYS_PYB_DRAG || ph == ADRP_PHYS_PYB_GND_DRAG_DW;
     const bool lag = h->cfg.link_frame_lag && !dyn;
-    const int64_t fields = 13 + (lag ? 4 : 0) + (drag ? 4 : 0) + (dyn ? 3 : 0);
+    const int64_t fields = 13 + (lag ? 4 : 0) + (drag ? 4 : 0) + (dyn ? 3 : 0) + (h->nf_base - HF_NBASE);
     const int64_t per_env = 2 * fields * int64_t(h->real_size)   // state read + write
                             + 2 * HI_N * 4                        // int state read + write
                             + int64_t(h->A) * 4                   // action

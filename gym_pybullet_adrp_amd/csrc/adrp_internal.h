@@ -52,6 +52,13 @@ constexpr int kBlock = kStepBlock;
 
 inline int race_group(int n) { return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : 8; }
 
+// HoverAviary action width (BaseRLAviary._actionSpace, BaseRLAviary.py:141-147) and whether the
+// action type runs the fused DSLPIDControl
+inline bool hover_has_pid(int t) { return t == ADRP_ACT_PID || t == ADRP_ACT_VEL || t == ADRP_ACT_ONE_D_PID; }
+inline int hover_act_dim(int t) {
+    return t == ADRP_ACT_PID ? 3 : (t == ADRP_ACT_ONE_D_RPM || t == ADRP_ACT_ONE_D_PID) ? 1 : 4;
+}
+
 template <typename Real>
 inline HoverArgs<Real> hover_args(const adrp_t* h) {
     const adrp_config& c = h->cfg;

@@ -33,7 +33,10 @@ namespace adrp {
 // float-field indices of the HoverAviary state snapshot ([field][E], SoA)
 enum HoverField {
     HF_POS = 0, HF_QUAT = 3, HF_VEL = 7, HF_OMEGA = 10, HF_LAST_RPM = 13, HF_ANGV = 17,
-    HF_LINK_QUAT = 20, HF_NBASE = 24
+    HF_LINK_QUAT = 20, HF_NBASE = 24,
+    // DSLPIDControl state (PID / VEL / ONE_D_PID handles only): last_rpy 3, integral_pos_e 3,
+    // integral_rpy_e 3 (control/DSLPIDControl.py:65-79)
+    HF_PID = 24, HF_NPID = 9
 };
 enum HoverInt { HI_STEP = 0, HI_EPISODE = 1, HI_RING_HEAD = 2, HI_N = 3 };
 
@@ -53,6 +56,10 @@ struct HoverConst {
     Real coll_hh, coll_r, coll_zoff;         // collision cylinder half-height, radius, z offset
     Real ang_max;                            // ANGULAR_MOTION_THRESHOLD / dt
     Real target[3];
+    // DSLPIDControl (PID / VEL / ONE_D_PID): GRAVITY = g*m (BaseControl.py:35, the env's own
+    // URDF), 1/(4 KF), CTRL_TIMESTEP and its inverse, SPEED_LIMIT as the float32 NumPy uses
+    Real pid_grav, pid_inv4kf, ctrl_dt, ctrl_hz;
+    float speed_limit;
 };
 
 // HoverAviary defaults: cf2x_IROS.urdf, PYB_FREQ 240, CTRL_FREQ 30, target (0,0,1), 8 s.
@@ -76,6 +83,9 @@ __host__ __device__ constexpr HoverConst<Real> cf2x_consts(int physics) {
     c.coll_hh = Real(0.0125); c.coll_r = Real(0.06); c.coll_zoff = Real(0);
     c.ang_max = Real(188.49555921538757);
     c.target[0] = Real(0); c.target[1] = Real(0); c.target[2] = Real(1);
+    c.pid_grav = Real(0.338492); c.pid_inv4kf = Real(791139240.5063292);
+    c.ctrl_dt = Real(0.03333333333333333); c.ctrl_hz = Real(30);
+    c.speed_limit = 0.25f;
     return c;
 }
 
@@ -365,6 +375,94 @@ __device__ __forceinline__ void write_row_generic(float* __restrict__ row, const
     }
 }
 
+// DSLPIDControl.computeControl (control/DSLPIDControl.py:82-259) for the HoverAviary PID / VEL /
+// ONE_D_PID action types (BaseRLAviary.py:193-235): once per env.step, on the state at the
+// start of the step.  ctl = last_rpy 3, integral_pos_e 3, integral_rpy_e 3 (in/out).  The
+// scipy Euler round trip of the target rotation (:205, :242-244) is the identity on a proper
+// rotation, so the target basis is used directly (oracle/oracle.c orc_dslpid, pinned by
+// tests/golden/pid_golden.npz).
+template <typename Real, int CTL>
+__device__ __forceinline__ void dslpid_rpm(const HoverConst<Real>& C, const Body<Real>& b, const float* act,
+                                           Real ctl[HF_NPID], Real rpm[4]) {
+    const M3<Real> R = rot(b.q);
+    const V3<Real> rpy = euler_xyz(b.q);   // accurate: the D term scales its error by 6e5
+    V3<Real> tp, tv = v3(Real(0), Real(0), Real(0));
+    Real tyaw = 0;
+    if constexpr (CTL == ADRP_ACT_PID) {
+        // _calculateNextStep(pos, action, step_size=1) (BaseAviary.py:1112-1160)
+        const V3<Real> d = v3(Real(act[0]) - b.pos.x, Real(act[1]) - b.pos.y, Real(act[2]) - b.pos.z);
+        const Real dist = sqrt_(dot(d, d));
+        tp = dist <= Real(1) ? v3(Real(act[0]), Real(act[1]), Real(act[2])) : b.pos + (Real(1) / dist) * d;
+    } else if constexpr (CTL == ADRP_ACT_VEL) {
+        // target_vel = SPEED_LIMIT*|a3|*a[0:3]/|a[0:3]| in float32 (float32 action, NEP 50)
+#pragma clang fp contract(off)
+        tp = b.pos;
+        tyaw = rpy.z;
+        // correctly rounded float32 sqrt / division through float64 (53 >= 2*24 + 2 bits)
+        const float n = float(sqrt(double(act[0] * act[0] + act[1] * act[1] + act[2] * act[2])));
+        const float s = C.speed_limit * fabsf(act[3]);
+        if (n != 0.0f) {
+            const double dn = double(n);
+            tv = v3(Real(s * float(double(act[0]) / dn)), Real(s * float(double(act[1]) / dn)),
+                    Real(s * float(double(act[2]) / dn)));
+        }
+    } else {   // ONE_D_PID: target_pos = pos + 0.1*[0, 0, a]
+        tp = v3(b.pos.x, b.pos.y, b.pos.z + Real(0.1) * Real(act[0]));
+    }
+    // _dslPIDPositionControl (:149-208)
+    constexpr Real PF[3] = {Real(.4), Real(.4), Real(1.25)}, IF[3] = {Real(.05), Real(.05), Real(.05)},
+                   DF[3] = {Real(.2), Real(.2), Real(.5)};
+    const Real pe[3] = {tp.x - b.pos.x, tp.y - b.pos.y, tp.z - b.pos.z};
+    const Real ve[3] = {tv.x - b.vel.x, tv.y - b.vel.y, tv.z - b.vel.z};
+    Real tt[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        Real ip = ctl[3 + k] + pe[k] * C.ctrl_dt;
+        ip = ip < Real(-2) ? Real(-2) : (ip > Real(2) ? Real(2) : ip);
+        if (k == 2) ip = ip < Real(-0.15) ? Real(-0.15) : (ip > Real(0.15) ? Real(0.15) : ip);
+        ctl[3 + k] = ip;
+        tt[k] = PF[k] * pe[k] + IF[k] * ip + DF[k] * ve[k];
+    }
+    tt[2] += C.pid_grav;
+    Real sc = tt[0] * R.a02 + tt[1] * R.a12 + tt[2] * R.a22;
+    sc = sc < Real(0) ? Real(0) : sc;
+    const Real thrust = (sqrt_(sc * C.pid_inv4kf) - Real(4070.3)) * Real(1.0 / 0.2685);
+    const V3<Real> ttv = v3(tt[0], tt[1], tt[2]);
+    const V3<Real> zax = rsqrt_(dot(ttv, ttv)) * ttv;
+    Real sy, cy;
+    sincos_(tyaw, &sy, &cy);
+    const V3<Real> yc = cross(zax, v3(cy, sy, Real(0)));
+    const V3<Real> yax = rsqrt_(dot(yc, yc)) * yc;
+    const V3<Real> xax = cross(yax, zax);
+    // _dslPIDAttitudeControl (:212-259): rot_e = vee(Rt^T R - R^T Rt)
+    const V3<Real> c0 = v3(R.a00, R.a10, R.a20), c1 = v3(R.a01, R.a11, R.a21), c2 = v3(R.a02, R.a12, R.a22);
+    const Real rot_e[3] = {dot(zax, c1) - dot(c2, yax), dot(xax, c2) - dot(c0, zax), dot(yax, c0) - dot(c1, xax)};
+    const Real cur[3] = {rpy.x, rpy.y, rpy.z};
+    constexpr Real PT[3] = {Real(70000), Real(70000), Real(60000)}, IT[3] = {Real(0), Real(0), Real(500)},
+                   DT[3] = {Real(20000), Real(20000), Real(12000)};
+    Real tq[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const Real rr_e = -(cur[k] - ctl[k]) * C.ctrl_hz;
+        ctl[k] = cur[k];
+        Real ir = ctl[6 + k] - rot_e[k] * C.ctrl_dt;
+        ir = ir < Real(-1500) ? Real(-1500) : (ir > Real(1500) ? Real(1500) : ir);
+        if (k < 2) ir = ir < Real(-1) ? Real(-1) : (ir > Real(1) ? Real(1) : ir);
+        ctl[6 + k] = ir;
+        const Real t = -PT[k] * rot_e[k] + DT[k] * rr_e + IT[k] * ir;
+        tq[k] = t < Real(-3200) ? Real(-3200) : (t > Real(3200) ? Real(3200) : t);
+    }
+    // CF2X mixer [[-.5,-.5,-1],[-.5,.5,1],[.5,.5,-1],[.5,-.5,1]], PWM clip, PWM -> RPM
+    const Real hr = Real(0.5) * tq[0], hp = Real(0.5) * tq[1];
+    const Real pwm[4] = {thrust - hr - hp - tq[2], thrust - hr + hp + tq[2], thrust + hr + hp - tq[2],
+                         thrust + hr - hp + tq[2]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const Real p = pwm[i] < Real(20000) ? Real(20000) : (pwm[i] > Real(65535) ? Real(65535) : pwm[i]);
+        rpm[i] = Real(0.2685) * p + Real(4070.3);
+    }
+}
+
 template <typename Real>
 __device__ __forceinline__ void load_body(const HoverArgs<Real>& a, int e, Body<Real>& b, bool lag, bool drag,
                                           bool dyn) {
@@ -428,8 +526,9 @@ __device__ __forceinline__ void stage_row(float4* lds_row, const float o12[12], 
 }
 
 // B == 0: runtime ring length a.B;  SC > 0: compile-time sub-step count (loop fully unrolled);
-// STG: LDS-staged obs rows (needs A == 4, B == 15 and every lane of the block live)
-template <typename Real, int PH, int A, int B, int SC, bool STG = false>
+// STG: LDS-staged obs rows (needs A == 4, B == 15 and every lane of the block live);
+// CTL: 0 (RPM / ONE_D_RPM actions) or ADRP_ACT_PID / _VEL / _ONE_D_PID (fused DSLPIDControl)
+template <typename Real, int PH, int A, int B, int SC, bool STG = false, int CTL = 0>
 __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const HoverConst<Real>& C) {
     constexpr int BR = B > 0 ? B : 1;
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
@@ -464,10 +563,21 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     const bool lag = C.link_lag && !DYN;
     Body<Real> b;
     load_body(a, e, b, lag, DRAG, DYN);
-    // ---- _preprocessAction: RPM = HOVER_RPM * (1 + 0.05 a), the gain in float32 (NEP 50) ----
+    // ---- _preprocessAction: RPM = HOVER_RPM * (1 + 0.05 a), the gain in float32 (NEP 50),
+    //      or the DSLPIDControl output for the PID action types ----
     Real rpm[4];
+    if constexpr (CTL != 0) {
+        static_assert(A == (CTL == ADRP_ACT_PID ? 3 : CTL == ADRP_ACT_VEL ? 4 : 1), "PID action width");
+        Real ctl[HF_NPID];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rpm[i] = C.hover_rpm * Real(rpm_gain(act[A == 1 ? 0 : i]));
+        for (int k = 0; k < HF_NPID; ++k) ctl[k] = a.f[(HF_PID + k) * E + e];
+        dslpid_rpm<Real, CTL>(C, b, act, ctl, rpm);
+#pragma unroll
+        for (int k = 0; k < HF_NPID; ++k) a.f[(HF_PID + k) * E + e] = ctl[k];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rpm[i] = C.hover_rpm * Real(rpm_gain(act[A == 1 ? 0 : i]));
+    }
     // ---- sub-step loop (BaseAviary.py:347-376) ----
     bool touched = false;
 #ifdef ADRP_RACE_TIMING
@@ -643,7 +753,7 @@ struct HoverTail {
 // DEF: compiled-in cf2x_consts (the reference default) instead of the device block.
 // STG: LDS-staged coalesced obs rows (host: only when E % kStepBlock == 0).
 // Launch with kStepBlock threads per workgroup.
-template <typename Real, int PH, int A, int B, bool DEF, bool STG = false>
+template <typename Real, int PH, int A, int B, bool DEF, bool STG = false, int CTL = 0>
 __global__ void __launch_bounds__(256) hover_step_kernel(Real* f, float* ring, int32_t* ist, const float* act,
                                                          float* obs, float* rew, int E, HoverTail<Real> t) {
     HoverArgs<Real> a;
@@ -654,9 +764,9 @@ __global__ void __launch_bounds__(256) hover_step_kernel(Real* f, float* ring, i
     a.E = E; a.B = t.B; a.D = t.D; a.autoreset = t.autoreset;
     if constexpr (DEF) {
         constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
-        hover_step_body<Real, PH, A, B, C.S, STG>(a, C);
+        hover_step_body<Real, PH, A, B, C.S, STG, CTL>(a, C);
     } else {
-        hover_step_body<Real, PH, A, B, 0, STG>(a, *a.c);
+        hover_step_body<Real, PH, A, B, 0, STG, CTL>(a, *a.c);
     }
 }
 

@@ -19,6 +19,15 @@ from ..utils.enums import ActionType, DroneModel, ObservationType, Physics, PHYS
 from ..utils.spaces import Box
 
 
+# ActionType -> C-ABI code, and the per-drone action width (BaseRLAviary.py:141-147).  PID /
+# VEL / ONE_D_PID run DSLPIDControl (control/DSLPIDControl.py) fused into the step kernel; its
+# state persists across resets, as the reference builds the controllers once (:73-78).
+_ACT_CODE = {ActionType.RPM: abi.ACT_RPM, ActionType.ONE_D_RPM: abi.ACT_ONE_D_RPM, ActionType.PID: abi.ACT_PID,
+             ActionType.VEL: abi.ACT_VEL, ActionType.ONE_D_PID: abi.ACT_ONE_D_PID}
+_ACT_SIZE = {ActionType.RPM: 4, ActionType.VEL: 4, ActionType.PID: 3, ActionType.ONE_D_RPM: 1,
+             ActionType.ONE_D_PID: 1}
+
+
 class HoverAviary:
     """Batched counterpart of gym_pybullet_adrp.envs.HoverAviary."""
 
@@ -33,13 +42,13 @@ class HoverAviary:
             raise ValueError("GUI / video recording are out of scope (DESIGN.md)")
         if obs != ObservationType.KIN:
             raise ValueError("only ObservationType.KIN is supported")
-        if act not in (ActionType.RPM, ActionType.ONE_D_RPM):
-            raise ValueError("supported action types: RPM, ONE_D_RPM")
+        if act not in _ACT_CODE:
+            raise ValueError("supported action types: RPM, ONE_D_RPM, PID, VEL, ONE_D_PID")
         if pyb_freq % ctrl_freq != 0:
             raise ValueError("[ERROR] in BaseAviary.__init__(), pyb_freq is not divisible by env_freq.")
         cfg = _lib.default_config(abi.TASK_HOVER)
         cfg.physics = PHYSICS_CODE[physics]
-        cfg.act_type = abi.ACT_ONE_D_RPM if act == ActionType.ONE_D_RPM else abi.ACT_RPM
+        cfg.act_type = _ACT_CODE[act]
         cfg.num_envs = int(num_envs)
         cfg.pyb_freq, cfg.ctrl_freq = int(pyb_freq), int(ctrl_freq)
         cfg.action_buffer_size = int(ctrl_freq // 2)
@@ -75,6 +84,8 @@ class HoverAviary:
         self.GRAVITY = self.G * self.M
         self.HOVER_RPM = np.sqrt(self.GRAVITY / (4 * self.KF))
         self.MAX_RPM = np.sqrt((d.thrust2weight * self.GRAVITY) / (4 * self.KF))
+        if act == ActionType.VEL:
+            self.SPEED_LIMIT = 0.03 * d.max_speed_kmh * (1000 / 3600)   # BaseRLAviary.py:94-95
         self.num_envs = cfg.num_envs
         self.action_space = self._actionSpace()
         self.observation_space = self._observationSpace()
@@ -90,14 +101,14 @@ class HoverAviary:
 
     # ---- spaces (BaseRLAviary.py:132-156, 243-277) ----
     def _actionSpace(self):
-        size = 1 if self.ACT_TYPE == ActionType.ONE_D_RPM else 4
+        size = _ACT_SIZE[self.ACT_TYPE]
         return Box(low=-np.ones((1, size)), high=np.ones((1, size)), dtype=np.float32)
 
     def _observationSpace(self):
         lo, hi = -np.inf, np.inf
         low = [lo, lo, 0] + [lo] * 9
         high = [hi] * 12
-        size = 1 if self.ACT_TYPE == ActionType.ONE_D_RPM else 4
+        size = _ACT_SIZE[self.ACT_TYPE]
         low += [-1] * size * self.ACTION_BUFFER_SIZE
         high += [+1] * size * self.ACTION_BUFFER_SIZE
         return Box(low=np.array([low]), high=np.array([high]), dtype=np.float32)

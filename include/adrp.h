@@ -64,6 +64,10 @@ extern "C" {
 #define ADRP_ACT_RPM 0          /* HoverAviary: a in [-1,1]^4 -> HOVER_RPM*(1+0.05a) (BaseRLAviary.py:192) */
 #define ADRP_ACT_ONE_D_RPM 1    /* HoverAviary: a in [-1,1]   -> 4 x HOVER_RPM*(1+0.05a) (BaseRLAviary.py:225) */
 #define ADRP_ACT_FULLSTATE 2    /* MultiRace: [x,y,z,yaw] absolute FULLSTATE setpoint (MultiRaceAviary.py:190-194) */
+/* HoverAviary with the fused DSLPIDControl (control/DSLPIDControl.py:82-259), once per env.step */
+#define ADRP_ACT_PID 3          /* a in R^3: waypoint, capped 1 m away (BaseRLAviary.py:193-207, BaseAviary.py:1112-1160) */
+#define ADRP_ACT_VEL 4          /* a in R^4: direction + |a3| x SPEED_LIMIT target velocity (BaseRLAviary.py:208-223) */
+#define ADRP_ACT_ONE_D_PID 5    /* a in R:   target z = z + 0.1a (BaseRLAviary.py:226-235) */
 
 /* adrp_config.race_mode — utils/enums.py:84-87 (RaceMode) */
 #define ADRP_RACE_COMPARE 0
@@ -162,8 +166,8 @@ void adrp_destroy(adrp_t* h);
 /* Error text of the last failing call on h (h may be NULL for adrp_create failures). */
 const char* adrp_last_error(const adrp_t* h);
 
-/* Per-drone observation width D (72 Hover/RPM, 27 Hover/ONE_D_RPM, 49 / 49+6(N-1) Race)
- * and action width A (4 or 1). */
+/* Per-drone observation width D (12 + B*A for Hover: 72 RPM/VEL, 57 PID, 27 ONE_D_*;
+ * 49 / 49+6(N-1) Race) and action width A (4, 3 or 1). */
 int adrp_obs_dim(const adrp_t* h);
 int adrp_act_dim(const adrp_t* h);
 

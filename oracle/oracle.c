@@ -42,6 +42,7 @@ static v3 vcross(v3 a, v3 b) {
     return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 static double vnorm(v3 a) { return sqrt(vdot(a, a)); }
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
 typedef struct { double m[3][3]; } m33;
 /* btMatrix3x3::setRotation */
@@ -240,6 +241,7 @@ struct orc_handle {
     float* ring;            /* [E][buf][A] */
     uint8_t* contact;       /* [E] ground-model flag of the last step */
     int64_t contacts;
+    double* pid;            /* [E][9] DSLPIDControl state (PID / VEL / ONE_D_PID), else NULL */
     struct rdrone_s* rd;    /* [E*N] MultiRace per-drone state (race.c) */
     struct renv_s* re;      /* [E] MultiRace per-env state */
 };
@@ -257,6 +259,14 @@ static void race_set_row(orc_t* o, size_t slot, int e, int first, const double* 
 #define RACE_NI 9
 static const char* k_race_i[RACE_NI] = {"step_counter", "episode", "tick", "last_att_tick", "last_pos_tick",
                                          "tumble", "gate", "flags", "wr_gate"};
+
+/* BaseRLAviary._actionSpace (BaseRLAviary.py:141-147) */
+static int hover_act_dim(int act_type) {
+    return act_type == ADRP_ACT_PID ? 3 : (act_type == ADRP_ACT_ONE_D_RPM || act_type == ADRP_ACT_ONE_D_PID) ? 1 : 4;
+}
+static int hover_has_pid(int act_type) {
+    return act_type == ADRP_ACT_PID || act_type == ADRP_ACT_VEL || act_type == ADRP_ACT_ONE_D_PID;
+}
 
 int orc_obs_dim(const orc_t* o) { return o->D; }
 int orc_act_dim(const orc_t* o) { return o->A; }
@@ -294,13 +304,14 @@ int orc_create(const adrp_config* cfg, orc_t** out) {
     if (cfg->num_envs <= 0 || cfg->num_drones != 1) return fail("hover: num_envs > 0, num_drones == 1");
     if (cfg->ctrl_freq <= 0 || cfg->pyb_freq % cfg->ctrl_freq != 0)
         return fail("pyb_freq is not divisible by env_freq");
-    if (cfg->act_type != ADRP_ACT_RPM && cfg->act_type != ADRP_ACT_ONE_D_RPM) return fail("hover act_type");
+    if (cfg->act_type != ADRP_ACT_RPM && cfg->act_type != ADRP_ACT_ONE_D_RPM && cfg->act_type != ADRP_ACT_PID &&
+        cfg->act_type != ADRP_ACT_VEL && cfg->act_type != ADRP_ACT_ONE_D_PID) return fail("hover act_type");
     if (cfg->physics < 0 || cfg->physics > ADRP_PHYS_PYB_GND_DRAG_DW) return fail("physics");
     if (cfg->action_buffer_size <= 0) return fail("action_buffer_size");
     orc_t* o = (orc_t*)calloc(1, sizeof *o);
     o->cfg = *cfg;
     o->E = cfg->num_envs; o->N = cfg->num_drones;
-    o->A = cfg->act_type == ADRP_ACT_ONE_D_RPM ? 1 : 4;
+    o->A = hover_act_dim(cfg->act_type);
     o->D = 12 + cfg->action_buffer_size * o->A;
     o->S = cfg->pyb_freq / cfg->ctrl_freq;
     o->dt = 1.0 / cfg->pyb_freq;
@@ -313,6 +324,7 @@ int orc_create(const adrp_config* cfg, orc_t** out) {
     o->ring_head = (int32_t*)calloc(o->E, 4);
     o->ring = (float*)calloc((size_t)o->E * cfg->action_buffer_size * o->A, 4);
     o->contact = (uint8_t*)calloc(o->E, 1);
+    if (hover_has_pid(cfg->act_type)) o->pid = (double*)calloc((size_t)o->E * 9, sizeof(double));
     *out = o;
     return ADRP_OK;
 }
@@ -320,7 +332,7 @@ int orc_create(const adrp_config* cfg, orc_t** out) {
 void orc_destroy(orc_t* o) {
     if (!o) return;
     free(o->b); free(o->step_counter); free(o->episode); free(o->ring_head); free(o->ring);
-    free(o->contact); free(o->rd); free(o->re); free(o);
+    free(o->contact); free(o->pid); free(o->rd); free(o->re); free(o);
 }
 
 /* ---- per-link external force accumulators (what p.applyExternalForce/Torque build) ---- */
@@ -468,12 +480,114 @@ void orc_hover_rpm(const adrp_config* cfg, const float* act, double rpm[4]) {
     }
 }
 
+/* ---- DSLPIDControl.computeControl (control/DSLPIDControl.py:82-259), float64 ----------
+   in  = pos 3, quat 4 (x,y,z,w), vel 3, target_pos 3, target_rpy 3, target_vel 3
+   st  = last_rpy 3, integral_pos_e 3, integral_rpy_e 3 (in/out; DSLPIDControl.reset zeroes them)
+   The controller reads the drone's own URDF (DroneModel.CF2X = cf2x_IROS.urdf,
+   BaseControl.py:35-37 / 185-224): GRAVITY = g*m, KF.  target_rpy_rates = 0 (never passed by
+   BaseRLAviary).  The scipy Euler round trip of the target rotation (:205, :242-244:
+   from_matrix -> as_euler('XYZ') -> from_euler -> as_quat -> from_quat -> as_matrix) is the
+   identity on a proper rotation, so the target matrix is used directly (pinned by
+   tests/golden/pid_golden.npz to rounding). */
+#define DSL_PWM2RPM_SCALE 0.2685
+#define DSL_PWM2RPM_CONST 4070.3
+void orc_dslpid(const adrp_config* cfg, double dt, const double in[19], double st[9], double rpm[4]) {
+    static const double P_FOR[3] = {.4, .4, 1.25}, I_FOR[3] = {.05, .05, .05}, D_FOR[3] = {.2, .2, .5};
+    static const double P_TOR[3] = {70000., 70000., 60000.}, I_TOR[3] = {.0, .0, 500.},
+                        D_TOR[3] = {20000., 20000., 12000.};
+    static const double MIX[4][3] = {{-.5, -.5, -1}, {-.5, .5, 1}, {.5, .5, -1}, {.5, -.5, 1}};  /* CF2X */
+    const double grav = cfg->gravity * cfg->drone.m, kf = cfg->drone.kf;
+    qt q = {in[3], in[4], in[5], in[6]};
+    m33 R = mat_from_quat(q);                                   /* p.getMatrixFromQuaternion */
+    /* _dslPIDPositionControl (:149-208) */
+    double pos_e[3], vel_e[3], tt[3];
+    for (int k = 0; k < 3; ++k) {
+        pos_e[k] = in[10 + k] - in[k];
+        vel_e[k] = in[16 + k] - in[7 + k];
+        double ip = st[3 + k] + pos_e[k] * dt;
+        ip = clampd(ip, -2., 2.);
+        if (k == 2) ip = clampd(ip, -0.15, .15);
+        st[3 + k] = ip;
+    }
+    for (int k = 0; k < 3; ++k) tt[k] = P_FOR[k] * pos_e[k] + I_FOR[k] * st[3 + k] + D_FOR[k] * vel_e[k];
+    tt[2] += grav;
+    double scalar = tt[0] * R.m[0][2] + tt[1] * R.m[1][2] + tt[2] * R.m[2][2];
+    if (scalar < 0.) scalar = 0.;
+    const double thrust = (sqrt(scalar / (4 * kf)) - DSL_PWM2RPM_CONST) / DSL_PWM2RPM_SCALE;
+    v3 ttv = V(tt[0], tt[1], tt[2]);
+    v3 zax = vscale(ttv, 1.0 / vnorm(ttv));
+    v3 xc = V(cos(in[15]), sin(in[15]), 0);
+    v3 yc = vcross(zax, xc);
+    v3 yax = vscale(yc, 1.0 / vnorm(yc));
+    v3 xax = vcross(yax, zax);
+    m33 Rt;   /* columns x, y, z */
+    Rt.m[0][0] = xax.x; Rt.m[0][1] = yax.x; Rt.m[0][2] = zax.x;
+    Rt.m[1][0] = xax.y; Rt.m[1][1] = yax.y; Rt.m[1][2] = zax.y;
+    Rt.m[2][0] = xax.z; Rt.m[2][1] = yax.z; Rt.m[2][2] = zax.z;
+    /* _dslPIDAttitudeControl (:212-259) */
+    double qq[4] = {q.x, q.y, q.z, q.w}, rpy[3];
+    orc_euler_from_quat(qq, rpy);
+    double Me[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double a = 0, b = 0;
+            for (int k = 0; k < 3; ++k) { a += Rt.m[k][i] * R.m[k][j]; b += R.m[k][i] * Rt.m[k][j]; }
+            Me[i][j] = a - b;
+        }
+    const double rot_e[3] = {Me[2][1], Me[0][2], Me[1][0]};
+    double tq[3];
+    for (int k = 0; k < 3; ++k) {
+        const double rr_e = 0.0 - (rpy[k] - st[k]) / dt;
+        st[k] = rpy[k];
+        double ir = st[6 + k] - rot_e[k] * dt;
+        ir = clampd(ir, -1500., 1500.);
+        if (k < 2) ir = clampd(ir, -1., 1.);
+        st[6 + k] = ir;
+        tq[k] = clampd(-P_TOR[k] * rot_e[k] + D_TOR[k] * rr_e + I_TOR[k] * ir, -3200, 3200);
+    }
+    for (int i = 0; i < 4; ++i) {
+        double pwm = thrust + MIX[i][0] * tq[0] + MIX[i][1] * tq[1] + MIX[i][2] * tq[2];
+        pwm = clampd(pwm, 20000., 65535.);
+        rpm[i] = DSL_PWM2RPM_SCALE * pwm + DSL_PWM2RPM_CONST;
+    }
+}
+
+/* BaseRLAviary._preprocessAction PID / VEL / ONE_D_PID branches (BaseRLAviary.py:193-235):
+   the controller's inputs from the drone state at the start of the env.step */
+static void pid_inputs(const adrp_config* cfg, const float* act, const double pos[3], const double quat[4],
+                       const double vel[3], double in[19]) {
+    memset(in, 0, 19 * sizeof(double));
+    memcpy(in, pos, 3 * sizeof(double));
+    memcpy(in + 3, quat, 4 * sizeof(double));
+    memcpy(in + 7, vel, 3 * sizeof(double));
+    if (cfg->act_type == ADRP_ACT_PID) {
+        /* _calculateNextStep(pos, destination=action, step_size=1) (BaseAviary.py:1112-1160) */
+        double d[3], dist = 0;
+        for (int k = 0; k < 3; ++k) { d[k] = (double)act[k] - pos[k]; dist += d[k] * d[k]; }
+        dist = sqrt(dist);
+        for (int k = 0; k < 3; ++k) in[10 + k] = dist <= 1.0 ? (double)act[k] : pos[k] + d[k] / dist * 1.0;
+    } else if (cfg->act_type == ADRP_ACT_VEL) {
+        /* target_pos = pos, target_rpy = (0, 0, yaw), target_vel = SPEED_LIMIT*|a3|*unit(a[0:3]),
+           in float32 (float32 action, NEP 50 weak Python scalars) */
+        memcpy(in + 10, pos, 3 * sizeof(double));
+        double rpy[3];
+        orc_euler_from_quat(quat, rpy);
+        in[15] = rpy[2];
+        const float n = sqrtf(act[0] * act[0] + act[1] * act[1] + act[2] * act[2]);
+        const float lim = (float)(0.03 * cfg->drone.max_speed_kmh * (1000.0 / 3600));   /* BaseRLAviary.py:95 */
+        const float s = lim * fabsf(act[3]);
+        for (int k = 0; k < 3; ++k) in[16 + k] = n != 0.0f ? (double)(s * (act[k] / n)) : 0.0;
+    } else {   /* ONE_D_PID: target_pos = pos + 0.1*[0, 0, a] */
+        in[10] = pos[0] + 0.1 * 0.0;
+        in[11] = pos[1] + 0.1 * 0.0;
+        in[12] = pos[2] + 0.1 * (double)act[0];
+    }
+}
+
 /* ---- Bullet 3.x btMultiBody floating-base step, restated ---------------------------- */
 #define BT_DAMPING 0.04          /* btMultiBody m_linearDamping / m_angularDamping defaults */
 #define BT_MAX_COORD_VEL 100.0   /* btMultiBody m_maxCoordinateVelocity */
 #define BT_ANGULAR_MOTION_THRESHOLD (0.5 * (PI / 2))
-
-static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
 /* returns 1 if the documented ground model acted */
 static int bullet_step(const orc_t* o, body_t* b, const forces_t* F, double mass, v3 inertia) {
@@ -667,7 +781,17 @@ static void hover_step_env(orc_t* o, int e, const float* act, float* obs_row, fl
     for (int j = 0; j < A; ++j) ring[o->ring_head[e] * A + j] = act[j];
     o->ring_head[e] = (o->ring_head[e] + 1) % B;
     double rpm[4];
-    orc_hover_rpm(c, act, rpm);
+    if (o->pid) {
+        /* DSLPIDControl on the state at the start of the step (_getDroneStateVector) */
+        qt q = qconj(b->q_wtb);
+        const double pos[3] = {b->pos.x, b->pos.y, b->pos.z}, quat[4] = {q.x, q.y, q.z, q.w},
+                     vel[3] = {b->vel.x, b->vel.y, b->vel.z};
+        double in[19];
+        pid_inputs(c, act, pos, quat, vel, in);
+        orc_dslpid(c, 1.0 / c->ctrl_freq, in, o->pid + (size_t)e * 9, rpm);
+    } else {
+        orc_hover_rpm(c, act, rpm);
+    }
     uint8_t touched = 0;
     for (int s = 0; s < o->S; ++s) {
         if (c->physics == ADRP_PHYS_DYN) {
@@ -724,10 +848,15 @@ static const char* k_hover_f[] = {"pos_x", "pos_y", "pos_z", "quat_x", "quat_y",
                                   "link_quat_x", "link_quat_y", "link_quat_z", "link_quat_w"};
 static const char* k_hover_i[] = {"step_counter", "episode", "ring_head"};
 #define HOVER_NF_BASE 24
+/* DSLPIDControl state fields (PID / VEL / ONE_D_PID only), between the body and the ring */
+static const char* k_hover_pid[9] = {"pid_last_rpy_x", "pid_last_rpy_y", "pid_last_rpy_z",
+                                     "pid_int_pos_x", "pid_int_pos_y", "pid_int_pos_z",
+                                     "pid_int_rpy_x", "pid_int_rpy_y", "pid_int_rpy_z"};
+#define HOVER_NF_CTL(o) (HOVER_NF_BASE + ((o)->pid ? 9 : 0))
 
 int orc_state_layout(const orc_t* o, int* nf, int* ni) {
     if (o->cfg.task == ADRP_TASK_RACE) { *nf = RACE_NF; *ni = RACE_NI; return ADRP_OK; }
-    *nf = HOVER_NF_BASE + o->cfg.action_buffer_size * o->A;
+    *nf = HOVER_NF_CTL(o) + o->cfg.action_buffer_size * o->A;
     *ni = 3;
     return ADRP_OK;
 }
@@ -740,7 +869,8 @@ const char* orc_state_field(const orc_t* o, int is_int, int index) {
     if (is_int) return (index >= 0 && index < 3) ? k_hover_i[index] : NULL;
     if (index < 0) return NULL;
     if (index < HOVER_NF_BASE) return k_hover_f[index];
-    int k = index - HOVER_NF_BASE;
+    if (index < HOVER_NF_CTL(o)) return k_hover_pid[index - HOVER_NF_BASE];
+    int k = index - HOVER_NF_CTL(o);
     if (k >= o->cfg.action_buffer_size * o->A) return NULL;
     snprintf(buf, sizeof buf, "ring_%d_%d", k / o->A, k % o->A);
     return buf;
@@ -770,7 +900,9 @@ int orc_get_state(const orc_t* o, double* f, int32_t* ii) {
                                    w.x, w.y, w.z, b->last_rpm[0], b->last_rpm[1], b->last_rpm[2], b->last_rpm[3],
                                    b->ang_v.x, b->ang_v.y, b->ang_v.z, lq.x, lq.y, lq.z, lq.w};
         for (int k = 0; k < HOVER_NF_BASE; ++k) f[(size_t)k * E + e] = v[k];
-        for (int k = 0; k < B * A; ++k) f[(size_t)(HOVER_NF_BASE + k) * E + e] = o->ring[(size_t)e * B * A + k];
+        if (o->pid)
+            for (int k = 0; k < 9; ++k) f[(size_t)(HOVER_NF_BASE + k) * E + e] = o->pid[(size_t)e * 9 + k];
+        for (int k = 0; k < B * A; ++k) f[(size_t)(HOVER_NF_CTL(o) + k) * E + e] = o->ring[(size_t)e * B * A + k];
         ii[e] = o->step_counter[e];
         ii[E + e] = o->episode[e];
         ii[2 * E + e] = o->ring_head[e];
@@ -810,7 +942,9 @@ int orc_set_state(orc_t* o, const double* f, const int32_t* ii) {
         qt lq = {F_(20), F_(21), F_(22), F_(23)};
         b->link_q_wtb = qconj(lq);
         b->link_pos = b->pos;
-        for (int k = 0; k < B * A; ++k) o->ring[(size_t)e * B * A + k] = (float)F_(HOVER_NF_BASE + k);
+        if (o->pid)
+            for (int k = 0; k < 9; ++k) o->pid[(size_t)e * 9 + k] = F_(HOVER_NF_BASE + k);
+        for (int k = 0; k < B * A; ++k) o->ring[(size_t)e * B * A + k] = (float)F_(HOVER_NF_CTL(o) + k);
 #undef F_
         o->step_counter[e] = ii[e];
         o->episode[e] = ii[E + e];

@@ -59,6 +59,10 @@ void orc_derived_constants(const adrp_config* cfg, double out[6]);
 int orc_force_assembly(const adrp_config* cfg, int N, const double* states, int n, const double rpm[4],
                        const double prev_rpm[4], double link_force[5][3], double link_torque[5][3]);
 void orc_hover_rpm(const adrp_config* cfg, const float* act, double rpm[4]);
+/* DSLPIDControl.computeControl (control/DSLPIDControl.py:82-259): in = pos 3, quat 4, vel 3,
+ * target_pos 3, target_rpy 3, target_vel 3; st = last_rpy 3, integral_pos_e 3,
+ * integral_rpy_e 3 (in/out) */
+void orc_dslpid(const adrp_config* cfg, double dt, const double in[19], double st[9], double rpm[4]);
 /* HoverAviary obs / reward / terminated / truncated at the current state (no physics,
  * step_counter unchanged): _computeObs/_computeReward/_computeTerminated/_computeTruncated */
 int orc_hover_eval(const orc_t* o, float* obs, float* rew, uint8_t* term, uint8_t* trunc);

@@ -51,6 +51,7 @@ def _load():
     lib.orc_derived_constants.argtypes = [P, P]
     lib.orc_force_assembly.argtypes = [P, I, P, I, P, P, P, P]
     lib.orc_hover_rpm.argtypes = [P, P, P]
+    lib.orc_dslpid.argtypes = [P, D, P, P, P]
     lib.orc_hover_eval.argtypes = [P, P, P, P, P]
     lib.orc_config_size.restype = ctypes.c_uint32
     lib.orc_compute_pwms.argtypes = [P, P]
@@ -173,6 +174,16 @@ def force_assembly(cfg, states, n, rpm, prev):
 def hover_rpm(cfg, act):
     a = np.ascontiguousarray(act, np.float32); o = np.zeros(4)
     lib().orc_hover_rpm(ctypes.byref(cfg), _ptr(a), _ptr(o))
+    return o
+
+
+def dslpid(cfg, dt, inp, st):
+    """DSLPIDControl.computeControl: inp = pos3 quat4 vel3 target_pos3 target_rpy3 target_vel3;
+    st (9, float64) = last_rpy, integral_pos_e, integral_rpy_e, updated in place."""
+    i = np.ascontiguousarray(inp, float)
+    assert i.shape == (19,) and st.dtype == np.float64 and st.shape == (9,) and st.flags.c_contiguous
+    o = np.zeros(4)
+    lib().orc_dslpid(ctypes.byref(cfg), dt, _ptr(i), _ptr(st), _ptr(o))
     return o
 
 

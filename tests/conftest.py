@@ -16,3 +16,9 @@ def pytest_configure(config):
 def golden():
     import numpy as np
     return np.load(os.path.join(ROOT, "tests", "golden", "hover_golden.npz"))
+
+
+@pytest.fixture(scope="session")
+def pid_golden():
+    import numpy as np
+    return np.load(os.path.join(ROOT, "tests", "golden", "pid_golden.npz"))

@@ -657,10 +657,86 @@ def race_fixtures(pb, m):
     return out
 
 
+def pid_fixtures(pb, m):
+    """DSLPIDControl (control/DSLPIDControl.py:82-259) and the HoverAviary PID / VEL /
+    ONE_D_PID action types (BaseRLAviary.py:193-235), fully reference code."""
+    E = m.enums
+    DSL = importlib.import_module("gym_pybullet_adrp.control.DSLPIDControl").DSLPIDControl
+    rng = np.random.default_rng(13)
+    out = {}
+    # (1) computeControl sequences from a fresh controller: inputs, RPM, controller state
+    n_seq, T = 48, 12
+    dt = 1 / 30
+    cin = np.zeros((n_seq, T, 19))    # pos 3, quat 4, vel 3, target_pos 3, target_rpy 3, target_vel 3
+    crpm = np.zeros((n_seq, T, 4)); cst = np.zeros((n_seq, T, 9))
+    for s in range(n_seq):
+        ctrl = DSL(drone_model=E.DroneModel.CF2X)
+        big = s % 4 == 0                                   # saturate integrators / torques / PWM
+        for t in range(T):
+            pos, quat, vel, _ = random_state(rng, center=(0, 0, 1), tilt=0.6 if big else 0.2)
+            tp = pos + rng.uniform(-3, 3, 3) * (4.0 if big else 0.3)
+            trpy = np.array([0.0, 0.0, rng.uniform(-math.pi, math.pi) if s % 3 == 0 else 0.0])
+            tv = rng.uniform(-1, 1, 3) * (s % 2)
+            rpm, _, _ = ctrl.computeControl(control_timestep=dt, cur_pos=pos, cur_quat=quat, cur_vel=vel,
+                                            cur_ang_vel=np.zeros(3), target_pos=tp, target_rpy=trpy,
+                                            target_vel=tv)
+            cin[s, t] = np.concatenate([pos, quat, vel, tp, trpy, tv])
+            crpm[s, t] = rpm
+            cst[s, t] = np.concatenate([ctrl.last_rpy, ctrl.integral_pos_e, ctrl.integral_rpy_e])
+    out.update(dsl_in=cin, dsl_rpm=crpm, dsl_state=cst)
+    # (2) closed-loop HoverAviary(physics=DYN) episodes per action type; the controller is
+    # built once per env (BaseRLAviary.py:73-78) and never reset, so it carries across episodes
+    for name, at, A in (("pid", E.ActionType.PID, 3), ("vel", E.ActionType.VEL, 4),
+                        ("onedpid", E.ActionType.ONE_D_PID, 1)):
+        env = m.Hover.HoverAviary(physics=E.Physics.DYN, act=at)
+        n_ep, T = 4, 30
+        init = np.zeros((n_ep, 13)); acts = np.zeros((n_ep, T, 1, A), np.float32)
+        obs = np.zeros((n_ep, T, 12 + 15 * A)); rew = np.zeros((n_ep, T)); term = np.zeros((n_ep, T), bool)
+        trunc = np.zeros((n_ep, T), bool); states = np.zeros((n_ep, T, 13)); rpms = np.zeros((n_ep, T, 4))
+        ctl0 = np.zeros((n_ep, 9)); ctl = np.zeros((n_ep, T, 9)); ring0 = np.zeros((n_ep, 15, A), np.float32)
+        for ep in range(n_ep):
+            env.reset()
+            pos, quat, vel, _ = random_state(rng, center=(0, 0, 1.0), tilt=0.1)
+            set_drone_state(pb, env, 0, pos, quat, vel, np.zeros(3))
+            env._updateAndStoreKinematicInformation()      # _preprocessAction reads the stored state
+            init[ep] = np.concatenate([pos, quat, vel, np.zeros(3)])
+            c = env.ctrl[0]
+            ctl0[ep] = np.concatenate([c.last_rpy, c.integral_pos_e, c.integral_rpy_e])
+            ring0[ep] = np.array([np.asarray(a, np.float32).reshape(A) for a in env.action_buffer])
+            if name == "pid":
+                a = np.clip(pos + rng.uniform(-0.6, 0.6, 3), -1, 1)
+                a[2] = rng.uniform(0.5, 1.0)
+                if ep == 3:
+                    a = np.array([-1.0, 1.0, 1.0])          # > 1 m away: _calculateNextStep caps the step
+                seq = np.repeat(a[None], T, 0) + rng.uniform(-0.05, 0.05, (T, 3)) * (ep % 2)
+            elif name == "vel":
+                seq = rng.uniform(-1, 1, (T, 4))
+                seq[::7, :3] = 0                              # zero direction -> zero target velocity
+            else:
+                seq = rng.uniform(-1, 1, (T, 1))
+            acts[ep] = seq.astype(np.float32)[:, None, :]
+            for t in range(T):
+                o, r, te, tr, _ = env.step(acts[ep, t])
+                obs[ep, t] = o[0]; rew[ep, t] = r; term[ep, t] = te; trunc[ep, t] = tr
+                states[ep, t] = np.concatenate([env.pos[0], env.quat[0], env.vel[0], env.rpy_rates[0]])
+                rpms[ep, t] = env.last_clipped_action[0]
+                ctl[ep, t] = np.concatenate([c.last_rpy, c.integral_pos_e, c.integral_rpy_e])
+        out.update({f"{name}_init": init, f"{name}_act": acts, f"{name}_obs": obs, f"{name}_rew": rew,
+                    f"{name}_term": term, f"{name}_trunc": trunc, f"{name}_state": states,
+                    f"{name}_rpm": rpms, f"{name}_ctl0": ctl0, f"{name}_ctl": ctl, f"{name}_ring0": ring0})
+    return out
+
+
 def main():
     os.chdir(REF)   # MultiRaceAviary resolves URDF_DIR relative to the cwd (read only)
     pb = install_stubs()
     m = import_reference(pb)
+    if os.environ.get("GOLDEN_ONLY") == "pid":
+        px = pid_fixtures(pb, m)
+        path = os.path.join(HERE, "pid_golden.npz")
+        np.savez_compressed(path, **px)
+        print("wrote", path, len(px), "arrays")
+        return
     fx = {}
     fx.update(hover_fixtures(pb, m))
     fx.update(force_fixtures(pb, m))
@@ -673,6 +749,10 @@ def main():
     path = os.path.join(HERE, "race_golden.npz")
     np.savez_compressed(path, **rx)
     print("wrote", path, len(rx), "arrays")
+    px = pid_fixtures(pb, m)
+    path = os.path.join(HERE, "pid_golden.npz")
+    np.savez_compressed(path, **px)
+    print("wrote", path, len(px), "arrays")
 
 
 if __name__ == "__main__":

@@ -102,3 +102,16 @@ def test_kernel_variant_selection(lib):
         c = cfg.copy()
         mutate(c)
         assert _lib.kernel_name(c).endswith(",generic>"), _lib.kernel_name(c)
+
+
+def test_pid_action_kernels(lib):
+    """PID / VEL / ONE_D_PID select the fused-DSLPIDControl kernels (action width 3 / 4 / 1)."""
+    from gym_pybullet_adrp_amd import _lib
+    cfg = _lib.default_config(abi.TASK_HOVER)
+    for at, name, a in ((abi.ACT_PID, "PID", 3), (abi.ACT_VEL, "VEL", 4), (abi.ACT_ONE_D_PID, "ONE_D_PID", 1)):
+        c = cfg.copy()
+        c.act_type = at
+        assert _lib.kernel_name(c) == f"hover_step<f32,PYB,A{a},Bn,generic,{name}>"
+    c = cfg.copy()
+    c.act_type = 6
+    assert _lib.kernel_name(c).startswith("hover_step<")   # naming only; adrp_create rejects it

@@ -11,6 +11,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from gym_pybullet_adrp_amd import _lib  # noqa: E402
 from gym_pybullet_adrp_amd.envs.hover import HoverAviary  # noqa: E402
 from gym_pybullet_adrp_amd.utils import abi  # noqa: E402
 from gym_pybullet_adrp_amd.utils.enums import ActionType, Physics  # noqa: E402
@@ -266,3 +267,94 @@ def test_generic_ring_length(ctrl_freq):
         orc.set_state(f, i)
         env.set_state(torch.from_numpy(f.astype(np.float32)), torch.from_numpy(i))
     env.close()
+
+
+PID_GROUPS = {"pid_last_rpy": ["pid_last_rpy_x", "pid_last_rpy_y", "pid_last_rpy_z"],
+              "pid_int_pos": ["pid_int_pos_x", "pid_int_pos_y", "pid_int_pos_z"],
+              "pid_int_rpy": ["pid_int_rpy_x", "pid_int_rpy_y", "pid_int_rpy_z"]}
+GROUPS.update(PID_GROUPS)
+FLOORS.update({"pid_last_rpy": 1e-3, "pid_int_pos": 1e-3, "pid_int_rpy": 1e-3})
+PID_ACTS = {ActionType.PID: 3, ActionType.VEL: 4, ActionType.ONE_D_PID: 1}
+
+
+def random_pid_state(rng, env, orc):
+    """random_states + a DSLPIDControl state (last_rpy near the pose, integrators inside and
+    on their clips) in both."""
+    f, i = random_states(rng, env.num_envs, env, orc, tilt=0.15, omega=1.0)
+    names, _ = orc.field_names()
+    idx = {n: k for k, n in enumerate(names)}
+    E = env.num_envs
+    rpy = np.array([O.euler_from_quat(f[[idx[f"quat_{a}"] for a in "xyzw"], e]) for e in range(E)])
+    for k, ax in enumerate("xyz"):
+        f[idx[f"pid_last_rpy_{ax}"]] = rpy[:, k] + rng.uniform(-0.02, 0.02, E)
+        f[idx[f"pid_int_pos_{ax}"]] = np.clip(rng.uniform(-2.5, 2.5, E), -2, 2) * (0.075 if ax == "z" else 1)
+        f[idx[f"pid_int_rpy_{ax}"]] = rng.uniform(-1, 1, E) * (1 if ax != "z" else 20)
+    real = np.float64 if env.cfg.precision else np.float32
+    f = f.astype(real).astype(np.float64)
+    orc.set_state(f, i)
+    env.set_state(torch.from_numpy(f.astype(real)), torch.from_numpy(i))
+
+
+def pid_actions(rng, act, E, obs):
+    if act == ActionType.PID:    # waypoints, half of them more than 1 m away (capped step)
+        return np.clip(obs[:, :, :3] + rng.uniform(-1.5, 1.5, (E, 1, 3)), -2, 2).astype(np.float32)
+    a = rng.uniform(-1, 1, (E, 1, PID_ACTS[act])).astype(np.float32)
+    if act == ActionType.VEL:
+        a[::9, :, :3] = 0        # zero direction -> zero target velocity
+    return a
+
+
+@pytest.mark.parametrize("precision,rtol", [("fp32", 1e-4), ("fp64", 1e-9)])
+@pytest.mark.parametrize("physics", [Physics.PYB_GND_DRAG_DW, Physics.DYN])
+@pytest.mark.parametrize("act", list(PID_ACTS))
+def test_pid_action_types(act, physics, precision, rtol):
+    """HoverAviary PID / VEL / ONE_D_PID (BaseRLAviary.py:193-235): the fused DSLPIDControl
+    (control/DSLPIDControl.py:82-259) + sub-steps, teacher-forced per env.step against the
+    oracle (itself pinned to the reference by tests/golden/pid_golden.npz).  Controller
+    state, RPMs (last_rpm, PYB_GND_DRAG_DW) and the 3- / 4- / 1-wide action ring included."""
+    E = 2048 if precision == "fp32" else 256
+    rng = np.random.default_rng(500 + list(PID_ACTS).index(act))
+    env, orc = pair(E, physics, act=act, precision=precision, autoreset=False)
+    assert env.h.A == PID_ACTS[act] and env.h.D == 12 + 15 * PID_ACTS[act]
+    assert _lib.kernel_name(env.cfg).endswith({ActionType.PID: "PID>", ActionType.VEL: "VEL>",
+                                         ActionType.ONE_D_PID: "ONE_D_PID>"}[act])
+    random_pid_state(rng, env, orc)
+    active = active_fields(physics) | set(PID_GROUPS)
+    obs = orc.hover_eval()[0]
+    for t in range(4):
+        a = pid_actions(rng, act, E, obs)
+        obs, rew_o, te_o, tr_o, _ = orc.step(a)
+        obs_g, rew_g, te_g, tr_g, _ = env.step(torch.from_numpy(a))
+        torch.cuda.synchronize()
+        compare_state(env, orc, rtol, active)
+        og = obs_g.cpu().numpy()
+        np.testing.assert_array_equal(og[..., 12:], obs[..., 12:])
+        np.testing.assert_allclose(rew_g.cpu().numpy(), rew_o, rtol=max(rtol, 1e-6), atol=1e-5)
+        f, i = orc.get_state()
+        real = np.float64 if env.cfg.precision else np.float32
+        env.set_state(torch.from_numpy(f.astype(real)), torch.from_numpy(i))
+        orc.set_state(f.astype(real).astype(np.float64), i)
+    env.close()
+
+
+def test_pid_controller_persists_across_resets():
+    """The reference builds the DSLPIDControl objects once (BaseRLAviary.py:73-78) and never
+    resets them: a masked reset keeps the controller state, as the oracle does."""
+    E = 256
+    env, orc = pair(E, Physics.PYB, act=ActionType.ONE_D_PID, autoreset=False, initial_xyzs=[0, 0, 1.0])
+    env.reset(); orc.reset()
+    a = np.full((E, 1, 1), 0.5, np.float32)
+    for _ in range(3):
+        env.step(torch.from_numpy(a)); orc.step(a)
+    names, _ = orc.field_names()
+    pid = [k for k, n in enumerate(names) if n.startswith("pid_")]
+    f, i = orc.get_state()                    # teacher-force: identical state, then reset half
+    env.set_state(torch.from_numpy(f.astype(np.float32)), torch.from_numpy(i))
+    orc.set_state(f.astype(np.float32).astype(np.float64), i)
+    before = env.get_state()[0][pid].clone()
+    mask = np.zeros(E, np.uint8); mask[::2] = 1
+    env.reset(mask=torch.from_numpy(mask)); orc.reset(mask)
+    torch.cuda.synchronize()
+    assert torch.equal(env.get_state()[0][pid], before)
+    assert before.abs().sum() > 0
+    compare_state(env, orc, 1e-4, {"pos", "quat", "vel", "omega"} | set(PID_GROUPS))
