@@ -65,6 +65,12 @@ def load():
     lib.adrp_set_diagnostics.restype = I
     lib.adrp_diagnostic_contact_count.argtypes = [P, I]
     lib.adrp_diagnostic_contact_count.restype = I
+    lib.adrp_policy_create.argtypes = [I, I, I, I, I, P, P, P, P, P, P, ctypes.POINTER(P)]
+    lib.adrp_policy_create.restype = I
+    lib.adrp_policy_act.argtypes = [P, P, I, I, I, P, P]
+    lib.adrp_policy_act.restype = I
+    lib.adrp_policy_destroy.argtypes = [P]
+    lib.adrp_policy_destroy.restype = None
     if lib.adrp_abi_version() != abi.ABI_VERSION:
         raise AdrpError(f"libadrp ABI {lib.adrp_abi_version()} != python mirror {abi.ABI_VERSION}")
     _lib = lib

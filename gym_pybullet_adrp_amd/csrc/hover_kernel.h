@@ -525,6 +525,25 @@ __device__ __forceinline__ void stage_row(float4* lds_row, const float o12[12], 
     }
 }
 
+// per-lane select of the speculatively computed reset state (branch-free, so the reset work
+// cannot be sunk back under the done condition)
+template <typename Real>
+__device__ __forceinline__ void select_reset(bool done, Body<Real>& b, const Body<Real>& rb, int32_t& sc, int32_t rsc,
+                                             int32_t& ep, int32_t rep, float o12[12], const float ro12[12]) {
+    auto s3 = [&](V3<Real>& x, const V3<Real>& y) { x.x = done ? y.x : x.x; x.y = done ? y.y : x.y; x.z = done ? y.z : x.z; };
+    auto s4 = [&](Q4<Real>& x, const Q4<Real>& y) {
+        x.x = done ? y.x : x.x; x.y = done ? y.y : x.y; x.z = done ? y.z : x.z; x.w = done ? y.w : x.w;
+    };
+    s3(b.pos, rb.pos); s3(b.vel, rb.vel); s3(b.w, rb.w); s3(b.angv, rb.angv);
+    s4(b.q, rb.q); s4(b.ql, rb.ql);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b.prev_rpm[i] = done ? rb.prev_rpm[i] : b.prev_rpm[i];
+    sc = done ? rsc : sc;
+    ep = done ? rep : ep;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) o12[k] = done ? ro12[k] : o12[k];
+}
+
 // B == 0: runtime ring length a.B;  SC > 0: compile-time sub-step count (loop fully unrolled);
 // STG: LDS-staged obs rows (needs A == 4, B == 15 and every lane of the block live);
 // CTL: 0 (RPM / ONE_D_RPM actions) or ADRP_ACT_PID / _VEL / _ONE_D_PID (fused DSLPIDControl)
@@ -563,6 +582,19 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     const bool lag = C.link_lag && !DYN;
     Body<Real> b;
     load_body(a, e, b, lag, DRAG, DYN);
+#ifdef ADRP_SPEC_RESET
+    // Speculative auto-reset: the next episode's initial state (Philox draws, quaternion, obs)
+    // depends only on (env, episode), so it is computed for every lane up front, where its
+    // independent instructions fill the dependency stalls of the sub-step chain (one wave
+    // per SIMD at E = 4096), and selected at the end for the done lanes.
+    Body<Real> rb;
+    int32_t rsc = sc, rep = ep;
+    float ro12[12];
+    if (a.autoreset) {
+        hover_reset_state(a, C, e, rb, rsc, rep);
+        hover_obs12(C, rb, ro12);
+    }
+#endif
     // ---- _preprocessAction: RPM = HOVER_RPM * (1 + 0.05 a), the gain in float32 (NEP 50),
     //      or the DSLPIDControl output for the PID action types ----
     Real rpm[4];
@@ -686,12 +718,20 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
 #pragma unroll
                 for (int k = 0; k < kRowF4; ++k) trow[k] = t[k];
             }
+#ifndef ADRP_SPEC_RESET
             hover_reset_state(a, C, e, b, sc, ep);
             hover_obs12(C, b, o12);      // the reset keeps the ring: only the kinematic part changes
             my[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
             my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
             my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
+#endif
         }
+#ifdef ADRP_SPEC_RESET
+        select_reset(done, b, rb, sc, rsc, ep, rep, o12, ro12);
+        my[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
+        my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
+        my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
+#endif
         RACE_SET(t4);
         __syncthreads();
         float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
@@ -712,9 +752,14 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
                 if constexpr (B > 0) write_row<A, B>(a.tobs + size_t(e) * D, o12, ring, head1);
                 else write_row_generic<A>(a.tobs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
             }
+#ifndef ADRP_SPEC_RESET
             hover_reset_state(a, C, e, b, sc, ep);
             hover_obs12(C, b, o12);
+#endif
         }
+#ifdef ADRP_SPEC_RESET
+        select_reset(done, b, rb, sc, rsc, ep, rep, o12, ro12);
+#endif
         RACE_SET(t4);
         if constexpr (B > 0) write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
         else write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);

@@ -212,6 +212,33 @@ int adrp_profile_end(adrp_t* h, float* kernel_ms, int cap);
 int adrp_set_diagnostics(adrp_t* h, int enable);
 int adrp_diagnostic_contact_count(adrp_t* h, int reset);
 
+/* ---------------------------------------------------------------------------------------
+ * On-device policy forward: the actor of an SB3 PPO MlpPolicy
+ * (in_dim -> hidden1 -> hidden2 -> 4, Tanh or ReLU) + the RLController action transform,
+ * on f32 MFMA.  Replaces, batched, RLController.predict / _action_transform
+ * (user_controller/RLController.py:39-73, RLControllerTwoGates.py:38-69) over
+ * PPO.predict(obs, deterministic=True) (stable_baselines3 2.3.2: mlp_extractor.policy_net,
+ * action_net, clip to the [-1, 1] Box).  Weights are host float32 arrays in torch Linear
+ * layout ([out][in] row-major): the policy.pth tensors mlp_extractor.policy_net.{0,2}.* and
+ * action_net.*.  obs rows are the first in_dim floats of each obs_stride-wide row (e.g.
+ * adrp_step's obs_dev with rows = E*N); act_dev receives float [rows][4].
+ * --------------------------------------------------------------------------------------- */
+#define ADRP_POLICY_TANH 0          /* SB3 MlpPolicy default activation_fn (nn.Tanh) */
+#define ADRP_POLICY_RELU 1          /* policy_kwargs activation_fn=nn.ReLU (twogates.zip) */
+#define ADRP_POLICY_RAW 0           /* act = clip(mean, -1, 1) */
+#define ADRP_POLICY_RELATIVE 1      /* RLController: a[3]=0; obs[[0,1,2,5]] + a*[1,1,1,pi], yaw map2pi */
+#define ADRP_POLICY_ABSOLUTE 2      /* RLControllerTwoGates: a[3]=0; a*[1,1,1,pi], yaw map2pi */
+
+typedef struct adrp_policy adrp_policy_t;
+
+/* hidden1, hidden2 in {16, 32, 64, 128}; in_dim 1..256 */
+int adrp_policy_create(int device, int in_dim, int hidden1, int hidden2, int activation,
+                       const float* w1, const float* b1, const float* w2, const float* b2,
+                       const float* w3, const float* b3, adrp_policy_t** out);
+int adrp_policy_act(adrp_policy_t* p, const float* obs_dev, int rows, int obs_stride, int mode,
+                    float* act_dev, void* stream);
+void adrp_policy_destroy(adrp_policy_t* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -727,10 +727,77 @@ def pid_fixtures(pb, m):
     return out
 
 
+def policy_fixtures(pb, m):
+    """On-device policy: the actor weights of the reference's two SB3 zips
+    (user_controller/*.zip, read with torch.load(weights_only=True), nothing unpickled) and
+    the RLController / RLControllerTwoGates action transforms (user_controller/*.py:56-73)
+    run on scripted agent outputs (stable_baselines3 is absent: PPO.load returns a stand-in
+    whose predict hands back preset actions)."""
+    import io
+    import json
+    import zipfile
+    import torch
+    out = {}
+    keys = ("mlp_extractor.policy_net.0.weight", "mlp_extractor.policy_net.0.bias",
+            "mlp_extractor.policy_net.2.weight", "mlp_extractor.policy_net.2.bias",
+            "action_net.weight", "action_net.bias")
+    for name in ("example_RL_model", "twogates"):
+        with zipfile.ZipFile(os.path.join(REF, "user_controller", name + ".zip")) as zf:
+            sd = torch.load(io.BytesIO(zf.read("policy.pth")), map_location="cpu", weights_only=True)
+            kw = json.loads(zf.read("data")).get("policy_kwargs") or {}
+        for i, k in enumerate(keys):
+            out[f"{name}_w{i}"] = sd[k].float().numpy()
+        out[f"{name}_relu"] = np.array("ReLU" in str(kw.get("activation_fn", "Tanh")))
+
+    class _Agent:
+        preset = None
+
+        def predict(self, obs, deterministic=True):
+            return _Agent.preset.copy(), None
+
+    sb3 = types.ModuleType("stable_baselines3")
+    sb3.PPO = types.SimpleNamespace(load=lambda *_a, **_k: _Agent())
+    sys.modules["stable_baselines3"] = sb3
+    uc = types.ModuleType("user_controller")          # bypass the package __init__
+    uc.__path__ = [os.path.join(REF, "user_controller")]
+    sys.modules["user_controller"] = uc
+    uc.BaseController = importlib.import_module("user_controller.BaseController").BaseController
+    RL = importlib.import_module("user_controller.RLController").RLController
+    RL2 = importlib.import_module("user_controller.RLControllerTwoGates").RLControllerTwoGates
+    rng = np.random.default_rng(31)
+    n = 256
+    obs = np.zeros((n, 49))
+    obs[:, :3] = rng.uniform(-3, 3, (n, 3))
+    obs[:, 3:6] = rng.uniform(-math.pi, math.pi, (n, 3))
+    obs[:, 6:12] = rng.uniform(-2, 2, (n, 6))
+    obs[:, 12:] = rng.uniform(-1.5, 1.5, (n, 37))
+    obs[:8, 5] = [math.pi, -math.pi, math.pi - 1e-7, -math.pi + 1e-7, 0.0, 3.0, -3.0, 1e-9]   # map2pi edges
+    obs = obs.astype(np.float32).astype(np.float64)
+    acts = rng.uniform(-1.2, 1.2, (n, 4)).astype(np.float32)
+    rel = np.zeros((n, 4)); ab = np.zeros((n, 4))
+    for k in range(n):
+        c = RL(0, initial_obs=obs[k], initial_info={})
+        _Agent.preset = acts[k]
+        cmd, args = c.predict(obs[k], ep_time=0.0)
+        rel[k] = np.concatenate([np.asarray(args[0], float), [args[3]]])
+        c2 = RL2(0, initial_obs=obs[k], initial_info={})
+        _Agent.preset = acts[k][None, :].astype(np.float64)
+        cmd2, args2 = c2.predict(obs[k], ep_time=0.0)
+        ab[k] = np.concatenate([np.asarray(args2[0], float), [args2[3]]])
+    out.update(pol_obs=obs, pol_agent_act=acts, pol_relative=rel, pol_absolute=ab)
+    return out
+
+
 def main():
     os.chdir(REF)   # MultiRaceAviary resolves URDF_DIR relative to the cwd (read only)
     pb = install_stubs()
     m = import_reference(pb)
+    if os.environ.get("GOLDEN_ONLY") == "policy":
+        px = policy_fixtures(pb, m)
+        path = os.path.join(HERE, "policy_golden.npz")
+        np.savez_compressed(path, **px)
+        print("wrote", path, len(px), "arrays")
+        return
     if os.environ.get("GOLDEN_ONLY") == "pid":
         px = pid_fixtures(pb, m)
         path = os.path.join(HERE, "pid_golden.npz")
@@ -751,6 +818,10 @@ def main():
     print("wrote", path, len(rx), "arrays")
     px = pid_fixtures(pb, m)
     path = os.path.join(HERE, "pid_golden.npz")
+    np.savez_compressed(path, **px)
+    print("wrote", path, len(px), "arrays")
+    px = policy_fixtures(pb, m)
+    path = os.path.join(HERE, "policy_golden.npz")
     np.savez_compressed(path, **px)
     print("wrote", path, len(px), "arrays")
 
