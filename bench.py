@@ -48,7 +48,21 @@ def parse():
     p.add_argument("--level", default="level0", help="race: track preset (level0 = config 3, level3 = config 4)")
     p.add_argument("--drones", type=int, default=2, help="race: drones per env")
     p.add_argument("--racemode", default="COMPARE", choices=["COMPARE", "COMPETE"])
+    p.add_argument("--policy", default=None,
+                   help="race: closed loop with the on-device PPO actor: 'example' / 'twogates' (the reference's "
+                        "user_controller zips, weights from tests/golden/policy_golden.npz) or a SB3 zip path")
     return p.parse_args()
+
+
+def make_policy(spec, device, racemode):
+    from gym_pybullet_adrp_amd.policy import ACTOR_KEYS, DevicePolicy
+    mode = "absolute" if spec == "twogates" else "relative"     # RLControllerTwoGates / RLController
+    if spec in ("example", "twogates"):
+        g = np.load(os.path.join(ROOT, "tests", "golden", "policy_golden.npz"))
+        name = "example_RL_model" if spec == "example" else "twogates"
+        w = {k: g[f"{name}_w{i}"] for i, k in enumerate(ACTOR_KEYS)}
+        return DevicePolicy(w, "relu" if bool(g[f"{name}_relu"]) else "tanh", device, mode)
+    return DevicePolicy.from_zip(spec, device, mode)
 
 
 def cpu_baseline(cfg, seconds):
@@ -127,8 +141,22 @@ def main():
         acts = torch.cat([tgt, torch.zeros((nbuf, E, N, 1), device=dev)], -1).contiguous()
     else:
         acts = (torch.rand((nbuf, E, 1, 4), generator=gen, device=dev) * 2 - 1).contiguous()
+    policy = None
+    if args.policy:
+        if args.task != "race":
+            raise SystemExit("--policy drives MultiRaceAviary (FULLSTATE setpoints)")
+        policy = make_policy(args.policy, local, args.racemode)
+        pact = torch.empty((E, args.drones, 4), device=dev)
+
+        class _Loop:   # one "step" = policy forward on the current obs + env.step on its setpoints
+            def step(self, _a):
+                policy.act(env._obs, out=pact)
+                return env.step(pact)
+        stepper = _Loop()
+    else:
+        stepper = env
     for k in range(args.warmup):
-        env.step(acts[k % nbuf])
+        stepper.step(acts[k % nbuf])
     torch.cuda.synchronize()
 
     # ---- timed region: exactly K env.steps, replayed from a captured HIP graph ----
@@ -137,12 +165,12 @@ def main():
     side = torch.cuda.Stream(device=dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
-        env.step(acts[0])
+        stepper.step(acts[0])
     torch.cuda.current_stream(dev).wait_stream(side)
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         for k in range(G):
-            env.step(acts[k % nbuf])
+            stepper.step(acts[k % nbuf])
     graph.replay()                                           # untimed: warms the graph
     torch.cuda.synchronize()
     if world > 1:
@@ -169,6 +197,22 @@ def main():
         env.step(acts[k % nbuf])
     kern_ms = env.h.profile_end(nk)
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    policy_rec = None
+    if policy is not None:   # policy launches are on torch's current stream: torch events see them
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(200)]
+        for a, b in ev:
+            a.record()
+            policy.act(env._obs, out=pact)
+            b.record()
+        torch.cuda.synchronize()
+        pol_us = float(np.mean([a.elapsed_time(b) for a, b in ev])) * 1e3
+        rows = E * args.drones
+        flops = 2 * rows * (policy.in_dim * policy.h1 + policy.h1 * policy.h2 + policy.h2 * 4)
+        policy_rec = {"weights": args.policy, "arch": f"{policy.in_dim}-{policy.h1}-{policy.h2}-4",
+                      "kernel_us": pol_us, "rows": rows, "flops": flops,
+                      "mfma_f32": {"achieved_tflops": flops / pol_us / 1e6, "unit": "TFLOP/s"},
+                      "bytes": rows * (env.h.D + 4) * 4,
+                      "note": "event pairs around each policy launch on the current stream"}
 
     # ---- eager (no graph) end-to-end rate, for reference ----
     torch.cuda.synchronize()
@@ -244,12 +288,18 @@ def main():
                             "parallelism": f"env-sharded dp{world}"}
         result["data"] = "synthetic: level preset resets (device Philox), FULLSTATE targets start + U(+-0.3) m"
         result["drone_steps_per_s"] = result["value"] * args.drones
+        if policy_rec is not None:
+            result["config"]["workload"] += f"; closed loop: on-device PPO actor ({args.policy}) each step"
+            result["data"] = "synthetic: level preset resets (device Philox); setpoints from the reference's PPO actor"
+            result["policy"] = policy_rec
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(env.cfg, args.cpu_seconds)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if policy is not None:
+        policy.close()
     env.close()
     if world > 1:
         dist.barrier()

@@ -5,6 +5,7 @@
 // adrp_step's obs buffer in, FULLSTATE setpoints for the next adrp_step out, on the same stream.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -20,6 +21,7 @@ int seterr(adrp_t* h, int code, const std::string& msg);
 struct adrp_policy {
     int device = 0;
     int in_dim = 0, h1 = 0, h2 = 0, relu = 0;
+    int row_tiles = 0;       // 16-row tiles per block (ADRP_POLICY_RT; 0 = default)
     PolicyLayout L{};
     float* blob = nullptr;   // device fragment blob
 };
@@ -28,9 +30,8 @@ struct adrp_policy {
 // fragments policy_kernel reads (see policy_kernel.h for the k order).
 static std::vector<float> build_blob(int in_dim, int H1, int H2, const float* w1, const float* b1, const float* w2,
                                      const float* b2, const float* w3, const float* b3, PolicyLayout* L) {
-    const int T1 = H1 / 16, T2 = H2 / 16, S1 = (in_dim + 3) / 4;
+    const int T1 = H1 / 16, T2 = H2 / 16, S1 = kPolicyS1;
     L->in_dim = in_dim;
-    L->s1 = S1;
     L->f1 = 0;
     L->f2 = L->f1 + T1 * S1 * 64;
     L->f3 = L->f2 + T2 * T1 * 4 * 64;
@@ -67,17 +68,25 @@ static std::vector<float> build_blob(int in_dim, int H1, int H2, const float* w1
 template <int T1, int T2>
 static hipError_t launch_policy(const adrp_policy_t* p, const float* obs, int rows, int stride, float* act, int mode,
                                 hipStream_t s) {
-    const size_t lds = size_t(p->L.total) * sizeof(float);
-    static bool attr = false;   // per instantiation: allow > 64 KiB of dynamic LDS
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&policy_kernel<T1, T2>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    const dim3 grid((rows + 63) / 64);
-    hipLaunchKernelGGL((policy_kernel<T1, T2>), grid, dim3(256), lds, s, p->blob, p->L, obs, rows, stride, act, mode,
-                       p->relu);
+    // row tiles per block: each block reuses its weight fragments over RT x 16 rows
+    const int tiles = (rows + 15) / 16;
+    int rt = p->row_tiles;
+    if (rt == 0) rt = T1 >= 8 ? 2 : 1;   // measured (rocprof, MI355X): 49-64-64 @ 4096 rows best at 1,
+                                          // 49-128-128 @ 16384 rows at 2 (tools/policy_probe.py)
+    const dim3 grid((tiles + rt - 1) / rt), blk(64 * (T1 > T2 ? T1 : T2));
+#define ADRP_POLICY_LAUNCH(R)                                                                                   \
+    do {                                                                                                        \
+        if (p->relu)                                                                                            \
+            hipLaunchKernelGGL((policy_kernel<T1, T2, true, R>), grid, blk, 0, s, p->blob, p->L, obs, rows, stride, act, \
+                               mode);                                                                           \
+        else                                                                                                    \
+            hipLaunchKernelGGL((policy_kernel<T1, T2, false, R>), grid, blk, 0, s, p->blob, p->L, obs, rows, stride,     \
+                               act, mode);                                                                      \
+    } while (0)
+    if (rt >= 4) ADRP_POLICY_LAUNCH(4);
+    else if (rt == 2) ADRP_POLICY_LAUNCH(2);
+    else ADRP_POLICY_LAUNCH(1);
+#undef ADRP_POLICY_LAUNCH
     return hipGetLastError();
 }
 
@@ -100,7 +109,7 @@ extern "C" int adrp_policy_create(int device, int in_dim, int hidden1, int hidde
     if (!out) return seterr(nullptr, ADRP_ERR_INVALID, "out is NULL");
     *out = nullptr;
     if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3) return seterr(nullptr, ADRP_ERR_INVALID, "NULL weight pointer");
-    if (in_dim < 1 || in_dim > 256) return seterr(nullptr, ADRP_ERR_INVALID, "policy in_dim must be 1..256");
+    if (in_dim < 1 || in_dim > 4 * kPolicyS1) return seterr(nullptr, ADRP_ERR_INVALID, "policy in_dim must be 1..64");
     if (!pow2_tiles(hidden1) || !pow2_tiles(hidden2))
         return seterr(nullptr, ADRP_ERR_INVALID, "policy hidden sizes must be 16, 32, 64 or 128");
     if (activation != ADRP_POLICY_TANH && activation != ADRP_POLICY_RELU)
@@ -112,11 +121,8 @@ extern "C" int adrp_policy_create(int device, int in_dim, int hidden1, int hidde
     adrp_policy_t* p = new adrp_policy_t();
     p->device = device;
     p->in_dim = in_dim; p->h1 = hidden1; p->h2 = hidden2; p->relu = activation == ADRP_POLICY_RELU;
+    if (const char* env = getenv("ADRP_POLICY_RT")) p->row_tiles = atoi(env);
     const std::vector<float> blob = build_blob(in_dim, hidden1, hidden2, w1, b1, w2, b2, w3, b3, &p->L);
-    if (size_t(p->L.total) * sizeof(float) > 160 * 1024) {
-        delete p;
-        return seterr(nullptr, ADRP_ERR_INVALID, "policy weights exceed the 160 KiB LDS of a CU");
-    }
     if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&p->blob, blob.size() * sizeof(float)) != hipSuccess) {
         delete p;
         return seterr(nullptr, ADRP_ERR_OOM, "hipMalloc failed");

@@ -10,14 +10,14 @@
 //     -> action_net (Linear) = the Gaussian mean; BasePolicy.predict clips it to the Box [-1, 1]
 //   map2pi                                        gym_pybullet_adrp/utils/utils.py:188-197
 //
-// Layout: one wave = 16 observation rows; all three layers run on the f32-input MFMA
+// Layout: one block = 16 observation rows; all three layers run on the f32-input MFMA
 // v_mfma_f32_16x16x4_f32 (exact f32 fma chains, no reduced precision), oriented so that each
-// layer's accumulator tile is the next layer's B operand with no lane movement:
+// layer's accumulator tile is, element for element, the next layer's B operand:
 //   H1ᵀ = W1 · Xᵀ,  H2ᵀ = W2 · act(H1ᵀ + b1),  Oᵀ = W3 · act(H2ᵀ + b2)
 // A 16x16 f32 accumulator holds [unit = 16 t + 4 (lane >> 4) + reg][row = lane & 15]; as a
 // B operand, k-step (t, reg) then covers units {16 t + 4 g + reg : g = 0..3}.  The host
-// pre-permutes every weight tile into that k order ("fragments": 64 floats, one per lane,
-// read conflict-free from LDS), so no layer needs a transpose or an LDS round trip.
+// pre-permutes every weight tile into that k order ("fragments": 64 floats, one per lane),
+// so the hand-off between layers is a same-lane LDS store / load with no transpose.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -27,9 +27,12 @@ namespace adrp {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// fragment-blob layout (floats), written by the host (policy.hip: build_blob)
+// fragment-blob layout (floats), written by the host (policy.hip: build_blob).  Layer 1 is
+// always kPolicyS1 = 16 k-steps (in_dim <= 64, zero-padded weights), so no loop has a
+// runtime trip count.
+constexpr int kPolicyS1 = 16;
 struct PolicyLayout {
-    int in_dim, s1;          // observation width, k-steps of layer 1 (ceil(in_dim / 4))
+    int in_dim;              // observation width (<= 4 * kPolicyS1)
     int f1, f2, f3;          // fragment offsets of layers 1..3 (in floats)
     int b1, b2, b3;          // bias offsets
     int total;               // blob size in floats
@@ -38,8 +41,19 @@ struct PolicyLayout {
 // action transform (RLController._action_transform variants)
 enum { POLICY_RAW = 0, POLICY_RELATIVE = 1, POLICY_ABSOLUTE = 2 };
 
-__device__ __forceinline__ float policy_act(float x, int relu) {
-    return relu ? (x > 0.0f ? x : 0.0f) : tanhf(x);
+// tanh(x) = (e^2x - 1) / (e^2x + 1), branch-free on the hardware exp2 / rcp (|x| clamped to 15,
+// where tanh is 1 in f32); absolute error ~1e-7, far inside the policy's 2e-5 bar.  OCML's
+// tanhf branches per lane range, which splits the unrolled MFMA schedule into blocks.
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float c = __builtin_amdgcn_fmed3f(x, -15.0f, 15.0f);
+    const float t = __builtin_amdgcn_exp2f(c * 2.8853900817779268f);     // e^(2c)
+    return (t - 1.0f) * __builtin_amdgcn_rcpf(t + 1.0f);
+}
+
+template <bool RELU>
+__device__ __forceinline__ float policy_act(float x) {
+    if constexpr (RELU) return x > 0.0f ? x : 0.0f;
+    else return tanh_fast(x);
 }
 
 // map2pi(angle) = ((angle + pi) % (2 pi)) - pi with NumPy's floor-mod, in float64
@@ -51,78 +65,102 @@ __device__ __forceinline__ double map2pi_d(double a) {
     return r - pi;
 }
 
-// T1 = H1 / 16, T2 = H2 / 16.  Block = 4 waves = 64 rows; the blob is staged in LDS once.
-template <int T1, int T2>
-__global__ void __launch_bounds__(256) policy_kernel(const float* __restrict__ blob, PolicyLayout L,
+// T1 = H1 / 16, T2 = H2 / 16, RELU (else Tanh).  One block = 16 observation rows and
+// NW = max(T1, T2) waves: wave w owns hidden-unit tile w of each layer, so a launch has
+// NW x rows / 16 waves (all SIMDs busy at the race batch sizes) and each wave issues its few
+// weight fragments (read straight from global memory: 256 contiguous bytes per fragment per
+// wave, the blob L2-resident after the first waves) together with its observation loads, at
+// entry: one memory latency per launch.  The activations between layers go through LDS in
+// the B-operand order, so every read and write is conflict-free (lds[(tile*4 + reg)*64 + lane]).
+// RT row tiles (16 rows each) per block reuse the weight fragments a wave holds in registers.
+template <int T1, int T2, bool RELU, int RT>
+__global__ void __launch_bounds__(512) policy_kernel(const float* __restrict__ blob, PolicyLayout L,
                                                      const float* __restrict__ obs, int rows, int obs_stride,
-                                                     float* __restrict__ act, int mode, int relu) {
-    extern __shared__ float lds[];
-    {   // stage the fragment blob (float4, whole block)
-        const float4* src = reinterpret_cast<const float4*>(blob);
-        float4* dst = reinterpret_cast<float4*>(lds);
-        const int n4 = L.total >> 2;
-        for (int k = threadIdx.x; k < n4; k += blockDim.x) dst[k] = src[k];
-    }
-    __syncthreads();
+                                                     float* __restrict__ act, int mode) {
+    __shared__ float h1s[T1 * 4 * 64];
+    __shared__ float h2s[T2 * 4 * 64];
     const int lane = threadIdx.x & 63;
-    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
-    if (row0 >= rows) return;                      // whole wave out of range (after the barrier)
+    const int w = threadIdx.x >> 6;          // wave = unit tile
+    const int g = lane >> 4;
+    const bool l1 = w < T1, l2 = w < T2;
+    // ---- the weights this wave needs, issued up front, kept for all RT row tiles ----
+    float w1f[kPolicyS1], w2f[T1][4], b1v[4], b2v[4];
+#pragma unroll
+    for (int s = 0; s < kPolicyS1; ++s) w1f[s] = blob[L.f1 + ((l1 ? w : 0) * kPolicyS1 + s) * 64 + lane];
+#pragma unroll
+    for (int t = 0; t < T1; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w2f[t][i] = blob[L.f2 + (((l2 ? w : 0) * T1 + t) * 4 + i) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        b1v[i] = blob[L.b1 + 16 * (l1 ? w : 0) + 4 * g + i];
+        b2v[i] = blob[L.b2 + 16 * (l2 ? w : 0) + 4 * g + i];
+    }
+    float w3f[T2][4], b3v[4];
+    if (w == 0) {
+#pragma unroll
+        for (int u = 0; u < T2; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w3f[u][i] = blob[L.f3 + (u * 4 + i) * 64 + lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b3v[i] = blob[L.b3 + i];
+    }
+    for (int rt = 0; rt < RT; ++rt) {
+    const int row0 = (blockIdx.x * RT + rt) * 16;
+    if (row0 >= rows) return;                // block-uniform
     const int r = row0 + (lane & 15);
     const bool live = r < rows;
-    const int g = lane >> 4;
     const float* xrow = obs + size_t(live ? r : row0) * obs_stride;
-
-    // ---- layer 1: H1ᵀ[16 t + ...][row] = Σ_k W1[unit][k] X[row][k] ----
-    f32x4 h1[T1];
+    float xb[kPolicyS1];
 #pragma unroll
-    for (int t = 0; t < T1; ++t) h1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < L.s1; ++s) {
+    for (int s = 0; s < kPolicyS1; ++s) {
         const int k = 4 * s + g;
-        const float xb = (live && k < L.in_dim) ? xrow[k] : 0.0f;
-#pragma unroll
-        for (int t = 0; t < T1; ++t) {
-            const float wa = lds[L.f1 + (t * L.s1 + s) * 64 + lane];
-            h1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa, xb, h1[t], 0, 0, 0);
-        }
+        const float v = xrow[k < L.in_dim ? k : 0];
+        xb[s] = (live && k < L.in_dim) ? v : 0.0f;
     }
-#pragma unroll
-    for (int t = 0; t < T1; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) h1[t][i] = policy_act(h1[t][i] + lds[L.b1 + 16 * t + 4 * g + i], relu);
 
-    // ---- layer 2: the layer-1 accumulators are the B operands ----
-    f32x4 h2[T2];
+    // ---- layer 1, unit tile w: two interleaved accumulator chains over the 16 k-steps ----
+    if (l1) {
+        f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
 #pragma unroll
-    for (int u = 0; u < T2; ++u) h2[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < kPolicyS1; s += 2) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1f[s], xb[s], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1f[s + 1], xb[s + 1], a1, 0, 0, 0);
+        }
 #pragma unroll
-    for (int t = 0; t < T1; ++t)
+        for (int i = 0; i < 4; ++i) h1s[(w * 4 + i) * 64 + lane] = policy_act<RELU>(a0[i] + a1[i] + b1v[i]);
+    }
+    __syncthreads();
+    // ---- layer 2, unit tile w: B operands = layer-1 tiles (t, reg) from LDS ----
+    if (l2) {
+        f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int t = 0; t < T1; ++t)
 #pragma unroll
-            for (int u = 0; u < T2; ++u) {
-                const float wa = lds[L.f2 + ((u * T1 + t) * 4 + i) * 64 + lane];
-                h2[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa, h1[t][i], h2[u], 0, 0, 0);
+            for (int i = 0; i < 4; i += 2) {
+                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[t][i], h1s[(t * 4 + i) * 64 + lane], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[t][i + 1], h1s[(t * 4 + i + 1) * 64 + lane], a1, 0, 0, 0);
             }
 #pragma unroll
+        for (int i = 0; i < 4; ++i) h2s[(w * 4 + i) * 64 + lane] = policy_act<RELU>(a0[i] + a1[i] + b2v[i]);
+    }
+    __syncthreads();
+    if (w == 0) {
+    // ---- layer 3 (action_net, 4 outputs padded to a 16-unit tile), wave 0 ----
+    f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
+#pragma unroll
     for (int u = 0; u < T2; ++u)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) h2[u][i] = policy_act(h2[u][i] + lds[L.b2 + 16 * u + 4 * g + i], relu);
-
-    // ---- layer 3 (action_net, 4 outputs padded to a 16-unit tile) ----
-    f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < T2; ++u)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float wa = lds[L.f3 + (u * 4 + i) * 64 + lane];
-            o = __builtin_amdgcn_mfma_f32_16x16x4f32(wa, h2[u][i], o, 0, 0, 0);
+        for (int i = 0; i < 4; i += 2) {
+            o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w3f[u][i], h2s[(u * 4 + i) * 64 + lane], o0, 0, 0, 0);
+            o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w3f[u][i + 1], h2s[(u * 4 + i + 1) * 64 + lane], o1, 0, 0, 0);
         }
-    // lanes 0..15 hold the 4 outputs of row (lane & 15) in o[0..3]
-    if (g != 0 || !live) return;
+    // lanes 0..15 hold the 4 outputs of row (lane & 15)
+    if (g == 0 && live) {
     float a[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const float m = o[i] + lds[L.b3 + i];
+        const float m = o0[i] + o1[i] + b3v[i];
         a[i] = m < -1.0f ? -1.0f : (m > 1.0f ? 1.0f : m);     // np.clip(actions, low, high)
     }
     float4 out;
@@ -138,6 +176,10 @@ __global__ void __launch_bounds__(256) policy_kernel(const float* __restrict__ b
                           float(map2pi_d(pyaw + 0.0 * 3.141592653589793)));
     }
     reinterpret_cast<float4*>(act)[r] = out;
+    }
+    }
+    __syncthreads();          // h1s / h2s are rewritten by the next row tile
+    }
 }
 
 }  // namespace adrp

@@ -231,7 +231,7 @@ int adrp_diagnostic_contact_count(adrp_t* h, int reset);
 
 typedef struct adrp_policy adrp_policy_t;
 
-/* hidden1, hidden2 in {16, 32, 64, 128}; in_dim 1..256 */
+/* hidden1, hidden2 in {16, 32, 64, 128}; in_dim 1..64 */
 int adrp_policy_create(int device, int in_dim, int hidden1, int hidden2, int activation,
                        const float* w1, const float* b1, const float* w2, const float* b2,
                        const float* w3, const float* b3, adrp_policy_t** out);
