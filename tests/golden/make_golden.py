@@ -788,10 +788,37 @@ def policy_fixtures(pb, m):
     return out
 
 
+def logger_fixtures(pb, m):
+    """utils/logger.py Logger.log / save array layout (states reordered, controls, timestamps),
+    on scripted 20-d state vectors, for both the growing and the preallocated mode."""
+    import tempfile
+    L = importlib.import_module("gym_pybullet_adrp.utils.logger").Logger
+    rng = np.random.default_rng(41)
+    n, T = 3, 7
+    st = rng.normal(size=(T, n, 20)); ct = rng.normal(size=(T, n, 12))
+    out = {"log_state": st, "log_control": ct}
+    for tag, dur in (("grow", 0), ("prealloc", 1)):
+        with tempfile.TemporaryDirectory() as d:
+            lg = L(logging_freq_hz=30, output_folder=os.path.join(d, "r"), num_drones=n, duration_sec=dur)
+            for t in range(T):
+                for j in range(n):
+                    lg.log(drone=j, timestamp=t / 30, state=st[t, j], control=ct[t, j])
+            out[f"log_{tag}_timestamps"] = lg.timestamps
+            out[f"log_{tag}_states"] = lg.states
+            out[f"log_{tag}_controls"] = lg.controls
+    return out
+
+
 def main():
     os.chdir(REF)   # MultiRaceAviary resolves URDF_DIR relative to the cwd (read only)
     pb = install_stubs()
     m = import_reference(pb)
+    if os.environ.get("GOLDEN_ONLY") == "logger":
+        px = logger_fixtures(pb, m)
+        path = os.path.join(HERE, "logger_golden.npz")
+        np.savez_compressed(path, **px)
+        print("wrote", path, len(px), "arrays")
+        return
     if os.environ.get("GOLDEN_ONLY") == "policy":
         px = policy_fixtures(pb, m)
         path = os.path.join(HERE, "policy_golden.npz")
@@ -822,6 +849,10 @@ def main():
     print("wrote", path, len(px), "arrays")
     px = policy_fixtures(pb, m)
     path = os.path.join(HERE, "policy_golden.npz")
+    np.savez_compressed(path, **px)
+    print("wrote", path, len(px), "arrays")
+    px = logger_fixtures(pb, m)
+    path = os.path.join(HERE, "logger_golden.npz")
     np.savez_compressed(path, **px)
     print("wrote", path, len(px), "arrays")
 
