@@ -733,13 +733,16 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
 #endif
         RACE_SET(t4);
+        // the state leaves first: its registers are free before the copy-out (holding both
+        // spilled the copy-out buffer to scratch)
+        store_body(a, e, b, lag, DRAG, DYN);
+        a.ist[HI_STEP * E + e] = sc;
+        a.ist[HI_EPISODE * E + e] = ep;
+        a.ist[HI_RING_HEAD * E + e] = head1;
         __syncthreads();
         float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
-        float4 v[kRowF4];
 #pragma unroll
-        for (int k = 0; k < kRowF4; ++k) v[k] = rows[threadIdx.x + kStepBlock * k];
-#pragma unroll
-        for (int k = 0; k < kRowF4; ++k) dst[threadIdx.x + kStepBlock * k] = v[k];
+        for (int k = 0; k < kRowF4; ++k) dst[threadIdx.x + kStepBlock * k] = rows[threadIdx.x + kStepBlock * k];
     } else {
 #pragma unroll
         for (int p = 0; p < B; ++p) {
@@ -765,10 +768,12 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         else write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
     }
     RACE_MARK(t5);
-    store_body(a, e, b, lag, DRAG, DYN);
-    a.ist[HI_STEP * E + e] = sc;
-    a.ist[HI_EPISODE * E + e] = ep;
-    a.ist[HI_RING_HEAD * E + e] = head1;
+    if constexpr (!STG) {
+        store_body(a, e, b, lag, DRAG, DYN);
+        a.ist[HI_STEP * E + e] = sc;
+        a.ist[HI_EPISODE * E + e] = ep;
+        a.ist[HI_RING_HEAD * E + e] = head1;
+    }
 #ifdef ADRP_RACE_TIMING
     RACE_MARK(t6);
     if (threadIdx.x == 0) {   // [loads, sub-steps, obs+flags, reset, obs row, state stores, total, -, waves]
