@@ -175,6 +175,18 @@ __device__ __forceinline__ V3<Real> euler_xyz_fast(Q4<Real> q) {
             fatan2_(Real(2) * (q.x * q.y + q.w * q.z), squ + sqx - sqy - sqz)};
 }
 
+// euler_xyz_fast with the gimbal-lock branches behind a wave-uniform test: the common path
+// evaluates 3 atan2 instead of the 5 an if-converted select computes (call with the lanes
+// that need the result active; inactive lanes do not vote)
+template <typename Real>
+__device__ __forceinline__ V3<Real> euler_xyz_fast_u(Q4<Real> q) {
+    const Real sarg = Real(-2) * (q.x * q.z - q.w * q.y);
+    if (__builtin_expect(__any(fabs_(sarg) >= Real(0.99999)), 0)) return euler_xyz_fast(q);
+    const Real sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
+    return {fatan2_(Real(2) * (q.y * q.z + q.w * q.x), squ - sqx - sqy + sqz), fasin_(sarg),
+            fatan2_(Real(2) * (q.x * q.y + q.w * q.z), squ + sqx - sqy - sqz)};
+}
+
 // getQuaternionFromEuler (rpy extrinsic xyz)
 template <typename Real>
 __device__ __forceinline__ Q4<Real> quat_from_euler(Real r, Real p, Real y) {

@@ -308,7 +308,7 @@ __device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& args, c
 
 template <typename Real>
 __device__ __forceinline__ V3<Real> hover_obs12(const HoverConst<Real>& a, const Body<Real>& b, float o[12]) {
-    const V3<Real> rpy = euler_xyz_fast(b.q);
+    const V3<Real> rpy = euler_xyz_fast_u(b.q);
     const V3<Real> w = a.physics == ADRP_PHYS_DYN ? b.angv : b.w;
     o[0] = float(b.pos.x); o[1] = float(b.pos.y); o[2] = float(b.pos.z);
     o[3] = float(rpy.x);   o[4] = float(rpy.y);   o[5] = float(rpy.z);

@@ -517,19 +517,22 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
             // rotation itself, except in getEulerFromQuaternion's gimbal branches
             float Rm[9];
             const Real sarg = Real(-2) * (d.q.x * d.q.z - d.q.w * d.q.y);
-            if (fabs_(sarg) < Real(0.99999)) {
-                const M3<Real> Rq = rot(d.q);
-                Rm[0] = float(Rq.a00); Rm[1] = float(Rq.a01); Rm[2] = float(Rq.a02);
-                Rm[3] = float(Rq.a10); Rm[4] = float(Rq.a11); Rm[5] = float(Rq.a12);
-                Rm[6] = float(Rq.a20); Rm[7] = float(Rq.a21); Rm[8] = float(Rq.a22);
-            } else {
-                float sr, cr, sp_, cp, sy, cy;
-                sincosf(float(rpy.x), &sr, &cr);
-                sincosf(float(rpy.y), &sp_, &cp);
-                sincosf(float(rpy.z), &sy, &cy);
-                Rm[0] = cy * cp; Rm[1] = cy * sp_ * sr - sy * cr; Rm[2] = cy * sp_ * cr + sy * sr;
-                Rm[3] = sy * cp; Rm[4] = sy * sp_ * sr + cy * cr; Rm[5] = sy * sp_ * cr - cy * sr;
-                Rm[6] = -sp_; Rm[7] = cp * sr; Rm[8] = cp * cr;
+            const M3<Real> Rq = rot(d.q);
+            Rm[0] = float(Rq.a00); Rm[1] = float(Rq.a01); Rm[2] = float(Rq.a02);
+            Rm[3] = float(Rq.a10); Rm[4] = float(Rq.a11); Rm[5] = float(Rq.a12);
+            Rm[6] = float(Rq.a20); Rm[7] = float(Rq.a21); Rm[8] = float(Rq.a22);
+            // the gimbal-lock path (3 libm sincosf) sits behind a wave-uniform test, so it is
+            // entered only when a lane needs it instead of being if-converted into every sub-step
+            if (__builtin_expect(__any(!(fabs_(sarg) < Real(0.99999))), 0)) {
+                if (!(fabs_(sarg) < Real(0.99999))) {
+                    float sr, cr, sp_, cp, sy, cy;
+                    sincosf(float(rpy.x), &sr, &cr);
+                    sincosf(float(rpy.y), &sp_, &cp);
+                    sincosf(float(rpy.z), &sy, &cy);
+                    Rm[0] = cy * cp; Rm[1] = cy * sp_ * sr - sy * cr; Rm[2] = cy * sp_ * cr + sy * sr;
+                    Rm[3] = sy * cp; Rm[4] = sy * sp_ * sr + cy * cr; Rm[5] = sy * sp_ * cr - cy * sr;
+                    Rm[6] = -sp_; Rm[7] = cp * sr; Rm[8] = cp * cr;
+                }
             }
             const float pos[3] = {float(d.pos.x), float(d.pos.y), float(d.pos.z)};
             const float vel[3] = {float(d.vel.x), float(d.vel.y), float(d.vel.z)};
@@ -834,7 +837,7 @@ template <typename Real>
 __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
                                              V3<Real> pos, Q4<Real> q, V3<Real> vel, V3<Real> w, int gate,
                                              float* row, bool write, Real* row0, uint32_t gin, uint32_t oin) {
-    const V3<Real> rpy = euler_xyz_fast(q);
+    const V3<Real> rpy = euler_xyz_fast_u(q);
     const Real k12[12] = {pos.x, pos.y, pos.z, rpy.x, rpy.y, rpy.z, vel.x, vel.y, vel.z, w.x, w.y, w.z};
     if (write)
 #pragma unroll
@@ -1136,7 +1139,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                     noise[2 * p + 1] = r * sn * H.noise_std;
                 }
             }
-            mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz_fast(d.q), noise);
+            mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz_fast_u(d.q), noise);
         }
     }
     RACE_MARK(t2);
@@ -1202,7 +1205,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             if (k < N && k != dn) {
-                const V3<Real> orpy = euler_xyz_fast(gq[k]);
+                const V3<Real> orpy = euler_xyz_fast_u(gq[k]);
                 float* p = row + 49 + 6 * idx;
                 p[0] = float(gpos[k].x); p[1] = float(gpos[k].y); p[2] = float(gpos[k].z);
                 p[3] = float(orpy.x); p[4] = float(orpy.y); p[5] = float(orpy.z);
@@ -1253,8 +1256,13 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
         Real r_passed = 0;
         if (gate_id > wr_gate % 4) {
             wr_gate = gate_id;
-            if (gate_id < 4 && gate_id < C.num_gates)
-                for (int k = 0; k < 3; ++k) tgt[k] = row0[3 + 3 * gate_id + k];
+            if (gate_id < 4 && gate_id < C.num_gates) {
+                // row0[3 + 3 gate_id + k] by selects: a lane-varying index would put row0 in scratch
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) tgt[k] = g == gate_id ? row0[3 + 3 * g + k] : tgt[k];
+            }
             r_passed = Real(5);
         }
         const Real r_col = (te && !all_fin) ? Real(-1) : Real(0), r_lab = (te && all_fin) ? Real(10) : Real(0);
