@@ -48,10 +48,34 @@ def parse():
     p.add_argument("--level", default="level0", help="race: track preset (level0 = config 3, level3 = config 4)")
     p.add_argument("--drones", type=int, default=2, help="race: drones per env")
     p.add_argument("--racemode", default="COMPARE", choices=["COMPARE", "COMPETE"])
+    p.add_argument("--no-sweep", action="store_true", help="hover: skip the env-count roofline sweep")
     p.add_argument("--policy", default=None,
                    help="race: closed loop with the on-device PPO actor: 'example' / 'twogates' (the reference's "
                         "user_controller zips, weights from tests/golden/policy_golden.npz) or a SB3 zip path")
     return p.parse_args()
+
+
+def roofline_sweep(make, sizes, launches=30):
+    """The same step kernel at larger env counts (one GPU): where the launch leaves the latency-bound
+    regime of E = 4096 and becomes HBM-bound.  Kernel time from dispatch-attached events."""
+    out = []
+    for n in sizes:
+        env = make(num_envs=n, env_offset=0)
+        env.reset()
+        a = torch.rand((4, n, 1, 4), device=env.device) * 2 - 1
+        for k in range(5):
+            env.step(a[k % 4])
+        torch.cuda.synchronize()
+        env.h.profile_begin(launches)
+        for k in range(launches):
+            env.step(a[k % 4])
+        us = float(np.mean(env.h.profile_end(launches))) * 1e3
+        gbps = env.step_bytes() / (us * 1e-6) / 1e9
+        out.append({"envs": n, "kernel_us": us, "env_steps_per_s": n / (us * 1e-6), "achieved_GBps": gbps,
+                    "frac": gbps / HBM_PEAK_GBPS})
+        env.close()
+        del a
+    return out
 
 
 def make_policy(spec, device, racemode):
@@ -292,6 +316,8 @@ def main():
             result["config"]["workload"] += f"; closed loop: on-device PPO actor ({args.policy}) each step"
             result["data"] = "synthetic: level preset resets (device Philox); setpoints from the reference's PPO actor"
             result["policy"] = policy_rec
+    if args.task == "hover" and world == 1 and not args.no_sweep and policy is None:
+        result["roofline"]["sweep"] = roofline_sweep(make, [65536, 262144, 1048576])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(env.cfg, args.cpu_seconds)
     elif rank == 0:

@@ -21,7 +21,9 @@ constexpr uint32_t TAG_RACE_TRACK = 0x52540000u;
 constexpr uint32_t TAG_RACE_DRONE = 0x52440000u;
 constexpr uint32_t TAG_RACE_NOISE = 0x524e0000u;
 constexpr uint32_t TAG_RACE_DIST = 0x52460000u;
-constexpr int kRaceBlock = 64;
+constexpr int kRaceBlock = 64;      // drone lanes per block (one wave runs the sub-step chain)
+constexpr int kRaceHelpers = 3;     // helper waves per block: the sub-step disturbance draws
+constexpr int kRacePreS = 32;       // sub-steps per env.step whose draws fit the LDS table
 
 #ifdef ADRP_RACE_TIMING
 #define GJK_STAT(n) do { atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
@@ -1007,10 +1009,71 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
 // ---------------------------------------------------------------------------------------
 // env.step kernel
 // ---------------------------------------------------------------------------------------
-template <typename Real, int PH, int G>
-__global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a) {
+// The 7 disturbance values of one drone and sub-step (MultiRaceAviary.py:222-228, 532-544): the
+// world force U(lo, hi) on link 4 and the N(0, std) thrust noise per motor (Box-Muller pairs).
+template <typename Real>
+__device__ __forceinline__ void race_substep_draws(const RaceConst<Real>& H, uint64_t seed, uint64_t gid, uint32_t ep,
+                                                   int dn, uint32_t idx, Real fd[3], Real noise[4]) {
+    const U4 u = draw(seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), idx);
+    fd[0] = H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * u01r<Real>(u.a);
+    fd[1] = H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * u01r<Real>(u.b);
+    fd[2] = H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * u01r<Real>(u.c);
+    const U4 v = draw(seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
+    const uint32_t x[4] = {v.a, v.b, v.c, v.d};
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const Real u1 = (Real(x[2 * p] >> 8) + Real(1)) * Real(1.0 / 16777216.0);
+        const Real u2 = Real(x[2 * p + 1] >> 8) * Real(1.0 / 16777216.0);
+        Real r, sn, cs;
+        if constexpr (sizeof(Real) == 4) {   // v_log_f32 is log2; v_sin/v_cos take turns
+            r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+            sn = __builtin_amdgcn_sinf(u2);
+            cs = __builtin_amdgcn_cosf(u2);
+        } else {
+            r = sqrt_(Real(-2) * log(u1));
+            sincos_(Real(6.283185307179586) * u2, &sn, &cs);
+        }
+        noise[2 * p] = r * cs * H.noise_std;
+        noise[2 * p + 1] = r * sn * H.noise_std;
+    }
+}
+
+// Block = kRaceBlock drone lanes.  Wave 0 runs the serial sub-step chain (physics -> controller ->
+// physics ...; one wave per CU at the race batch sizes, one instruction per 4 cycles).  With
+// disturbances on, kRaceHelpers more waves, on the CU's otherwise idle SIMDs, pre-compute every
+// sub-step's draws into LDS while wave 0 loads its state; the chain then reads 7 values per
+// sub-step instead of running two Philox4x32-10 draws and a Box-Muller pair (~200 instructions).
+// PRE: helper waves present (the host sets it only for fp32 with disturbances on and
+// S <= kRacePreS, and then launches kRaceBlock * (1 + kRaceHelpers) threads per block).
+template <typename Real, int PH, int G, bool PRE>
+__global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) race_step_kernel(RaceArgs<Real> a) {
     RACE_MARK(t0);
     const RaceConst<Real>& C = *a.c;
+    static_assert(!PRE || sizeof(Real) == 4, "pre-computed draws: fp32 kernel only");
+    __shared__ float pre_draws[PRE ? kRacePreS * 7 * kRaceBlock : 1];
+    constexpr bool pre = PRE;
+    const int tl = threadIdx.x % kRaceBlock;
+    if (threadIdx.x >= kRaceBlock) {   // helper waves
+        if (pre) {
+            const int hl = blockIdx.x * kRaceBlock + tl;
+            const int he = hl / G < a.E ? hl / G : a.E - 1, hd = hl % G < C.N ? hl % G : 0;
+            const size_t hEN = size_t(a.E) * C.N, hslot = size_t(he) * C.N + hd;
+            const int hsc0 = a.ist[RI_STEP * hEN + hslot];
+            const uint32_t hep = uint32_t(a.ist[RI_EPISODE * hEN + hslot] - 1);
+            const uint64_t hgid = uint64_t(a.env_offset + he);
+            for (int s = int(threadIdx.x / kRaceBlock) - 1; s < C.S; s += kRaceHelpers) {
+                Real fd[3], nz[4];
+                race_substep_draws(C, a.seed, hgid, hep, hd, uint32_t(hsc0 + s), fd, nz);
+                float* dst = pre_draws + s * 7 * kRaceBlock + tl;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) dst[k * kRaceBlock] = float(fd[k]);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) dst[(3 + k) * kRaceBlock] = float(nz[k]);
+            }
+            __syncthreads();
+        }
+        return;
+    }
     // register copy of the constants the sub-step loop reads (uniform -> SGPRs; no reloads
     // behind the state stores, which the compiler cannot prove do not alias a.c)
     RaceConst<Real> H;
@@ -1028,7 +1091,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
     H.dyn_mass = C.dyn_mass; H.dyn_inv_mass = C.dyn_inv_mass; H.dyn_arm = C.dyn_arm;
     H.coll_hh = C.coll_hh; H.coll_r = C.coll_r; H.coll_zoff = C.coll_zoff; H.ang_max = C.ang_max;
     H.noise_std = C.noise_std;
-    const int lane = blockIdx.x * kRaceBlock + threadIdx.x;
+    const int lane = blockIdx.x * kRaceBlock + tl;
     const int e_raw = lane / G, d_raw = lane % G;
     const int N = C.N;
     const bool active = e_raw < a.E && d_raw < N;
@@ -1065,6 +1128,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
         lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
         lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
     }
+    if (pre) __syncthreads();   // the helpers' draws are in LDS
     RACE_MARK(t1);
 #ifdef ADRP_RACE_TIMING
     uint64_t acc_phys = 0;
@@ -1099,10 +1163,15 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
                 Fx = fz * col2(Rs);
             }
             if (H.disturbances) {   // world-frame force on link 4 at posObj = self.pos (532-544)
-                const U4 u = draw(a.seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), idx);
-                const V3<Real> fd = v3(H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * u01r<Real>(u.a),
-                                       H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * u01r<Real>(u.b),
-                                       H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * u01r<Real>(u.c));
+                V3<Real> fd;
+                if (pre) {
+                    const float* src = pre_draws + s * 7 * kRaceBlock + tl;
+                    fd = v3(Real(src[0]), Real(src[kRaceBlock]), Real(src[2 * kRaceBlock]));
+                } else {
+                    Real f3[3], nz[4];
+                    race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, nz);
+                    fd = v3(f3[0], f3[1], f3[2]);
+                }
                 const V3<Real> lo = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? d.pos : d.lpos;
                 Fx = Fx + fd;
                 Tx = cross(d.kpos - lo, fd);
@@ -1120,23 +1189,13 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_kernel(RaceArgs<Real> a)
         } else {
             Real noise[4] = {Real(0), Real(0), Real(0), Real(0)};
             if (H.disturbances) {
-                const U4 u = draw(a.seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
-                const uint32_t x[4] = {u.a, u.b, u.c, u.d};
+                if (pre) {
+                    const float* src = pre_draws + (s * 7 + 3) * kRaceBlock + tl;
 #pragma unroll
-                for (int p = 0; p < 2; ++p) {
-                    const Real u1 = (Real(x[2 * p] >> 8) + Real(1)) * Real(1.0 / 16777216.0);
-                    const Real u2 = Real(x[2 * p + 1] >> 8) * Real(1.0 / 16777216.0);
-                    Real r, sn, cs;
-                    if constexpr (sizeof(Real) == 4) {   // v_log_f32 is log2; v_sin/v_cos take turns
-                        r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-                        sn = __builtin_amdgcn_sinf(u2);
-                        cs = __builtin_amdgcn_cosf(u2);
-                    } else {
-                        r = sqrt_(Real(-2) * log(u1));
-                        sincos_(Real(6.283185307179586) * u2, &sn, &cs);
-                    }
-                    noise[2 * p] = r * cs * H.noise_std;
-                    noise[2 * p + 1] = r * sn * H.noise_std;
+                    for (int k = 0; k < 4; ++k) noise[k] = Real(src[k * kRaceBlock]);
+                } else {
+                    Real f3[3];
+                    race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, noise);
                 }
             }
             mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz_fast_u(d.q), noise);

@@ -5,7 +5,11 @@
 
 template <typename Real, int PH>
 static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
-    const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G + kRaceBlock - 1) / kRaceBlock));
+    // kRaceBlock drone lanes, + kRaceHelpers helper waves per block when the sub-step draws can be
+    // pre-computed (fp32, disturbances on, S <= kRacePreS; race_kernel.h)
+    const bool helpers = sizeof(Real) == 4 && h->cfg.track.disturbances && h->S <= kRacePreS;
+    const dim3 blk(kRaceBlock * (helpers ? 1 + kRaceHelpers : 1)),
+        grid((unsigned)((size_t(h->E) * G + kRaceBlock - 1) / kRaceBlock));
     auto go = [&](auto kernel) {
         if (h->prof_n < h->prof_cap) {
             hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
@@ -14,11 +18,21 @@ static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t*
             hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
         }
     };
-    switch (G) {
-        case 1: go(race_step_kernel<Real, PH, 1>); break;
-        case 2: go(race_step_kernel<Real, PH, 2>); break;
-        case 4: go(race_step_kernel<Real, PH, 4>); break;
-        default: go(race_step_kernel<Real, PH, 8>); break;
+    constexpr bool F32 = sizeof(Real) == 4;
+    if (helpers) {
+        switch (G) {
+            case 1: go(race_step_kernel<Real, PH, 1, F32>); break;
+            case 2: go(race_step_kernel<Real, PH, 2, F32>); break;
+            case 4: go(race_step_kernel<Real, PH, 4, F32>); break;
+            default: go(race_step_kernel<Real, PH, 8, F32>); break;
+        }
+    } else {
+        switch (G) {
+            case 1: go(race_step_kernel<Real, PH, 1, false>); break;
+            case 2: go(race_step_kernel<Real, PH, 2, false>); break;
+            case 4: go(race_step_kernel<Real, PH, 4, false>); break;
+            default: go(race_step_kernel<Real, PH, 8, false>); break;
+        }
     }
 }
 
