@@ -97,7 +97,8 @@ struct HoverReset {
 
 // kernel argument block: pointers and a few scalars only (it is rewritten for every
 // launch, so it is cold in every cache: keep it to two 64-byte lines)
-constexpr int kStepBlock = 64;   // one wave per workgroup: E = 4096 -> 64 CUs, no intra-block sync
+constexpr int kStepBlock = 64;   // envs per workgroup: one chain wave (E = 4096 -> 64 CUs)
+constexpr int kResetFields = 16; // pos 3, quat 4, vel 3, w 3, angv 3 of a reset state (HELP)
 
 template <typename Real>
 struct HoverArgs {
@@ -525,33 +526,42 @@ __device__ __forceinline__ void stage_row(float4* lds_row, const float o12[12], 
     }
 }
 
-// per-lane select of the speculatively computed reset state (branch-free, so the reset work
-// cannot be sunk back under the done condition)
-template <typename Real>
-__device__ __forceinline__ void select_reset(bool done, Body<Real>& b, const Body<Real>& rb, int32_t& sc, int32_t rsc,
-                                             int32_t& ep, int32_t rep, float o12[12], const float ro12[12]) {
-    auto s3 = [&](V3<Real>& x, const V3<Real>& y) { x.x = done ? y.x : x.x; x.y = done ? y.y : x.y; x.z = done ? y.z : x.z; };
-    auto s4 = [&](Q4<Real>& x, const Q4<Real>& y) {
-        x.x = done ? y.x : x.x; x.y = done ? y.y : x.y; x.z = done ? y.z : x.z; x.w = done ? y.w : x.w;
-    };
-    s3(b.pos, rb.pos); s3(b.vel, rb.vel); s3(b.w, rb.w); s3(b.angv, rb.angv);
-    s4(b.q, rb.q); s4(b.ql, rb.ql);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) b.prev_rpm[i] = done ? rb.prev_rpm[i] : b.prev_rpm[i];
-    sc = done ? rsc : sc;
-    ep = done ? rep : ep;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) o12[k] = done ? ro12[k] : o12[k];
-}
-
 // B == 0: runtime ring length a.B;  SC > 0: compile-time sub-step count (loop fully unrolled);
 // STG: LDS-staged obs rows (needs A == 4, B == 15 and every lane of the block live);
-// CTL: 0 (RPM / ONE_D_RPM actions) or ADRP_ACT_PID / _VEL / _ONE_D_PID (fused DSLPIDControl)
-template <typename Real, int PH, int A, int B, int SC, bool STG = false, int CTL = 0>
+// CTL: 0 (RPM / ONE_D_RPM actions) or ADRP_ACT_PID / _VEL / _ONE_D_PID (fused DSLPIDControl);
+// HELP (STG + auto-reset only): a second wave per block computes the next-episode initial state
+// of the first wave's envs (3 Philox draws, quaternion, Euler obs: ~1/4 of a wave's instruction
+// stream at E = 4096, where nearly every wave has a done lane) on another SIMD, into LDS; the
+// chain wave, issue-bound at one instruction per 4 cycles, only copies it for its done lanes.
+template <typename Real, int PH, int A, int B, int SC, bool STG = false, int CTL = 0, bool HELP = false>
 __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const HoverConst<Real>& C) {
     constexpr int BR = B > 0 ? B : 1;
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     constexpr bool DYN = (PH == ADRP_PHYS_DYN);
+    static_assert(!HELP || STG, "the reset helper wave pairs with the staged (all lanes live) kernel");
+    __shared__ Real rs_body[HELP ? kResetFields * kStepBlock : 1];
+    __shared__ float rs_obs[HELP ? 12 * kStepBlock : 1];
+    if constexpr (HELP) {
+        if (threadIdx.x >= kStepBlock) {
+            const int tl = threadIdx.x - kStepBlock;
+            const int he = blockIdx.x * kStepBlock + tl;
+            int32_t hsc = 0, hep = a.ist[HI_EPISODE * a.E + he];
+            Body<Real> rb;
+            hover_reset_state(a, C, he, rb, hsc, hep);
+            float o[12];
+            hover_obs12(C, rb, o);
+            const Real v[kResetFields] = {rb.pos.x, rb.pos.y, rb.pos.z, rb.q.x, rb.q.y, rb.q.z, rb.q.w,
+                                          rb.vel.x, rb.vel.y, rb.vel.z, rb.w.x, rb.w.y, rb.w.z,
+                                          rb.angv.x, rb.angv.y, rb.angv.z};
+#pragma unroll
+            for (int k = 0; k < kResetFields; ++k) rs_body[k * kStepBlock + tl] = v[k];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) rs_obs[k * kStepBlock + tl] = o[k];
+            __syncthreads();   // A: reset states in LDS
+            __syncthreads();   // B: the chain wave's staged obs rows
+            return;
+        }
+    }
     const int e = blockIdx.x * kStepBlock + threadIdx.x;
     const int E = a.E;
     const int D = B > 0 ? 12 + B * A : a.D;
@@ -582,19 +592,6 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     const bool lag = C.link_lag && !DYN;
     Body<Real> b;
     load_body(a, e, b, lag, DRAG, DYN);
-#ifdef ADRP_SPEC_RESET
-    // Speculative auto-reset: the next episode's initial state (Philox draws, quaternion, obs)
-    // depends only on (env, episode), so it is computed for every lane up front, where its
-    // independent instructions fill the dependency stalls of the sub-step chain (one wave
-    // per SIMD at E = 4096), and selected at the end for the done lanes.
-    Body<Real> rb;
-    int32_t rsc = sc, rep = ep;
-    float ro12[12];
-    if (a.autoreset) {
-        hover_reset_state(a, C, e, rb, rsc, rep);
-        hover_obs12(C, rb, ro12);
-    }
-#endif
     // ---- _preprocessAction: RPM = HOVER_RPM * (1 + 0.05 a), the gain in float32 (NEP 50),
     //      or the DSLPIDControl output for the PID action types ----
     Real rpm[4];
@@ -709,6 +706,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         my[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
         my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
         my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
+        if constexpr (HELP) __syncthreads();   // A: the helper wave's reset states
         if (done) {
             if (a.tobs) {   // terminal obs = the row just staged (this lane's own LDS row)
                 float4 t[kRowF4];
@@ -718,20 +716,31 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
 #pragma unroll
                 for (int k = 0; k < kRowF4; ++k) trow[k] = t[k];
             }
-#ifndef ADRP_SPEC_RESET
-            hover_reset_state(a, C, e, b, sc, ep);
-            hover_obs12(C, b, o12);      // the reset keeps the ring: only the kinematic part changes
+            if constexpr (HELP) {   // BaseAviary.reset from the helper's LDS copy
+                const int t = threadIdx.x;
+                Real v[kResetFields];
+#pragma unroll
+                for (int k = 0; k < kResetFields; ++k) v[k] = rs_body[k * kStepBlock + t];
+                b.pos = v3(v[0], v[1], v[2]);
+                b.q = {v[3], v[4], v[5], v[6]};
+                b.ql = b.q;
+                b.vel = v3(v[7], v[8], v[9]);
+                b.w = v3(v[10], v[11], v[12]);
+                b.angv = v3(v[13], v[14], v[15]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) b.prev_rpm[i] = Real(0);
+                sc = 0;
+                ep += 1;
+#pragma unroll
+                for (int k = 0; k < 12; ++k) o12[k] = rs_obs[k * kStepBlock + t];
+            } else {
+                hover_reset_state(a, C, e, b, sc, ep);
+                hover_obs12(C, b, o12);      // the reset keeps the ring: only the kinematic part changes
+            }
             my[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
             my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
             my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
-#endif
         }
-#ifdef ADRP_SPEC_RESET
-        select_reset(done, b, rb, sc, rsc, ep, rep, o12, ro12);
-        my[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
-        my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
-        my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
-#endif
         RACE_SET(t4);
         // the state leaves first: its registers are free before the copy-out (holding both
         // spilled the copy-out buffer to scratch)
@@ -755,14 +764,9 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
                 if constexpr (B > 0) write_row<A, B>(a.tobs + size_t(e) * D, o12, ring, head1);
                 else write_row_generic<A>(a.tobs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
             }
-#ifndef ADRP_SPEC_RESET
             hover_reset_state(a, C, e, b, sc, ep);
             hover_obs12(C, b, o12);
-#endif
         }
-#ifdef ADRP_SPEC_RESET
-        select_reset(done, b, rb, sc, rsc, ep, rep, o12, ro12);
-#endif
         RACE_SET(t4);
         if constexpr (B > 0) write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);
         else write_row_generic<A>(a.obs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
@@ -803,7 +807,7 @@ struct HoverTail {
 // DEF: compiled-in cf2x_consts (the reference default) instead of the device block.
 // STG: LDS-staged coalesced obs rows (host: only when E % kStepBlock == 0).
 // Launch with kStepBlock threads per workgroup.
-template <typename Real, int PH, int A, int B, bool DEF, bool STG = false, int CTL = 0>
+template <typename Real, int PH, int A, int B, bool DEF, bool STG = false, int CTL = 0, bool HELP = false>
 __global__ void __launch_bounds__(256) hover_step_kernel(Real* f, float* ring, int32_t* ist, const float* act,
                                                          float* obs, float* rew, int E, HoverTail<Real> t) {
     HoverArgs<Real> a;
@@ -814,9 +818,9 @@ __global__ void __launch_bounds__(256) hover_step_kernel(Real* f, float* ring, i
     a.E = E; a.B = t.B; a.D = t.D; a.autoreset = t.autoreset;
     if constexpr (DEF) {
         constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
-        hover_step_body<Real, PH, A, B, C.S, STG, CTL>(a, C);
+        hover_step_body<Real, PH, A, B, C.S, STG, CTL, HELP>(a, C);
     } else {
-        hover_step_body<Real, PH, A, B, 0, STG, CTL>(a, *a.c);
+        hover_step_body<Real, PH, A, B, 0, STG, CTL, HELP>(a, *a.c);
     }
 }
 

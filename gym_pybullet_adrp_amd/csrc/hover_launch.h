@@ -23,16 +23,16 @@ static void launch(K kernel, dim3 grid, dim3 blk, hipStream_t s, const HoverArgs
     }
 }
 
-template <typename Real, int A, int B, bool DEF, bool STG = false, int CTL = 0>
+template <typename Real, int A, int B, bool DEF, bool STG = false, int CTL = 0, bool HELP = false>
 static void launch_step_ph(const HoverArgs<Real>& a, int physics, dim3 grid, hipStream_t s, adrp_t* h) {
-    const dim3 blk(kBlock);
+    const dim3 blk(HELP ? 2 * kBlock : kBlock);   // HELP: + the reset helper wave
     switch (physics) {
-        case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B, DEF, STG, CTL>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B, DEF, STG, CTL>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_GND: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B, DEF, STG, CTL>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_DRAG: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B, DEF, STG, CTL>, grid, blk, s, a, h); break;
-        case ADRP_PHYS_PYB_DW: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B, DEF, STG, CTL>, grid, blk, s, a, h); break;
-        default: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B, DEF, STG, CTL>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B, DEF, STG, CTL, HELP>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B, DEF, STG, CTL, HELP>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_GND: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND, A, B, DEF, STG, CTL, HELP>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_DRAG: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B, DEF, STG, CTL, HELP>, grid, blk, s, a, h); break;
+        case ADRP_PHYS_PYB_DW: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_DW, A, B, DEF, STG, CTL, HELP>, grid, blk, s, a, h); break;
+        default: launch(hover_step_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B, DEF, STG, CTL, HELP>, grid, blk, s, a, h); break;
     }
 }
 
@@ -45,6 +45,7 @@ int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* ter
     const int ph = h->cfg.physics;
     // compiled-in constants exist for the reference default (CF2X @ 240/30 Hz, B = 15)
     const bool stg = h->stage_rows && h->E % kBlock == 0;
+    const bool help = h->cfg.autoreset && h->reset_helper;   // ADRP_RESET_HELPER=0 disables
     const int at = h->cfg.act_type;
     if (at == ADRP_ACT_PID || at == ADRP_ACT_VEL || at == ADRP_ACT_ONE_D_PID) {
         // fused DSLPIDControl: device-resident constants, runtime ring length
@@ -53,10 +54,12 @@ int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* ter
         else launch_step_ph<Real, 1, 0, false, false, ADRP_ACT_ONE_D_PID>(a, ph, grid, s, h);
     } else if (h->cf2x && h->B == 15) {
         if (h->A == 1) launch_step_ph<Real, 1, 15, true>(a, ph, grid, s, h);
+        else if (stg && help) launch_step_ph<Real, 4, 15, true, true, 0, true>(a, ph, grid, s, h);
         else if (stg) launch_step_ph<Real, 4, 15, true, true>(a, ph, grid, s, h);
         else launch_step_ph<Real, 4, 15, true>(a, ph, grid, s, h);
     } else if (h->A == 4 && h->B == 15 && stg) {
-        launch_step_ph<Real, 4, 15, false, true>(a, ph, grid, s, h);
+        if (help) launch_step_ph<Real, 4, 15, false, true, 0, true>(a, ph, grid, s, h);
+        else launch_step_ph<Real, 4, 15, false, true>(a, ph, grid, s, h);
     } else if (h->A == 1) {
         if (h->B == 15) launch_step_ph<Real, 1, 15, false>(a, ph, grid, s, h);
         else launch_step_ph<Real, 1, 0, false>(a, ph, grid, s, h);
