@@ -541,11 +541,23 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     static_assert(!HELP || STG, "the reset helper wave pairs with the staged (all lanes live) kernel");
     __shared__ Real rs_body[HELP ? kResetFields * kStepBlock : 1];
     __shared__ float rs_obs[HELP ? 12 * kStepBlock : 1];
+    __shared__ float4 rows[STG ? kStepBlock * kRowF4 : 1];
     if constexpr (HELP) {
         if (threadIdx.x >= kStepBlock) {
             const int tl = threadIdx.x - kStepBlock;
             const int he = blockIdx.x * kStepBlock + tl;
-            int32_t hsc = 0, hep = a.ist[HI_EPISODE * a.E + he];
+            const int E = a.E;
+            // the action ring: its part of the obs row is independent of the physics, so this
+            // wave loads it, stages it in LDS and appends the action (deque.append)
+            const float4 av = reinterpret_cast<const float4*>(a.act)[he];
+            float rg[BR][4];    // plain floats: float4 struct copies under a select went to scratch
+#pragma unroll
+            for (int p = 0; p < B; ++p) {
+                const float4 v = reinterpret_cast<const float4*>(a.ring)[size_t(p) * E + he];
+                rg[p][0] = v.x; rg[p][1] = v.y; rg[p][2] = v.z; rg[p][3] = v.w;
+            }
+            const int32_t head = a.ist[HI_RING_HEAD * E + he];
+            int32_t hsc = 0, hep = a.ist[HI_EPISODE * E + he];
             Body<Real> rb;
             hover_reset_state(a, C, he, rb, hsc, hep);
             float o[12];
@@ -557,8 +569,37 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
             for (int k = 0; k < kResetFields; ++k) rs_body[k * kStepBlock + tl] = v[k];
 #pragma unroll
             for (int k = 0; k < 12; ++k) rs_obs[k * kStepBlock + tl] = o[k];
-            __syncthreads();   // A: reset states in LDS
-            __syncthreads();   // B: the chain wave's staged obs rows
+            // ring part of the obs row, oldest first; the appended action is the newest entry.
+            // Every env appends once per env.step and resets keep the ring, so the head is the
+            // same for every env in practice: then the slot -> row position map is scalar.
+            float4* my = rows + tl * kRowF4;
+            const int hu = __builtin_amdgcn_readfirstlane(head);
+            if (__all(head == hu)) {
+                const int h1 = hu + 1 == B ? 0 : hu + 1;
+#pragma unroll
+                for (int p = 0; p < B; ++p) {
+                    const int k = p >= h1 ? p - h1 : p - h1 + B;
+                    my[3 + k] = make_float4(rg[p][0], rg[p][1], rg[p][2], rg[p][3]);
+                }
+                my[3 + B - 1] = av;
+            } else {
+                const int h1 = head + 1 == B ? 0 : head + 1;
+#pragma unroll
+                for (int p = 0; p < B; ++p) {
+                    int k = p - h1;
+                    k += k < 0 ? B : 0;
+                    const bool hit = p == head;
+                    my[3 + k] = make_float4(hit ? av.x : rg[p][0], hit ? av.y : rg[p][1], hit ? av.z : rg[p][2],
+                                            hit ? av.w : rg[p][3]);
+                }
+            }
+            reinterpret_cast<float4*>(a.ring)[size_t(head) * E + he] = av;
+            __syncthreads();   // A: reset states and ring rows in LDS
+            __syncthreads();   // B: the chain wave's kinematic parts and reset rows
+            // second half of the block's coalesced copy-out
+            float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
+#pragma unroll
+            for (int k = kRowF4 / 2; k < kRowF4; ++k) dst[tl + kStepBlock * k] = rows[tl + kStepBlock * k];
             return;
         }
     }
@@ -578,7 +619,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     }
     float ring[BR][A];
 #pragma unroll
-    for (int p = 0; p < B; ++p) {   // (no-op for B == 0)
+    for (int p = 0; p < (HELP ? 0 : B); ++p) {   // (no-op for B == 0; HELP: the helper wave's job)
         if constexpr (A == 4) {
             const float4 v = reinterpret_cast<const float4*>(a.ring)[size_t(p) * E + e];
             ring[p][0] = v.x; ring[p][1] = v.y; ring[p][2] = v.z; ring[p][3] = v.w;
@@ -650,7 +691,9 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     RACE_MARK(t2);
     if (touched && a.contact_count) atomicAdd(a.contact_count, 1);
     // ---- action ring: append this action at `head` (deque.append, BaseRLAviary.py:187) ----
-    if constexpr (A == 4)
+    if constexpr (HELP) {
+        // the helper wave appends
+    } else if constexpr (A == 4)
         reinterpret_cast<float4*>(a.ring)[size_t(head) * E + e] = make_float4(act[0], act[1], act[2], act[3]);
     else
 #pragma unroll
@@ -680,13 +723,14 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         // The obs row is assembled in LDS (18 float4 per lane, no padding: the copy-out
         // reads contiguous float4s at immediate offsets) and leaves as one coalesced block.
         static_assert(A == 4 && B == 15, "staged rows: 72-float rows only");
-        __shared__ float4 rows[kStepBlock * kRowF4];
         float4* my = rows + threadIdx.x * kRowF4;
         // Every env appends once per env.step and resets keep the ring, so the ring head is
         // the same for every env in practice: then the slot -> row position map is scalar
         // and the appended action simply overwrites the newest position.
         const int hu = __builtin_amdgcn_readfirstlane(head);
-        if (__all(head == hu)) {
+        if constexpr (HELP) {
+            // the ring part of the row is staged by the helper wave
+        } else if (__all(head == hu)) {
             const int h1 = hu + 1 == B ? 0 : hu + 1;
 #pragma unroll
             for (int p = 0; p < B; ++p) {
@@ -750,8 +794,9 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         a.ist[HI_RING_HEAD * E + e] = head1;
         __syncthreads();
         float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
+        constexpr int KC = HELP ? kRowF4 / 2 : kRowF4;   // HELP: the helper copies the other half
 #pragma unroll
-        for (int k = 0; k < kRowF4; ++k) dst[threadIdx.x + kStepBlock * k] = rows[threadIdx.x + kStepBlock * k];
+        for (int k = 0; k < KC; ++k) dst[threadIdx.x + kStepBlock * k] = rows[threadIdx.x + kStepBlock * k];
     } else {
 #pragma unroll
         for (int p = 0; p < B; ++p) {
