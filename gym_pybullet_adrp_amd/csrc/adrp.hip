@@ -349,6 +349,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
         return cleanup(seterr(h, ADRP_ERR_DEVICE, "initialisation failed"));
     if (const char* env = getenv("ADRP_STAGE_ROWS")) h->stage_rows = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RESET_HELPER")) h->reset_helper = atoi(env) != 0;
+    if (const char* env = getenv("ADRP_RACE_HELPERS")) h->race_helpers = atoi(env) != 0;
     const int rc = race ? (h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h))
                         : (h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h));
     if (rc != ADRP_OK) return cleanup(seterr(h, rc, "constant block upload failed"));

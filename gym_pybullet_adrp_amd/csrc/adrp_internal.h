@@ -33,6 +33,7 @@ struct adrp_handle {
     bool cf2x = false;            // compiled-in constants (hover_step_kernel<..., DEF=true>)
     bool stage_rows = true;       // LDS-staged obs rows when E % 64 == 0 (ADRP_STAGE_ROWS=0 disables)
     bool reset_helper = true;     // staged kernels: reset states from a helper wave (ADRP_RESET_HELPER=0)
+    bool race_helpers = true;     // race fp32: helper waves (track copy, draws) (ADRP_RACE_HELPERS=0)
     int diagnostics = 0;
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;

@@ -728,11 +728,25 @@ __device__ __forceinline__ Real point_part_dist(V3<Real> lp, V3<Real> h, Real r,
 }
 
 constexpr int kGateParts = 5, kObstParts = 2, kObstBit0 = ADRP_MAX_GATES * kGateParts;
+constexpr int kTrackFields = RF_WR_TARGET - RF_GATE;   // the env's actual gates (16) + obstacles (12)
+
+// Where a lane reads its env's actual gate / obstacle poses: the SoA fields in HBM, or (L) the
+// block's LDS copy [field][kRaceBlock] that the helper waves load while the chain runs.
+template <typename Real, bool L>
+struct TrackSrc {
+    const Real* f;
+    size_t EN, slot;
+    const float* lds;
+    int tl;
+    __device__ __forceinline__ Real operator()(int field) const {
+        if constexpr (L) return Real(lds[(field - RF_GATE) * kRaceBlock + tl]);
+        else return ld(f, field, EN, slot);
+    }
+};
 
 // placed collision shape of queue bit b (gate b / 5, part b % 5; obstacle bits from kObstBit0)
-template <typename Real>
-__device__ __forceinline__ Shape<Real> track_part_shape(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
-                                                        int b) {
+template <typename Real, class TS>
+__device__ __forceinline__ Shape<Real> track_part_shape(const RaceConst<Real>& C, const TS& T, int b) {
     V3<Real> off, h;
     Real r;
     int cyl;
@@ -740,25 +754,22 @@ __device__ __forceinline__ Shape<Real> track_part_shape(const RaceConst<Real>& C
         const int g = b / kGateParts, k = b - g * kGateParts;
         M3<Real> R;
         gate_part(k, C.gate_type[g] > 0, off, R, h, r, cyl);
-        const V3<Real> org = v3(ld(f, RF_GATE + 4 * g, EN, slot), ld(f, RF_GATE + 4 * g + 1, EN, slot),
-                                ld(f, RF_GATE + 4 * g + 2, EN, slot));
-        const M3<Real> Rg = rotz_(ld(f, RF_GATE + 4 * g + 3, EN, slot));
+        const V3<Real> org = v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
+        const M3<Real> Rg = rotz_(T(RF_GATE + 4 * g + 3));
         return Shape<Real>{org + mul(Rg, off), mmul_(Rg, R), h, r, cyl};
     }
     const int o = (b - kObstBit0) / kObstParts, k = (b - kObstBit0) - o * kObstParts;
     obst_part(k, off, h, r, cyl);
-    const V3<Real> org = v3(ld(f, RF_OBST + 3 * o, EN, slot), ld(f, RF_OBST + 3 * o + 1, EN, slot),
-                            ld(f, RF_OBST + 3 * o + 2, EN, slot));
+    const V3<Real> org = v3(T(RF_OBST + 3 * o), T(RF_OBST + 3 * o + 1), T(RF_OBST + 3 * o + 2));
     const M3<Real> I = {Real(1), Real(0), Real(0), Real(0), Real(1), Real(0), Real(0), Real(0), Real(1)};
     return Shape<Real>{org + off, I, h, r, cyl};
 }
 
 // in-range bits (gate g -> bit g, obstacle k -> bit k) for `cut`; returns the contact
 // decision (distance < ccut) when want_contact
-template <typename Real>
-__device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
-                                            const Shape<Real>& ds, Real cut, bool want_contact, Real ccut,
-                                            uint32_t& gin, uint32_t& oin) {
+template <typename Real, class TS>
+__device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds, Real cut,
+                                            bool want_contact, Real ccut, uint32_t& gin, uint32_t& oin) {
     const Real tol = sizeof(Real) == 4 ? Real(1e-5) : Real(1e-10);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
     const V3<Real> p = ds.c;
@@ -767,10 +778,9 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real
 #pragma unroll
     for (int g = 0; g < ADRP_MAX_GATES; ++g) {
         if (g < C.num_gates) {
-            const V3<Real> dp = p - v3(ld(f, RF_GATE + 4 * g, EN, slot), ld(f, RF_GATE + 4 * g + 1, EN, slot),
-                                       ld(f, RF_GATE + 4 * g + 2, EN, slot));
+            const V3<Real> dp = p - v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
             Real sn, cs;
-            sincos_(ld(f, RF_GATE + 4 * g + 3, EN, slot), &sn, &cs);
+            sincos_(T(RF_GATE + 4 * g + 3), &sn, &cs);
             const V3<Real> lg = v3(cs * dp.x + sn * dp.y, -sn * dp.x + cs * dp.y, dp.z);   // Rz(yaw)^T dp
             const int low = C.gate_type[g] > 0;
             bool in = false;
@@ -795,8 +805,7 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real
 #pragma unroll
     for (int o = 0; o < ADRP_MAX_OBSTACLES; ++o) {
         if (o < C.num_obstacles) {
-            const V3<Real> dp = p - v3(ld(f, RF_OBST + 3 * o, EN, slot), ld(f, RF_OBST + 3 * o + 1, EN, slot),
-                                       ld(f, RF_OBST + 3 * o + 2, EN, slot));
+            const V3<Real> dp = p - v3(T(RF_OBST + 3 * o), T(RF_OBST + 3 * o + 1), T(RF_OBST + 3 * o + 2));
             bool in = false;
             uint32_t gamb = 0, camb = 0;
 #pragma unroll
@@ -822,7 +831,7 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real
         const int b = __builtin_ctz(amb);
         amb &= amb - 1;
         const bool for_contact = (camb_all >> b) & 1u;
-        const Shape<Real> s = track_part_shape(C, f, EN, slot, b);
+        const Shape<Real> s = track_part_shape(C, T, b);
         if (gjk_within(ds, s, for_contact ? ccut : cut)) {
             if (for_contact) contact = true;
             else if (b < kObstBit0) gin |= 1u << (b / kGateParts);
@@ -835,8 +844,8 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const Real
 // ---------------------------------------------------------------------------------------
 // obs row (MultiRaceAviary._computeObs, 566-661) written straight to global memory
 // ---------------------------------------------------------------------------------------
-template <typename Real>
-__device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Real* f, size_t EN, size_t slot,
+template <typename Real, class TS>
+__device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const TS& T,
                                              V3<Real> pos, Q4<Real> q, V3<Real> vel, V3<Real> w, int gate,
                                              float* row, bool write, Real* row0, uint32_t gin, uint32_t oin) {
     const V3<Real> rpy = euler_xyz_fast_u(q);
@@ -852,9 +861,8 @@ __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Rea
         Real v4[4] = {Real(0), Real(0), Real(0), Real(0)};
         Real in = 0;
         if (g < C.num_gates) {
-            const V3<Real> org = v3(ld(f, RF_GATE + 4 * g, EN, slot), ld(f, RF_GATE + 4 * g + 1, EN, slot),
-                                    ld(f, RF_GATE + 4 * g + 2, EN, slot));
-            const Real yaw = ld(f, RF_GATE + 4 * g + 3, EN, slot);
+            const V3<Real> org = v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
+            const Real yaw = T(RF_GATE + 4 * g + 3);
             in = (gin >> g) & 1u ? Real(1) : Real(0);
             if (in > Real(0)) { v4[0] = org.x; v4[1] = org.y; v4[2] = org.z; v4[3] = yaw; }
             else {
@@ -876,8 +884,7 @@ __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const Rea
         Real v3_[3] = {Real(0), Real(0), Real(0)};
         Real in = 0;
         if (k < C.num_obstacles) {
-            const V3<Real> org = v3(ld(f, RF_OBST + 3 * k, EN, slot), ld(f, RF_OBST + 3 * k + 1, EN, slot),
-                                    ld(f, RF_OBST + 3 * k + 2, EN, slot));
+            const V3<Real> org = v3(T(RF_OBST + 3 * k), T(RF_OBST + 3 * k + 1), T(RF_OBST + 3 * k + 2));
             in = (oin >> k) & 1u ? Real(1) : Real(0);
             if (in > Real(0)) { v3_[0] = org.x; v3_[1] = org.y; v3_[2] = org.z; }
             else {
@@ -935,8 +942,9 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
     Real row0[15];
     const V3<Real> zero = v3(Real(0), Real(0), Real(0));
     uint32_t gin, oin;
-    track_query(C, f, EN, slot, drone_shape(C, npos, nq), Real(0.45), false, Real(0), gin, oin);
-    race_obs_row(C, f, EN, slot, npos, nq, zero, zero, 0, obs_row, obs_row != nullptr, row0, gin, oin);
+    const TrackSrc<Real, false> T{f, EN, slot, nullptr, 0};   // the fields just written above
+    track_query(C, T, drone_shape(C, npos, nq), Real(0.45), false, Real(0), gin, oin);
+    race_obs_row(C, T, npos, nq, zero, zero, 0, obs_row, obs_row != nullptr, row0, gin, oin);
     if (C.compete && obs_row) {   // other drones' nominal pos + rpy
         int idx = 0;
         for (int k = 0; k < C.N; ++k) {
@@ -1043,25 +1051,28 @@ __device__ __forceinline__ void race_substep_draws(const RaceConst<Real>& H, uin
 // disturbances on, kRaceHelpers more waves, on the CU's otherwise idle SIMDs, pre-compute every
 // sub-step's draws into LDS while wave 0 loads its state; the chain then reads 7 values per
 // sub-step instead of running two Philox4x32-10 draws and a Box-Muller pair (~200 instructions).
-// PRE: helper waves present (the host sets it only for fp32 with disturbances on and
-// S <= kRacePreS, and then launches kRaceBlock * (1 + kRaceHelpers) threads per block).
+// PRE: helper waves present (fp32; the host then launches kRaceBlock * (1 + kRaceHelpers)
+// threads per block).  They load the env's actual track (28 fields per lane) into LDS for the
+// post-loop queries, and with disturbances on (S <= kRacePreS) the sub-step draws.
 template <typename Real, int PH, int G, bool PRE>
 __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) race_step_kernel(RaceArgs<Real> a) {
     RACE_MARK(t0);
     const RaceConst<Real>& C = *a.c;
     static_assert(!PRE || sizeof(Real) == 4, "pre-computed draws: fp32 kernel only");
     __shared__ float pre_draws[PRE ? kRacePreS * 7 * kRaceBlock : 1];
-    constexpr bool pre = PRE;
+    __shared__ float trk_lds[PRE ? kTrackFields * kRaceBlock : 1];
+    const bool pre = PRE && C.disturbances && C.S <= kRacePreS;    // grid-uniform
     const int tl = threadIdx.x % kRaceBlock;
     if (threadIdx.x >= kRaceBlock) {   // helper waves
-        if (pre) {
+        if constexpr (PRE) {
+            const int hw = int(threadIdx.x / kRaceBlock) - 1;
             const int hl = blockIdx.x * kRaceBlock + tl;
             const int he = hl / G < a.E ? hl / G : a.E - 1, hd = hl % G < C.N ? hl % G : 0;
             const size_t hEN = size_t(a.E) * C.N, hslot = size_t(he) * C.N + hd;
             const int hsc0 = a.ist[RI_STEP * hEN + hslot];
             const uint32_t hep = uint32_t(a.ist[RI_EPISODE * hEN + hslot] - 1);
             const uint64_t hgid = uint64_t(a.env_offset + he);
-            for (int s = int(threadIdx.x / kRaceBlock) - 1; s < C.S; s += kRaceHelpers) {
+            for (int s = hw; pre && s < C.S; s += kRaceHelpers) {
                 Real fd[3], nz[4];
                 race_substep_draws(C, a.seed, hgid, hep, hd, uint32_t(hsc0 + s), fd, nz);
                 float* dst = pre_draws + s * 7 * kRaceBlock + tl;
@@ -1070,7 +1081,11 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
 #pragma unroll
                 for (int k = 0; k < 4; ++k) dst[(3 + k) * kRaceBlock] = float(nz[k]);
             }
-            __syncthreads();
+            __syncthreads();   // 1: draws in LDS (the chain enters the sub-step loop)
+            // the track copy, off the chain's critical path: read after the loop
+            for (int k = hw; k < kTrackFields; k += kRaceHelpers)
+                trk_lds[k * kRaceBlock + tl] = float(ld(a.f, RF_GATE + k, hEN, hslot));
+            __syncthreads();   // 2: track in LDS
         }
         return;
     }
@@ -1128,7 +1143,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
         lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
     }
-    if (pre) __syncthreads();   // the helpers' draws are in LDS
+    if constexpr (PRE) __syncthreads();   // 1: the helpers' draws are in LDS
     RACE_MARK(t1);
 #ifdef ADRP_RACE_TIMING
     uint64_t acc_phys = 0;
@@ -1202,6 +1217,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         }
     }
     RACE_MARK(t2);
+    if constexpr (PRE) __syncthreads();   // 2: the helpers' track copy is in LDS
+    const TrackSrc<Real, PRE> T{a.f, EN, slot, trk_lds, tl};
     // ---- _gate_progress (471-506): rays of my current gate vs every drone of the env ----
     V3<Real> gpos[ADRP_MAX_DRONES];
     Q4<Real> gq[ADRP_MAX_DRONES];
@@ -1212,8 +1229,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     }
     const int gate0 = d.gate;
     if (C.num_gates > 0 && gate0 < C.num_gates) {
-        const Real gx = ld(a.f, RF_GATE + 4 * gate0, EN, slot), gy = ld(a.f, RF_GATE + 4 * gate0 + 1, EN, slot);
-        const Real rotg = ld(a.f, RF_GATE + 4 * gate0 + 3, EN, slot);
+        const Real gx = T(RF_GATE + 4 * gate0), gy = T(RF_GATE + 4 * gate0 + 1);
+        const Real rotg = T(RF_GATE + 4 * gate0 + 3);
         const Real h = C.gate_type[gate0] == 0 ? Real(1.0) : Real(0.525), half = Real(0.1875);
         Real sn, cs;
         sincos_(rotg, &sn, &cs);
@@ -1257,8 +1274,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     Real row0[15];
     const Shape<Real> ds = drone_shape(C, d.pos, d.q);
     uint32_t gin, oin;
-    bool crashed = track_query(C, a.f, EN, slot, ds, Real(0.45), true, Real(1e-6), gin, oin);
-    race_obs_row(C, a.f, EN, slot, d.pos, d.q, d.vel, wv, d.gate, row, active, row0, gin, oin);
+    bool crashed = track_query(C, T, ds, Real(0.45), true, Real(1e-6), gin, oin);
+    race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, active, row0, gin, oin);
     if (C.compete && active) {   // other drones' pos + rpy (653-659)
         int idx = 0;
 #pragma unroll

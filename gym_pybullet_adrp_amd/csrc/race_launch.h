@@ -5,9 +5,9 @@
 
 template <typename Real, int PH>
 static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
-    // kRaceBlock drone lanes, + kRaceHelpers helper waves per block when the sub-step draws can be
-    // pre-computed (fp32, disturbances on, S <= kRacePreS; race_kernel.h)
-    const bool helpers = sizeof(Real) == 4 && h->cfg.track.disturbances && h->S <= kRacePreS;
+    // kRaceBlock drone lanes, + kRaceHelpers helper waves per block in the fp32 kernel (the track
+    // copy into LDS, and the sub-step draws with disturbances on; race_kernel.h)
+    const bool helpers = sizeof(Real) == 4 && h->race_helpers;
     const dim3 blk(kRaceBlock * (helpers ? 1 + kRaceHelpers : 1)),
         grid((unsigned)((size_t(h->E) * G + kRaceBlock - 1) / kRaceBlock));
     auto go = [&](auto kernel) {
