@@ -1052,16 +1052,17 @@ __device__ __forceinline__ void race_substep_draws(const RaceConst<Real>& H, uin
 // sub-step's draws into LDS while wave 0 loads its state; the chain then reads 7 values per
 // sub-step instead of running two Philox4x32-10 draws and a Box-Muller pair (~200 instructions).
 // PRE: helper waves present (fp32; the host then launches kRaceBlock * (1 + kRaceHelpers)
-// threads per block).  They load the env's actual track (28 fields per lane) into LDS for the
-// post-loop queries, and with disturbances on (S <= kRacePreS) the sub-step draws.
-template <typename Real, int PH, int G, bool PRE>
+// threads per block): 2 = the sub-step draws (disturbances on, S <= kRacePreS), 1 = no draws to
+// make, so they copy the env's actual track (28 fields per lane) into LDS for the post-loop
+// queries instead (A/B: the copy pays without disturbances, but not on top of the draws).
+template <typename Real, int PH, int G, int PRE>
 __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) race_step_kernel(RaceArgs<Real> a) {
     RACE_MARK(t0);
     const RaceConst<Real>& C = *a.c;
     static_assert(!PRE || sizeof(Real) == 4, "pre-computed draws: fp32 kernel only");
-    __shared__ float pre_draws[PRE ? kRacePreS * 7 * kRaceBlock : 1];
-    __shared__ float trk_lds[PRE ? kTrackFields * kRaceBlock : 1];
-    const bool pre = PRE && C.disturbances && C.S <= kRacePreS;    // grid-uniform
+    __shared__ float pre_draws[PRE == 2 ? kRacePreS * 7 * kRaceBlock : 1];
+    __shared__ float trk_lds[PRE == 1 ? kTrackFields * kRaceBlock : 1];
+    constexpr bool pre = PRE == 2;
     const int tl = threadIdx.x % kRaceBlock;
     if (threadIdx.x >= kRaceBlock) {   // helper waves
         if constexpr (PRE) {
@@ -1072,7 +1073,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
             const int hsc0 = a.ist[RI_STEP * hEN + hslot];
             const uint32_t hep = uint32_t(a.ist[RI_EPISODE * hEN + hslot] - 1);
             const uint64_t hgid = uint64_t(a.env_offset + he);
-            for (int s = hw; pre && s < C.S; s += kRaceHelpers) {
+            for (int s = hw; pre && s < C.S; s += kRaceHelpers) {   // (PRE == 1: none)
                 Real fd[3], nz[4];
                 race_substep_draws(C, a.seed, hgid, hep, hd, uint32_t(hsc0 + s), fd, nz);
                 float* dst = pre_draws + s * 7 * kRaceBlock + tl;
@@ -1081,11 +1082,10 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
 #pragma unroll
                 for (int k = 0; k < 4; ++k) dst[(3 + k) * kRaceBlock] = float(nz[k]);
             }
-            __syncthreads();   // 1: draws in LDS (the chain enters the sub-step loop)
-            // the track copy, off the chain's critical path: read after the loop
-            for (int k = hw; k < kTrackFields; k += kRaceHelpers)
+            // PRE == 1: the track copy, off the chain's critical path (read after the loop)
+            for (int k = hw; PRE == 1 && k < kTrackFields; k += kRaceHelpers)
                 trk_lds[k * kRaceBlock + tl] = float(ld(a.f, RF_GATE + k, hEN, hslot));
-            __syncthreads();   // 2: track in LDS
+            __syncthreads();   // draws (before the chain's loop) / track (after it) in LDS
         }
         return;
     }
@@ -1143,7 +1143,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
         lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
     }
-    if constexpr (PRE) __syncthreads();   // 1: the helpers' draws are in LDS
+    if constexpr (PRE == 2) __syncthreads();   // the helpers' draws are in LDS
     RACE_MARK(t1);
 #ifdef ADRP_RACE_TIMING
     uint64_t acc_phys = 0;
@@ -1217,8 +1217,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         }
     }
     RACE_MARK(t2);
-    if constexpr (PRE) __syncthreads();   // 2: the helpers' track copy is in LDS
-    const TrackSrc<Real, PRE> T{a.f, EN, slot, trk_lds, tl};
+    if constexpr (PRE == 1) __syncthreads();   // the helpers' track copy is in LDS
+    const TrackSrc<Real, PRE == 1> T{a.f, EN, slot, trk_lds, tl};
     // ---- _gate_progress (471-506): rays of my current gate vs every drone of the env ----
     V3<Real> gpos[ADRP_MAX_DRONES];
     Q4<Real> gq[ADRP_MAX_DRONES];

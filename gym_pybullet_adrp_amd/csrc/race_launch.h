@@ -7,7 +7,8 @@ template <typename Real, int PH>
 static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
     // kRaceBlock drone lanes, + kRaceHelpers helper waves per block in the fp32 kernel (the track
     // copy into LDS, and the sub-step draws with disturbances on; race_kernel.h)
-    const bool helpers = sizeof(Real) == 4 && h->race_helpers;
+    const int helpers = sizeof(Real) != 4 || !h->race_helpers ? 0
+                        : h->cfg.track.disturbances && h->S <= kRacePreS ? 2 : 1;
     const dim3 blk(kRaceBlock * (helpers ? 1 + kRaceHelpers : 1)),
         grid((unsigned)((size_t(h->E) * G + kRaceBlock - 1) / kRaceBlock));
     auto go = [&](auto kernel) {
@@ -19,21 +20,18 @@ static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t*
         }
     };
     constexpr bool F32 = sizeof(Real) == 4;
-    if (helpers) {
+    auto by_g = [&](auto pre) {
+        constexpr int P = decltype(pre)::value;
         switch (G) {
-            case 1: go(race_step_kernel<Real, PH, 1, F32>); break;
-            case 2: go(race_step_kernel<Real, PH, 2, F32>); break;
-            case 4: go(race_step_kernel<Real, PH, 4, F32>); break;
-            default: go(race_step_kernel<Real, PH, 8, F32>); break;
+            case 1: go(race_step_kernel<Real, PH, 1, P>); break;
+            case 2: go(race_step_kernel<Real, PH, 2, P>); break;
+            case 4: go(race_step_kernel<Real, PH, 4, P>); break;
+            default: go(race_step_kernel<Real, PH, 8, P>); break;
         }
-    } else {
-        switch (G) {
-            case 1: go(race_step_kernel<Real, PH, 1, false>); break;
-            case 2: go(race_step_kernel<Real, PH, 2, false>); break;
-            case 4: go(race_step_kernel<Real, PH, 4, false>); break;
-            default: go(race_step_kernel<Real, PH, 8, false>); break;
-        }
-    }
+    };
+    if (helpers == 2) by_g(std::integral_constant<int, F32 ? 2 : 0>{});
+    else if (helpers == 1) by_g(std::integral_constant<int, F32 ? 1 : 0>{});
+    else by_g(std::integral_constant<int, 0>{});
 }
 
 template <typename Real>
