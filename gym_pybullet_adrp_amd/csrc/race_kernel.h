@@ -728,6 +728,7 @@ __device__ __forceinline__ Real point_part_dist(V3<Real> lp, V3<Real> h, Real r,
 }
 
 constexpr int kGateParts = 5, kObstParts = 2, kObstBit0 = ADRP_MAX_GATES * kGateParts;
+constexpr int kRaceMaxD = 49 + 6 * (ADRP_MAX_DRONES - 1);   // obs row floats (COMPETE, 8 drones)
 constexpr int kTrackFields = RF_WR_TARGET - RF_GATE;   // the env's actual gates (16) + obstacles (12)
 
 // Where a lane reads its env's actual gate / obstacle poses: the SoA fields in HBM, or (L) the
@@ -1062,6 +1063,9 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     static_assert(!PRE || sizeof(Real) == 4, "pre-computed draws: fp32 kernel only");
     __shared__ float pre_draws[PRE == 2 ? kRacePreS * 7 * kRaceBlock : 1];
     __shared__ float trk_lds[PRE == 1 ? kTrackFields * kRaceBlock : 1];
+    // the block's obs rows, laid out as in global memory (its envs' rows are contiguous there),
+    // so the copy-out is coalesced: direct per-lane row stores touch a line per lane per float
+    __shared__ float4 rows4[kRaceBlock * kRaceMaxD / 4];
     constexpr bool pre = PRE == 2;
     const int tl = threadIdx.x % kRaceBlock;
     if (threadIdx.x >= kRaceBlock) {   // helper waves
@@ -1270,7 +1274,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     RACE_MARK(t3);
     // ---- obs row, elimination (674-698) ----
     const V3<Real> wv = PH == ADRP_PHYS_DYN ? d.angv : d.w;
-    float* row = a.obs + slot * size_t(C.D);
+    float* const rows = reinterpret_cast<float*>(rows4);
+    float* row = rows + ((tl / G) * N + dn) * C.D;   // staged; inactive lanes write nothing
     Real row0[15];
     const Shape<Real> ds = drone_shape(C, d.pos, d.q);
     uint32_t gin, oin;
@@ -1356,23 +1361,38 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         RACE_ACC(4, t4 - t3); RACE_ACC(5, t5 - t4); RACE_ACC(6, t6 - t5); RACE_ACC(7, t6 - t0); RACE_ACC(8, 1);
     }
 #endif
-    if (!active) return;
-    if (dn == 0) {
-        a.rew[e] = reward;
-        a.term[e] = te;
-        a.trunc[e] = tr;
-    }
-    if (C.autoreset && (te || tr)) {
-        if (a.tobs) {
-            float* trow = a.tobs + slot * size_t(C.D);
-            for (int k = 0; k < C.D; ++k) trow[k] = row[k];
+    if (active) {
+        if (dn == 0) {
+            a.rew[e] = reward;
+            a.term[e] = te;
+            a.trunc[e] = tr;
         }
-        race_reset_lane(a, C, e, dn, EN, slot, episode, row);
-        return;
+        if (C.autoreset && (te || tr)) {
+            if (a.tobs) {
+                float* trow = a.tobs + slot * size_t(C.D);
+                for (int k = 0; k < C.D; ++k) trow[k] = row[k];
+            }
+            race_reset_lane(a, C, e, dn, EN, slot, episode, row);
+        } else {
+            store_drone(a, EN, slot, d, false);
+            a.ist[RI_STEP * EN + slot] = sc0 + C.S;
+            if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
+        }
     }
-    store_drone(a, EN, slot, d, false);
-    a.ist[RI_STEP * EN + slot] = sc0 + C.S;
-    if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
+    // ---- coalesced copy-out of the block's rows (envs e0 .. e0 + ne - 1) ----
+    __syncthreads();   // (the helper waves have ended)
+    const int e0 = blockIdx.x * (kRaceBlock / G);
+    const int ne = a.E - e0 < kRaceBlock / G ? a.E - e0 : kRaceBlock / G;
+    const int total = ne * N * C.D;
+    float* dst = a.obs + size_t(e0) * N * C.D;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        float4* dst4 = reinterpret_cast<float4*>(dst);
+        const int n4 = total >> 2;
+        for (int i = tl; i < n4; i += kRaceBlock) dst4[i] = rows4[i];
+        for (int i = 4 * n4 + tl; i < total; i += kRaceBlock) dst[i] = rows[i];
+    } else {
+        for (int i = tl; i < total; i += kRaceBlock) dst[i] = rows[i];
+    }
 }
 
 // reset kernel (MultiRaceAviary.reset): masked envs, one lane per drone
