@@ -743,6 +743,18 @@ struct TrackSrc {
         if constexpr (L) return Real(lds[(field - RF_GATE) * kRaceBlock + tl]);
         else return ld(f, field, EN, slot);
     }
+    // the same source for block lane l (drone slots of G-lane groups, clamped like the kernel's)
+    __device__ __forceinline__ TrackSrc lane(int l, int G, int N, int E) const {
+        TrackSrc t = *this;
+        if constexpr (L) {
+            t.tl = l;
+        } else {
+            const int gl = int(blockIdx.x) * kRaceBlock + l;
+            const int e = gl / G < E ? gl / G : E - 1, d = gl % G < N ? gl % G : 0;
+            t.slot = size_t(e) * N + d;
+        }
+        return t;
+    }
 };
 
 // placed collision shape of queue bit b (gate b / 5, part b % 5; obstacle bits from kObstBit0)
@@ -766,15 +778,16 @@ __device__ __forceinline__ Shape<Real> track_part_shape(const RaceConst<Real>& C
     return Shape<Real>{org + off, I, h, r, cyl};
 }
 
-// in-range bits (gate g -> bit g, obstacle k -> bit k) for `cut`; returns the contact
-// decision (distance < ccut) when want_contact
+// bounds pass: in-range bits decided by the bounds (gate g -> bit g, obstacle k -> bit k) for
+// `cut`, and the queue of pairs left to GJK (amb; camb_all: those queued for the contact cut)
 template <typename Real, class TS>
-__device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds, Real cut,
-                                            bool want_contact, Real ccut, uint32_t& gin, uint32_t& oin) {
+__device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds, Real cut,
+                                             bool want_contact, Real ccut, uint32_t& gin, uint32_t& oin,
+                                             uint32_t& amb, uint32_t& camb_all) {
     const Real tol = sizeof(Real) == 4 ? Real(1e-5) : Real(1e-10);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
     const V3<Real> p = ds.c;
-    uint32_t amb = 0, camb_all = 0;   // queued pairs; those queued for the contact cut
+    amb = 0; camb_all = 0;
     gin = 0; oin = 0;
 #pragma unroll
     for (int g = 0; g < ADRP_MAX_GATES; ++g) {
@@ -825,6 +838,15 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const TS& 
             camb_all |= camb << (kObstBit0 + o * kObstParts);
         }
     }
+}
+
+// in-range bits for `cut` (gin, oin); returns the contact decision (distance < ccut) when
+// want_contact.  Per lane: each lane walks its own GJK queue.
+template <typename Real, class TS>
+__device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds, Real cut,
+                                            bool want_contact, Real ccut, uint32_t& gin, uint32_t& oin) {
+    uint32_t amb, camb_all;
+    track_bounds(C, T, ds, cut, want_contact, ccut, gin, oin, amb, camb_all);
     // a contact-queued pair has its drone centre within dr of the part, so its body is
     // already in range by the upper bound: each queued pair needs exactly one of the cuts
     bool contact = false;
@@ -840,6 +862,66 @@ __device__ __forceinline__ bool track_query(const RaceConst<Real>& C, const TS& 
         }
     }
     return want_contact && contact;
+}
+
+// track_query with contacts for the whole wave (all kRaceBlock lanes of the block's single chain
+// wave reach it together): the lanes' GJK queues are pooled in LDS and dealt out one job per
+// lane per round, so a wave runs ceil(jobs / 64) GJKs instead of max-over-lanes queue length.
+// Same pairs, same GJK inputs (the owner lane's shape by cross-lane moves): same decisions.
+struct TrackJobs {
+    uint16_t job[kRaceBlock * (ADRP_MAX_GATES * kGateParts + ADRP_MAX_OBSTACLES * kObstParts)];
+    uint32_t res[kRaceBlock];
+};
+
+template <typename Real, class TS>
+__device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds,
+                                                 bool live, Real cut, Real ccut, uint32_t& gin, uint32_t& oin,
+                                                 TrackJobs& q, int tl, int G, int N, int E) {
+    uint32_t amb, camb_all;
+    track_bounds(C, T, ds, cut, true, ccut, gin, oin, amb, camb_all);
+    if (!live) amb = 0;
+    const int n = __popc(amb);
+    int incl = n;   // inclusive scan of the queue lengths
+#pragma unroll
+    for (int o = 1; o < kRaceBlock; o <<= 1) {
+        const int t = __shfl_up(incl, o, kRaceBlock);
+        if (tl >= o) incl += t;
+    }
+    const int total = __shfl(incl, kRaceBlock - 1, kRaceBlock);
+    int pos = incl - n;
+    q.res[tl] = 0;
+    for (uint32_t m = amb; m; m &= m - 1) {
+        const int b = __builtin_ctz(m);
+        q.job[pos++] = uint16_t((tl << 6) | (((camb_all >> b) & 1u) << 5) | b);
+    }
+    __syncthreads();
+    for (int base = 0; base < total; base += kRaceBlock) {
+        const int j = base + tl;
+        const int job = q.job[j < total ? j : total - 1];
+        const int L = job >> 6, b = job & 31;
+        const bool fc = (job >> 5) & 1;
+        Shape<Real> dl = ds;   // lane L's drone (h, r, cyl are the same for every drone)
+        dl.c = v3(shfl_(ds.c.x, L, kRaceBlock), shfl_(ds.c.y, L, kRaceBlock), shfl_(ds.c.z, L, kRaceBlock));
+        dl.R.a00 = shfl_(ds.R.a00, L, kRaceBlock); dl.R.a01 = shfl_(ds.R.a01, L, kRaceBlock);
+        dl.R.a02 = shfl_(ds.R.a02, L, kRaceBlock); dl.R.a10 = shfl_(ds.R.a10, L, kRaceBlock);
+        dl.R.a11 = shfl_(ds.R.a11, L, kRaceBlock); dl.R.a12 = shfl_(ds.R.a12, L, kRaceBlock);
+        dl.R.a20 = shfl_(ds.R.a20, L, kRaceBlock); dl.R.a21 = shfl_(ds.R.a21, L, kRaceBlock);
+        dl.R.a22 = shfl_(ds.R.a22, L, kRaceBlock);
+        if (j < total) {
+            const Shape<Real> s = track_part_shape(C, T.lane(L, G, N, E), b);
+            if (gjk_within(dl, s, fc ? ccut : cut)) {
+                const uint32_t bit = fc ? 1u << 8
+                                        : b < kObstBit0 ? 1u << (b / kGateParts)
+                                                        : 1u << (4 + (b - kObstBit0) / kObstParts);
+                atomicOr(&q.res[L], bit);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t r = q.res[tl];
+    gin |= r & 15u;
+    oin |= (r >> 4) & 15u;
+    return (r >> 8) & 1u;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1066,6 +1148,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     // the block's obs rows, laid out as in global memory (its envs' rows are contiguous there),
     // so the copy-out is coalesced: direct per-lane row stores touch a line per lane per float
     __shared__ float4 rows4[kRaceBlock * kRaceMaxD / 4];
+    __shared__ TrackJobs tjobs;
     constexpr bool pre = PRE == 2;
     const int tl = threadIdx.x % kRaceBlock;
     if (threadIdx.x >= kRaceBlock) {   // helper waves
@@ -1279,7 +1362,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     Real row0[15];
     const Shape<Real> ds = drone_shape(C, d.pos, d.q);
     uint32_t gin, oin;
-    bool crashed = track_query(C, T, ds, Real(0.45), true, Real(1e-6), gin, oin);
+    bool crashed = track_query_wave(C, T, ds, active, Real(0.45), Real(1e-6), gin, oin, tjobs, tl, G, N, a.E);
     race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, active, row0, gin, oin);
     if (C.compete && active) {   // other drones' pos + rpy (653-659)
         int idx = 0;
