@@ -25,7 +25,9 @@ constexpr int kRaceBlock = 64;      // drone lanes per block (one wave runs the 
 constexpr int kRaceHelpers = 3;     // helper waves per block: the sub-step disturbance draws
 constexpr int kRacePreS = 32;       // sub-steps per env.step whose draws fit the LDS table
 
-#ifdef ADRP_RACE_TIMING
+// GJK call counts (global atomics from every lane that runs a GJK: they inflate the phase times, so
+// they are a separate opt-in of the timing build)
+#if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
 #define GJK_STAT(n) do { atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
         atomicMax(&g_race_phase[19], (unsigned long long)(n)); } while (0)
 #else

@@ -315,3 +315,27 @@ def test_masked_reset():
     fo, io = orc.get_state()
     np.testing.assert_array_equal(ig.cpu().numpy(), io)
     env.close()
+
+
+@pytest.mark.parametrize("E,N,level,physics,mode", [(300, 2, "level0", Physics.PYB, RaceMode.COMPARE),
+                                                    (333, 4, "level3", Physics.PYB_DW, RaceMode.COMPETE),
+                                                    (37, 3, "level2", Physics.PYB, RaceMode.COMPETE)])
+def test_helper_waves_bit_identical(monkeypatch, E, N, level, physics, mode):
+    """the fp32 kernel's helper waves (LDS track copy / pre-drawn disturbances) change who computes,
+    not what: 40 auto-reset env.steps with and without them (ADRP_RACE_HELPERS=0) agree bit for bit
+    (measured; the variants' code generation happens to contract identically)"""
+    outs = []
+    for helpers in ("1", "0"):
+        monkeypatch.setenv("ADRP_RACE_HELPERS", helpers)
+        env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=3,
+                              autoreset=True, reward="wrapper")
+        obs, _ = env.reset()
+        act = torch.from_numpy(targets(np.random.default_rng(4), obs.cpu().numpy(), E, N)).to(env.device)
+        seq = []
+        for _ in range(40):
+            obs, rew, te, tr, _ = env.step(act)
+            seq.append(torch.cat([obs.reshape(E, -1), rew.reshape(E, 1).float(), te.reshape(E, 1).float(),
+                                  tr.reshape(E, 1).float()], 1).cpu())
+        outs.append(torch.stack(seq))
+        env.close()
+    assert torch.equal(outs[0], outs[1])
