@@ -10,6 +10,18 @@
 
 namespace adrp {
 
+// obs copy-out store (a row block written once per step, read by the next launch or the host);
+// ADRP_NT_STORES: non-temporal (A/B: no change at hover E = 4096 or race config 4, so off)
+__device__ __forceinline__ void store_out(float4* p, float4 v) {
+#ifdef ADRP_NT_STORES
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(p));
+#else
+    *p = v;
+#endif
+}
+
 // phase timing (build with -DADRP_RACE_TIMING; tools/race_phases.py, tools/hover_phases.py):
 // lane 0 of every wave adds its s_memtime deltas per phase of the step kernel
 #ifdef ADRP_RACE_TIMING

@@ -599,7 +599,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
             // second half of the block's coalesced copy-out
             float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
 #pragma unroll
-            for (int k = kRowF4 / 2; k < kRowF4; ++k) dst[tl + kStepBlock * k] = rows[tl + kStepBlock * k];
+            for (int k = kRowF4 / 2; k < kRowF4; ++k) store_out(dst + tl + kStepBlock * k, rows[tl + kStepBlock * k]);
             return;
         }
     }
@@ -796,7 +796,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
         constexpr int KC = HELP ? kRowF4 / 2 : kRowF4;   // HELP: the helper copies the other half
 #pragma unroll
-        for (int k = 0; k < KC; ++k) dst[threadIdx.x + kStepBlock * k] = rows[threadIdx.x + kStepBlock * k];
+        for (int k = 0; k < KC; ++k) store_out(dst + threadIdx.x + kStepBlock * k, rows[threadIdx.x + kStepBlock * k]);
     } else {
 #pragma unroll
         for (int p = 0; p < B; ++p) {

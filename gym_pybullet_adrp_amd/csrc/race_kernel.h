@@ -1473,7 +1473,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
         float4* dst4 = reinterpret_cast<float4*>(dst);
         const int n4 = total >> 2;
-        for (int i = tl; i < n4; i += kRaceBlock) dst4[i] = rows4[i];
+        for (int i = tl; i < n4; i += kRaceBlock) store_out(dst4 + i, rows4[i]);
         for (int i = 4 * n4 + tl; i < total; i += kRaceBlock) dst[i] = rows[i];
     } else {
         for (int i = tl; i < total; i += kRaceBlock) dst[i] = rows[i];
