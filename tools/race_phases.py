@@ -1,12 +1,15 @@
 """Per-phase cost of race_step_kernel (needs the timing build: make -C gym_pybullet_adrp_amd/csrc timing).
 
 usage: ADRP_LIB=gym_pybullet_adrp_amd/libadrp_timing.so python tools/race_phases.py [LEVEL DRONES PHYSICS MODE E]
+       RACE_POLICY=example|twogates: setpoints from the on-device PPO actor (closed loop) instead of
+       fixed random targets
 Prints, per configuration, the s_memtime cycles per wave spent in each phase (mean over
 waves, and the slowest wave per launch averaged over launches) and the kernel time from
 dispatch events.
 """
 import ctypes
 import json
+import os
 import sys
 
 import numpy as np
@@ -36,8 +39,20 @@ for level, n, phys, mode, E in CONFIGS:
     tgt = obs0[..., :3].unsqueeze(0) + off
     tgt[..., 2] = tgt[..., 2].clamp(0.2, 1.5)
     acts = torch.cat([tgt, torch.zeros((16, E, n, 1), device=env.device)], -1).contiguous()
+    pol = os.environ.get("RACE_POLICY")
+    if pol:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)) + "/..")
+        from bench import make_policy
+        policy = make_policy(pol, env.device.index or 0, mode)
+        pact = torch.empty((E, n, 4), device=env.device)
+
+        def step(_a):
+            policy.act(env._obs, out=pact)
+            return env.step(pact)
+    else:
+        step = env.step
     for k in range(100):
-        env.step(acts[k % 16])
+        step(acts[k % 16])
     torch.cuda.synchronize()
     lib.adrp_race_phase_read(buf, 1)
     nk = 100
@@ -46,7 +61,7 @@ for level, n, phys, mode, E in CONFIGS:
     gjk_max = 0
     env.h.profile_begin(nk)
     for k in range(nk):
-        env.step(acts[k % 16])
+        step(acts[k % 16])
         torch.cuda.synchronize()
         lib.adrp_race_phase_read(buf, 1)
         v = np.array(list(buf), dtype=np.float64)
