@@ -1162,14 +1162,20 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
             const int hsc0 = a.ist[RI_STEP * hEN + hslot];
             const uint32_t hep = uint32_t(a.ist[RI_EPISODE * hEN + hslot] - 1);
             const uint64_t hgid = uint64_t(a.env_offset + he);
-            for (int s = hw; pre && s < C.S; s += kRaceHelpers) {   // (PRE == 1: none)
-                Real fd[3], nz[4];
-                race_substep_draws(C, a.seed, hgid, hep, hd, uint32_t(hsc0 + s), fd, nz);
-                float* dst = pre_draws + s * 7 * kRaceBlock + tl;
+            // PRE == 2: sub-steps [0, S/2) before the chain's loop starts, the rest by its middle
+            const int half = C.S / 2;
+            for (int part = 0; pre && part < 2; ++part) {
+                for (int s = hw; s < C.S; s += kRaceHelpers) {
+                    if ((s < half) != (part == 0)) continue;
+                    Real fd[3], nz[4];
+                    race_substep_draws(C, a.seed, hgid, hep, hd, uint32_t(hsc0 + s), fd, nz);
+                    float* dst = pre_draws + s * 7 * kRaceBlock + tl;
 #pragma unroll
-                for (int k = 0; k < 3; ++k) dst[k * kRaceBlock] = float(fd[k]);
+                    for (int k = 0; k < 3; ++k) dst[k * kRaceBlock] = float(fd[k]);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) dst[(3 + k) * kRaceBlock] = float(nz[k]);
+                    for (int k = 0; k < 4; ++k) dst[(3 + k) * kRaceBlock] = float(nz[k]);
+                }
+                if (part == 0) __syncthreads();   // first half in LDS
             }
             // PRE == 1: the track copy, off the chain's critical path (read after the loop)
             for (int k = hw; PRE == 1 && k < kTrackFields; k += kRaceHelpers)
@@ -1232,7 +1238,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
         lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
     }
-    if constexpr (PRE == 2) __syncthreads();   // the helpers' draws are in LDS
+    if constexpr (PRE == 2) __syncthreads();   // the helpers' first half of the draws is in LDS
     RACE_MARK(t1);
 #ifdef ADRP_RACE_TIMING
     uint64_t acc_phys = 0;
@@ -1241,6 +1247,9 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
 #ifdef ADRP_RACE_TIMING
         RACE_MARK(ta);
 #endif
+        if constexpr (PRE == 2) {
+            if (s == H.S / 2) __syncthreads();   // the helpers' second half of the draws
+        }
         const uint32_t idx = uint32_t(sc0 + s);
         if (PH != ADRP_PHYS_PYB) d.kpos = d.pos;          // KIN_PHYSICS read-back
         if constexpr (PH == ADRP_PHYS_DYN) {
