@@ -1,23 +1,35 @@
-"""Benchmark: HoverAviary env.step throughput (BASELINE.json configs[1]) on N MI355X.
+"""Benchmark: vectorised gym-pybullet-adrp env.step throughput on N MI355X (BASELINE.json).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One "step" = one env.step() of every env on every GPU: per GPU one fused launch over
-4096 envs x 8 PYB sub-steps (240 Hz physics, 30 Hz control) incl. obs/reward/
-termination and auto-reset.  Envs are sharded across ranks (weak scaling, no collective
-on the step path).  Inputs are resident in HBM before the timed region: per-env random
-airborne initial states (device RNG) and a pre-generated buffer of U[-1,1] actions.
+`value` is BASELINE.json configs[1] (HoverAviary, 4096 envs x 1 drone per GPU, PYB, 240/30 Hz =
+8 sub-steps, RPM actions, auto-reset): one "step" = one env.step() of every env on every GPU,
+one fused HIP launch per GPU, envs sharded across ranks (weak scaling, no collective on the
+step path).  Inputs are resident in HBM before the timed region.  `--gpus N` without a launcher
+starts N ranks itself (a child `torch.distributed.run`), before anything touches the GPU.
 
-Prints ONE JSON line on rank 0 with the roofline of the step kernel (per-launch HIP
-events on the launching stream) and a CPU baseline (the float64 oracle, one host core,
-bounded sample) timed in the same run.
+The same JSON line carries sub-records (`configs`), each timed the same way:
+  config5      every N: MultiRaceAviary COMPETE level3, 4 drones x 4096 envs per GPU, PYB_DW,
+               disturbances on (at N = 1 this is configs[3]); kernel-only and step + RCCL
+               all-gather of the packed obs/reward/flags (N > 1)
+  config3      N = 1: MultiRaceAviary COMPARE level0, 2 drones x 2048 envs, PYB
+  config3_policy  N = 1: config 3 driven by the reference's PPO actor on the device
+  config2_f64  N = 1: the `value` workload with the float64 kernel (reference precision)
+  config1      N = 1: one HoverAviary env (E = 1), per-step latency, GPU and CPU oracle
+Rooflines: the hover kernel is HBM-bound (bytes per launch / kernel time vs 8 TB/s); the race
+kernel is VALU/issue-bound (PMC-counted flops per launch / kernel time vs the fp32 vector peak;
+HBM fraction kept as information).  Kernel times are HIP events attached to each step kernel's
+own dispatch on its launching stream.  CPU baseline: the float64 oracle (test infrastructure)
+on the host, one thread and all of the job's cores (OpenMP over envs), bounded samples.
 """
 import argparse
+import functools
 import json
 import os
-import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,8 +40,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-ENVS_PER_GPU = 4096         # BASELINE.json configs[1]
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+VALU_F32_PEAK_TFLOPS = 157.3    # MI355X fp32 vector (FMA = 2 flops), MI355X_MICROARCH.md
+VALU_F64_PEAK_TFLOPS = 78.6
+ENVS_PER_GPU = 4096             # BASELINE.json configs[1]
+METRIC = "env-steps/sec (N parallel drones) at 1/2/4/8 MI355X; % HBM roofline"
 
 
 def parse():
@@ -41,150 +56,129 @@ def parse():
     p.add_argument("--physics", default="PYB")
     p.add_argument("--precision", default="fp32")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU-baseline leg")
     p.add_argument("--no-allgather", action="store_true", help="N>1: skip the obs all-gather variant")
+    p.add_argument("--no-configs", action="store_true", help="only the main line (no config sub-records)")
+    p.add_argument("--race-steps", type=int, default=200, help="timed steps of each race sub-record")
     p.add_argument("--task", default="hover", choices=["hover", "race"],
-                   help="hover = BASELINE configs[1] (default); race = configs[2]/[3] (MultiRaceAviary)")
-    p.add_argument("--level", default="level0", help="race: track preset (level0 = config 3, level3 = config 4)")
-    p.add_argument("--drones", type=int, default=2, help="race: drones per env")
+                   help="main line: hover = BASELINE configs[1] (default); race = configs[2]/[3]")
+    p.add_argument("--level", default="level0", help="race main line: track preset")
+    p.add_argument("--drones", type=int, default=2, help="race main line: drones per env")
     p.add_argument("--racemode", default="COMPARE", choices=["COMPARE", "COMPETE"])
     p.add_argument("--no-sweep", action="store_true", help="hover: skip the env-count roofline sweep")
     p.add_argument("--policy", default=None,
-                   help="race: closed loop with the on-device PPO actor: 'example' / 'twogates' (the reference's "
-                        "user_controller zips, weights from tests/golden/policy_golden.npz) or a SB3 zip path")
+                   help="race main line: closed loop with the on-device PPO actor: 'example' / 'twogates' "
+                        "(weights from tests/golden/policy_golden.npz) or a SB3 zip path")
+    p.add_argument("--launch-check", action="store_true",
+                   help="CPU-only check of the rank launch: every rank joins a gloo group, rank 0 prints the "
+                        "record of the world it saw, no GPU work")
     return p.parse_args()
 
 
-def roofline_sweep(make, sizes, launches=30):
-    """The same step kernel at larger env counts (one GPU): where the launch leaves the latency-bound
-    regime of E = 4096 and becomes HBM-bound.  Kernel time from dispatch-attached events."""
-    out = []
-    for n in sizes:
-        env = make(num_envs=n, env_offset=0)
-        env.reset()
-        a = torch.rand((4, n, 1, 4), device=env.device) * 2 - 1
-        for k in range(5):
-            env.step(a[k % 4])
-        torch.cuda.synchronize()
-        env.h.profile_begin(launches)
-        for k in range(launches):
-            env.step(a[k % 4])
-        us = float(np.mean(env.h.profile_end(launches))) * 1e3
-        gbps = env.step_bytes() / (us * 1e-6) / 1e9
-        out.append({"envs": n, "kernel_us": us, "env_steps_per_s": n / (us * 1e-6), "achieved_GBps": gbps,
-                    "frac": gbps / HBM_PEAK_GBPS})
-        env.close()
-        del a
-    return out
+# ----------------------------------------------------------------------------------------------
+# rank launch
+# ----------------------------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def make_policy(spec, device, racemode):
-    from gym_pybullet_adrp_amd.policy import ACTOR_KEYS, DevicePolicy
-    mode = "absolute" if spec == "twogates" else "relative"     # RLControllerTwoGates / RLController
-    if spec in ("example", "twogates"):
-        g = np.load(os.path.join(ROOT, "tests", "golden", "policy_golden.npz"))
-        name = "example_RL_model" if spec == "example" else "twogates"
-        w = {k: g[f"{name}_w{i}"] for i, k in enumerate(ACTOR_KEYS)}
-        return DevicePolicy(w, "relu" if bool(g[f"{name}_relu"]) else "tanh", device, mode)
-    return DevicePolicy.from_zip(spec, device, mode)
+def launch_ranks(n):
+    """`--gpus N` without a launcher: run this script under torch.distributed.run as a child and
+    return its exit code (no exec: this process never touches the GPU)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
-def cpu_baseline(cfg, seconds):
-    """float64 oracle (oracle/oracle.c), single host thread, bounded sample of the same
-    workload: 4096 envs stepped until ~`seconds` of CPU time."""
+def launch_check(args, world, rank):
+    dist.init_process_group("gloo")
+    seen = dist.get_world_size()
+    t = torch.tensor([rank, 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_arg": args.gpus, "world_seen": seen,
+                          "ranks_reported": int(t[1]), "rank_sum": int(t[0])}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------------
+# CPU side
+# ----------------------------------------------------------------------------------------------
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    return {"nproc": os.cpu_count(), "affinity": avail, "threads_allowed": min(share, avail), "model": model}
+
+
+def _oracle_leg(cfg, E, acts_fn, seconds, threads):
     from oracle import oracle as O
     c = cfg.copy()
-    race = c.task == 1
-    c.num_envs = 256 if race else ENVS_PER_GPU
-    c.env_offset = 0
-    orc = O.Oracle(c)
-    obs0 = orc.reset()
+    c.num_envs, c.env_offset = E, 0
+    O.set_threads(threads)
+    try:
+        orc = O.Oracle(c)
+        obs0 = orc.reset()
+        acts = acts_fn(obs0, E)
+        orc.step(acts[0])                     # warm
+        steps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            orc.step(acts[steps % len(acts)])
+            steps += 1
+        dt = time.perf_counter() - t0
+    finally:
+        O.set_threads(1)
+    return E * steps / dt, steps, dt
+
+
+def _hover_acts(obs0, E):
+    return np.random.default_rng(1).uniform(-1, 1, (8, E, 1, 4)).astype(np.float32)
+
+
+def _race_acts(obs0, E):
     rng = np.random.default_rng(1)
-    if race:
-        t = obs0[None, ..., :3] + rng.uniform(-0.3, 0.3, (8,) + obs0.shape[:2] + (3,))
-        t[..., 2] = np.clip(t[..., 2], 0.2, 1.5)
-        acts = np.concatenate([t, np.zeros(t.shape[:-1] + (1,))], -1).astype(np.float32)
-    else:
-        acts = rng.uniform(-1, 1, (8, c.num_envs, 1, 4)).astype(np.float32)
-    orc.step(acts[0])                     # warm
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        orc.step(acts[steps % 8])
-        steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": c.num_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{c.num_envs} envs x {steps} env.steps (float64 oracle, {dt:.1f} s, 1 thread, "
-                      f"{platform.processor() or platform.machine()})"}
+    t = obs0[None, ..., :3] + rng.uniform(-0.3, 0.3, (8,) + obs0.shape[:2] + (3,))
+    t[..., 2] = np.clip(t[..., 2], 0.2, 1.5)
+    return np.concatenate([t, np.zeros(t.shape[:-1] + (1,))], -1).astype(np.float32)
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    import functools
-    from gym_pybullet_adrp_amd import _lib
-    from gym_pybullet_adrp_amd.envs.hover import HoverAviary
-    from gym_pybullet_adrp_amd.utils.enums import Physics
+def cpu_baseline(cfg, seconds, race=False):
+    """The float64 oracle (oracle/oracle.c, test infrastructure) on the host: one thread and all of
+    the job's cores (OpenMP over envs; results bit-identical, tests/test_oracle_threads.py)."""
+    info = cpu_info()
+    E = 256 if race else ENVS_PER_GPU
+    fn = _race_acts if race else _hover_acts
+    v1, n1, d1 = _oracle_leg(cfg, E, fn, seconds, 1)
+    thr = info["threads_allowed"]
+    vN, nN, dN = _oracle_leg(cfg, max(E, 8 * thr), fn, seconds, thr)
+    return {"value": vN, "unit": "env-steps/s", "cores": thr, "kind": "port",
+            "sample": f"{max(E, 8 * thr)} envs x {nN} env.steps, float64 oracle, {dN:.1f} s, OpenMP {thr} threads "
+                      f"over envs; {info['model']}",
+            "one_core": {"value": v1, "cores": 1, "sample": f"{E} envs x {n1} env.steps, {d1:.1f} s, 1 thread"},
+            "host": info}
 
-    E = args.envs
-    if args.task == "race":
-        from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary
-        from gym_pybullet_adrp_amd.utils.enums import RaceMode
-        make = functools.partial(MultiRaceAviary, args.level, num_drones=args.drones, physics=Physics[args.physics],
-                                 racemode=RaceMode[args.racemode], device=local, precision=args.precision, seed=2024)
-    else:
-        make = functools.partial(HoverAviary, physics=Physics[args.physics], device=local, precision=args.precision,
-                                 seed=2024, initial_xyzs=[0, 0, 1.0],
-                                 init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1})
-    sharded = None
-    if world > 1:
-        from gym_pybullet_adrp_amd.sharding import ShardedAviary
-        sharded = ShardedAviary(E * world, make)     # rank r owns global envs [r*E, (r+1)*E)
-        env = sharded.env
-    else:
-        env = make(num_envs=E, env_offset=0)
-    dev = env.device
-    obs0, _ = env.reset()
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1 + rank)
-    nbuf = 64
-    if args.task == "race":
-        # SURVEY §8(d) config 3: FULLSTATE targets = start + U(+-0.3) m, z clipped to [0.2, 1.5], yaw 0
-        # (re-drawn per buffer slot)
-        N = args.drones
-        off = (torch.rand((nbuf, E, N, 3), generator=gen, device=dev) * 0.6 - 0.3)
-        tgt = obs0[..., :3].unsqueeze(0) + off
-        tgt[..., 2] = tgt[..., 2].clamp(0.2, 1.5)
-        acts = torch.cat([tgt, torch.zeros((nbuf, E, N, 1), device=dev)], -1).contiguous()
-    else:
-        acts = (torch.rand((nbuf, E, 1, 4), generator=gen, device=dev) * 2 - 1).contiguous()
-    policy = None
-    if args.policy:
-        if args.task != "race":
-            raise SystemExit("--policy drives MultiRaceAviary (FULLSTATE setpoints)")
-        policy = make_policy(args.policy, local, args.racemode)
-        pact = torch.empty((E, args.drones, 4), device=dev)
 
-        class _Loop:   # one "step" = policy forward on the current obs + env.step on its setpoints
-            def step(self, _a):
-                policy.act(env._obs, out=pact)
-                return env.step(pact)
-        stepper = _Loop()
-    else:
-        stepper = env
-    for k in range(args.warmup):
+# ----------------------------------------------------------------------------------------------
+# GPU timing
+# ----------------------------------------------------------------------------------------------
+def time_graph(stepper, acts, K, W, world, dev):
+    """W eager warm-up steps, then exactly K steps replayed from captured HIP graphs, bracketed by
+    barrier + synchronize; returns the max over ranks of the timed region (s) and the graph size."""
+    nbuf = acts.shape[0]
+    for k in range(W):
         stepper.step(acts[k % nbuf])
     torch.cuda.synchronize()
-
-    # ---- timed region: exactly K env.steps, replayed from a captured HIP graph ----
-    K = args.steps
     G = max(g for g in range(1, min(K, 256) + 1) if K % g == 0)   # steps per graph, G | K
     side = torch.cuda.Stream(device=dev)
     side.wait_stream(torch.cuda.current_stream(dev))
@@ -207,22 +201,150 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    del graph
+    return float(el.item()), G
 
-    # ---- kernel duration: HIP start/stop events attached to each step kernel's own
-    # dispatch (hipExtLaunchKernelGGL inside libadrp) on the launching stream, over nk launches
-    nk = min(K, 512)
+
+def kernel_times(env, acts, n):
+    """per-launch durations (ms) of the step kernel: start/stop events attached to its own
+    dispatch (hipExtLaunchKernelGGL in libadrp) on the launching stream"""
     torch.cuda.synchronize()
-    env.h.profile_begin(nk)
-    for k in range(nk):
-        env.step(acts[k % nbuf])
-    kern_ms = env.h.profile_end(nk)
-    kern_avg_s = float(np.mean(kern_ms)) / 1e3
-    policy_rec = None
-    if policy is not None:   # policy launches are on torch's current stream: torch events see them
+    env.h.profile_begin(n)
+    for k in range(n):
+        env.step(acts[k % acts.shape[0]])
+    return np.asarray(env.h.profile_end(n))
+
+
+def pmc_record(name, key):
+    """a per-launch counter summary committed under profiles/ (tools/pmc_summary.py)"""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        rec = json.load(fh)
+    return rec.get(key)
+
+
+def hover_make(precision, physics, dev, **kw):
+    from gym_pybullet_adrp_amd.envs.hover import HoverAviary
+    from gym_pybullet_adrp_amd.utils.enums import Physics
+    return functools.partial(HoverAviary, physics=Physics[physics], device=dev, precision=precision, seed=2024,
+                             initial_xyzs=[0, 0, 1.0], init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1},
+                             **kw)
+
+
+def race_make(level, drones, physics, racemode, precision, dev):
+    from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary
+    from gym_pybullet_adrp_amd.utils.enums import Physics, RaceMode
+    return functools.partial(MultiRaceAviary, level, num_drones=drones, physics=Physics[physics],
+                             racemode=RaceMode[racemode], device=dev, precision=precision, seed=2024)
+
+
+def hover_actions(E, dev, seed, nbuf=64):
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    return (torch.rand((nbuf, E, 1, 4), generator=gen, device=dev) * 2 - 1).contiguous()
+
+
+def race_actions(obs0, dev, seed, nbuf=64):
+    """FULLSTATE targets = start + U(+-0.3) m, z clipped to [0.2, 1.5], yaw 0"""
+    E, N = obs0.shape[:2]
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    off = torch.rand((nbuf, E, N, 3), generator=gen, device=dev) * 0.6 - 0.3
+    tgt = obs0[..., :3].unsqueeze(0) + off
+    tgt[..., 2] = tgt[..., 2].clamp(0.2, 1.5)
+    return torch.cat([tgt, torch.zeros((nbuf, E, N, 1), device=dev)], -1).contiguous()
+
+
+def make_policy(spec, device):
+    from gym_pybullet_adrp_amd.policy import ACTOR_KEYS, DevicePolicy
+    mode = "absolute" if spec == "twogates" else "relative"     # RLControllerTwoGates / RLController
+    if spec in ("example", "twogates"):
+        g = np.load(os.path.join(ROOT, "tests", "golden", "policy_golden.npz"))
+        name = "example_RL_model" if spec == "example" else "twogates"
+        w = {k: g[f"{name}_w{i}"] for i, k in enumerate(ACTOR_KEYS)}
+        return DevicePolicy(w, "relu" if bool(g[f"{name}_relu"]) else "tanh", device, mode)
+    return DevicePolicy.from_zip(spec, device, mode)
+
+
+def hbm_roofline(bytes_per_launch, kern_ms, traffic_key):
+    avg_s = float(np.mean(kern_ms)) / 1e3
+    ach = bytes_per_launch / avg_s / 1e9
+    pmc = pmc_record("pmc_traffic.json", traffic_key)
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
+            "traffic": None if pmc is None else pmc["hbm_bytes_per_launch"],
+            "traffic_source": None if pmc is None else f"profiles/pmc_traffic.json[{traffic_key}]",
+            "bytes_per_launch": bytes_per_launch, "kernel_us": avg_s * 1e6,
+            "kernel_us_median": float(np.median(kern_ms)) * 1e3, "timed_launches": int(len(kern_ms))}
+
+
+def valu_roofline(env, kern_ms, key, precision):
+    """race kernel: PMC-counted flops per launch (profiles/pmc_valu.json, tools/pmc_summary.py valu mode:
+    64 x (ADD + MUL + TRANS + 2 FMA) VALU instruction counts) over the kernel time, vs the vector peak.
+    HBM fraction kept alongside for information."""
+    avg_s = float(np.mean(kern_ms)) / 1e3
+    hbm = hbm_roofline(env.step_bytes(), kern_ms, key)
+    pmc = pmc_record("pmc_valu.json", key)
+    peak = VALU_F32_PEAK_TFLOPS if precision == "fp32" else VALU_F64_PEAK_TFLOPS
+    drones = env.num_envs * env.NUM_DRONES
+    rec = {"bound": "valu", "achieved": None, "peak": peak, "unit": "TFLOP/s", "frac": None,
+           "traffic": hbm["traffic"], "kernel_us": hbm["kernel_us"], "kernel_us_median": hbm["kernel_us_median"],
+           "timed_launches": hbm["timed_launches"],
+           "hbm": {"achieved_GBps": hbm["achieved"], "frac": hbm["frac"], "bytes_per_launch": hbm["bytes_per_launch"]}}
+    if pmc is not None:
+        flops = pmc["flops_per_launch"]
+        rec.update({"achieved": flops / avg_s / 1e12, "frac": flops / avg_s / 1e12 / peak,
+                    "flops_per_launch": flops, "flops_per_drone_step": flops / drones,
+                    "valu_busy": pmc.get("valu_busy"), "source": f"profiles/pmc_valu.json[{key}]"})
+    return rec
+
+
+def race_key(level, drones, physics, precision, E):
+    return f"race_{level}_{drones}_{physics}_{precision}_{E}"
+
+
+# ----------------------------------------------------------------------------------------------
+# workloads
+# ----------------------------------------------------------------------------------------------
+def bench_race(level, drones, physics, racemode, precision, E, K, W, world, rank, dev, seed,
+               sharded_gather=False, policy_spec=None):
+    from gym_pybullet_adrp_amd import _lib
+    make = race_make(level, drones, physics, racemode, precision, dev)
+    sharded = None
+    if world > 1:
+        from gym_pybullet_adrp_amd.sharding import ShardedAviary
+        sharded = ShardedAviary(E * world, make)
+        env = sharded.env
+    else:
+        env = make(num_envs=E, env_offset=0)
+    obs0, _ = env.reset()
+    acts = race_actions(obs0.clone(), dev, seed + rank)
+    policy = None
+    stepper = env
+    if policy_spec:
+        policy = make_policy(policy_spec, dev)
+        pact = torch.empty((E, drones, 4), device=dev)
+
+        class _Loop:   # one "step" = policy forward on the current obs + env.step on its setpoints
+            def step(self, _a):
+                policy.act(env._obs, out=pact)
+                return env.step(pact)
+        stepper = _Loop()
+    elapsed, G = time_graph(stepper, acts, K, W, world, dev)
+    kern = kernel_times(env, acts, min(K, 512))
+    key = race_key(level, drones, physics, precision, E)
+    rec = {"workload": f"MultiRaceAviary {racemode} {level}, {drones} drones x {E} envs per GPU, Physics.{physics} "
+                       f"500/25 Hz (20 sub-steps, Mellinger 500 Hz), {precision}",
+           "value": E * world * K / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
+           "ms_per_step": elapsed / K * 1e3, "drone_steps_per_s": E * world * K / elapsed * drones,
+           "kernel": _lib.kernel_name(env.cfg),
+           "roofline": valu_roofline(env, kern, key, precision),
+           "timed_region": f"{K // G} replays of a {G}-step HIP graph"}
+    if policy is not None:
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(200)]
         for a, b in ev:
             a.record()
@@ -230,106 +352,227 @@ def main():
             b.record()
         torch.cuda.synchronize()
         pol_us = float(np.mean([a.elapsed_time(b) for a, b in ev])) * 1e3
-        rows = E * args.drones
+        rows = E * drones
         flops = 2 * rows * (policy.in_dim * policy.h1 + policy.h1 * policy.h2 + policy.h2 * 4)
-        policy_rec = {"weights": args.policy, "arch": f"{policy.in_dim}-{policy.h1}-{policy.h2}-4",
-                      "kernel_us": pol_us, "rows": rows, "flops": flops,
-                      "mfma_f32": {"achieved_tflops": flops / pol_us / 1e6, "unit": "TFLOP/s"},
-                      "bytes": rows * (env.h.D + 4) * 4,
-                      "note": "event pairs around each policy launch on the current stream"}
+        rec["workload"] += f"; closed loop: on-device PPO actor ({policy_spec}) each step"
+        rec["policy"] = {"weights": policy_spec, "arch": f"{policy.in_dim}-{policy.h1}-{policy.h2}-4",
+                         "kernel_us": pol_us, "rows": rows, "flops": flops,
+                         "mfma_f32": {"achieved_tflops": flops / pol_us / 1e6, "unit": "TFLOP/s"},
+                         "note": "event pairs around each policy launch on the current stream"}
+        policy.close()
+    if sharded is not None:
+        rec["world"] = dist.get_world_size()
+        rec["backend"] = dist.get_backend()
+        if sharded_gather:
+            ng = min(K, 300)
+            for k in range(10):
+                sharded.gather(*env.step(acts[k % acts.shape[0]])[:4])
+            torch.cuda.synchronize()
+            dist.barrier()
+            tg0 = time.perf_counter()
+            for k in range(ng):
+                sharded.gather(*env.step(acts[k % acts.shape[0]])[:4])
+            torch.cuda.synchronize()
+            tg = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64, device=dev)
+            dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+            tg = float(tg.item())
+            rec["with_obs_allgather"] = {
+                "value": E * world * ng / tg, "unit": "env-steps/s", "ms_per_step": tg / ng * 1e3, "steps": ng,
+                "collective": "all_gather_into_tensor (RCCL over xGMI) of packed fp32 obs+reward+flags, eager",
+                "bytes_per_rank_per_step": E * (drones * env.h.D + 3) * 4}
+    env.close()
+    return rec
 
-    # ---- eager (no graph) end-to-end rate, for reference ----
+
+def bench_hover(args, precision, E, K, W, world, rank, dev, sweep=False, sharded_gather=False):
+    from gym_pybullet_adrp_amd import _lib
+    make = hover_make(precision, args.physics, dev)
+    sharded = None
+    if world > 1:
+        from gym_pybullet_adrp_amd.sharding import ShardedAviary
+        sharded = ShardedAviary(E * world, make)     # rank r owns global envs [r*E, (r+1)*E)
+        env = sharded.env
+    else:
+        env = make(num_envs=E, env_offset=0)
+    env.reset()
+    acts = hover_actions(E, dev, 1 + rank)
+    elapsed, G = time_graph(env, acts, K, W, world, dev)
+    kern = kernel_times(env, acts, min(K, 512))
+    # eager (no graph) end-to-end rate, for reference
     torch.cuda.synchronize()
-    te0 = time.perf_counter()
     ne = min(K, 1000)
+    te0 = time.perf_counter()
     for k in range(ne):
-        env.step(acts[k % nbuf])
+        env.step(acts[k % acts.shape[0]])
     torch.cuda.synchronize()
-    eager = {"env_steps_per_s_per_gpu": E * ne / (time.perf_counter() - te0),
-             "ms_per_step": (time.perf_counter() - te0) / ne * 1e3}
-
-    # ---- config 5 variant (N > 1): every step followed by the RCCL all-gather that
-    # reassembles obs/reward/flags for a learner (eager; not part of `value`) ----
-    allgather = None
-    if sharded is not None and not args.no_allgather:
+    te = time.perf_counter() - te0
+    rec = {"value": E * world * K / elapsed, "ms_per_step": elapsed / K * 1e3,
+           "kernel": _lib.kernel_name(env.cfg),
+           "roofline": hbm_roofline(env.step_bytes(), kern, f"{args.physics}_{precision}_{E}"),
+           "timing": {"timed_region": f"{K // G} replays of a {G}-step HIP graph (one fused launch per env.step)",
+                      "eager": {"env_steps_per_s_per_gpu": E * ne / te, "ms_per_step": te / ne * 1e3}}}
+    if sharded is not None and sharded_gather:
         ng = min(K, 500)
         for k in range(10):
-            sharded.gather(*env.step(acts[k % nbuf])[:4])
+            sharded.gather(*env.step(acts[k % acts.shape[0]])[:4])
         torch.cuda.synchronize()
         dist.barrier()
         tg0 = time.perf_counter()
         for k in range(ng):
-            sharded.gather(*env.step(acts[k % nbuf])[:4])
+            sharded.gather(*env.step(acts[k % acts.shape[0]])[:4])
         torch.cuda.synchronize()
         tg = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64, device=dev)
         dist.all_reduce(tg, op=dist.ReduceOp.MAX)
         tg = float(tg.item())
-        allgather = {"value": E * world * ng / tg, "unit": "env-steps/s", "ms_per_step": tg / ng * 1e3,
-                     "steps": ng, "collective": "all_gather_into_tensor (RCCL) of packed fp32 obs+reward+flags",
-                     "bytes_per_rank_per_step": E * (env.h.D + 3) * 4}
+        rec["with_obs_allgather"] = {"value": E * world * ng / tg, "unit": "env-steps/s",
+                                     "ms_per_step": tg / ng * 1e3, "steps": ng,
+                                     "collective": "all_gather_into_tensor (RCCL) of packed fp32 obs+reward+flags",
+                                     "bytes_per_rank_per_step": E * (env.h.D + 3) * 4}
+    if sweep:
+        rec["roofline"]["sweep"] = roofline_sweep(make, [65536, 262144, 1048576])
+    cfg = env.cfg.copy()
+    env.close()
+    return rec, cfg
 
-    bytes_per_launch = env.step_bytes()
-    achieved = bytes_per_launch / kern_avg_s / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        with open(pmc) as fh:
-            rec = json.load(fh)
-        key = f"{args.physics}_{args.precision}_{E}" if args.task == "hover" else \
-            f"race_{args.level}_{args.drones}_{args.physics}_{args.precision}_{E}"
-        if key in rec:
-            traffic = rec[key]["hbm_bytes_per_launch"]
-    result = {
-        "metric": "env-steps/sec (N parallel drones) at 1/2/4/8 MI355X; % HBM roofline",
-        "value": E * world * K / elapsed,
-        "unit": "env-steps/s",
-        "n_gpus": world,
-        "steps": K,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / K * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32" if args.precision == "fp32" else "f64",
-        "data": "synthetic: device-RNG airborne initial states around (0,0,1), U[-1,1] RPM actions",
-        "config": {"workload": f"HoverAviary Physics.{args.physics} 240/30 Hz (8 sub-steps), {E} envs x 1 drone "
-                               f"per GPU, RPM actions, auto-reset", "envs_per_gpu": E, "global_envs": E * world,
-                   "drones_per_env": 1, "parallelism": f"env-sharded dp{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                     "bytes_per_launch": bytes_per_launch, "kernel_us": kern_avg_s * 1e6,
-                     "kernel_us_median": float(np.median(kern_ms)) * 1e3, "timed_launches": int(len(kern_ms))},
-        "timing": {"timed_region": f"{K // G} replays of a {G}-step HIP graph (one fused launch per env.step)",
-                   "eager": eager},
-        "kernel": _lib.kernel_name(env.cfg),
-    }
-    if allgather is not None:
-        result["with_obs_allgather"] = allgather
+
+def roofline_sweep(make, sizes, launches=30):
+    """The same step kernel at larger env counts (one GPU): where the launch leaves the latency-bound
+    regime of E = 4096 and becomes HBM-bound.  Kernel time from dispatch-attached events."""
+    out = []
+    for n in sizes:
+        env = make(num_envs=n, env_offset=0)
+        env.reset()
+        a = torch.rand((4, n, 1, 4), device=env.device) * 2 - 1
+        for k in range(5):
+            env.step(a[k % 4])
+        us = float(np.mean(kernel_times(env, a, launches))) * 1e3
+        gbps = env.step_bytes() / (us * 1e-6) / 1e9
+        out.append({"envs": n, "kernel_us": us, "env_steps_per_s": n / (us * 1e-6), "achieved_GBps": gbps,
+                    "frac": gbps / HBM_PEAK_GBPS})
+        env.close()
+        del a
+    return out
+
+
+def bench_config1(args, dev, cpu_seconds, with_cpu):
+    """BASELINE configs[0]: one HoverAviary env (E = 1, PYB, 240/30 Hz) stepped from Python like
+    examples/pid.py: per-step latency on the GPU (synchronised each step, and graph-replayed)
+    and the float64 oracle for one env on one host core."""
+    make = hover_make("fp32", "PYB", dev)
+    env = make(num_envs=1, env_offset=0)
+    env.reset()
+    acts = hover_actions(1, dev, 3)
+    for k in range(50):
+        env.step(acts[k % acts.shape[0]])
+    torch.cuda.synchronize()
+    n = 500
+    t0 = time.perf_counter()
+    for k in range(n):
+        env.step(acts[k % acts.shape[0]])
+        torch.cuda.synchronize()
+    sync_s = (time.perf_counter() - t0) / n
+    elapsed, G = time_graph(env, acts, 1000, 10, 1, dev)
+    kern = kernel_times(env, acts, 200)
+    rec = {"workload": "HoverAviary 1 env x 1 drone, Physics.PYB 240/30 Hz (8 sub-steps), RPM actions, fp32",
+           "gpu_sync_per_step": {"value": 1 / sync_s, "unit": "env-steps/s", "us_per_step": sync_s * 1e6,
+                                 "note": "Python env.step + torch.cuda.synchronize each step"},
+           "gpu_graph": {"value": 1000 / elapsed, "unit": "env-steps/s", "us_per_step": elapsed / 1000 * 1e6},
+           "kernel_us": float(np.mean(kern)) * 1e3}
+    if with_cpu:
+        v, steps, dt = _oracle_leg(env.cfg, 1, _hover_acts, min(cpu_seconds, 3.0), 1)
+        rec["cpu_oracle_1env"] = {"value": v, "unit": "env-steps/s", "cores": 1,
+                                  "sample": f"1 env x {steps} env.steps, {dt:.1f} s"}
+    env.close()
+    return rec
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launch_check:
+        return launch_check(args, world, rank)
+    if torch.cuda.device_count() < world:
+        sys.exit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPUs")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world
+    dev = local
+    E, K, W = args.envs, args.steps, args.warmup
+    RK, RW = args.race_steps, max(10, args.race_steps // 10)
+
+    result = {"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
+              "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+              "dtype": "f32" if args.precision == "fp32" else "f64"}
+    hover_cfg = None
     if args.task == "race":
-        result["config"] = {"workload": f"MultiRaceAviary {args.racemode} {args.level}, {args.drones} drones x {E} envs "
-                                        f"per GPU, Physics.{args.physics} 500/25 Hz (20 sub-steps, Mellinger 500 Hz)",
-                            "envs_per_gpu": E, "global_envs": E * world, "drones_per_env": args.drones,
-                            "parallelism": f"env-sharded dp{world}"}
-        result["data"] = "synthetic: level preset resets (device Philox), FULLSTATE targets start + U(+-0.3) m"
-        result["drone_steps_per_s"] = result["value"] * args.drones
-        if policy_rec is not None:
-            result["config"]["workload"] += f"; closed loop: on-device PPO actor ({args.policy}) each step"
-            result["data"] = "synthetic: level preset resets (device Philox); setpoints from the reference's PPO actor"
-            result["policy"] = policy_rec
-    if args.task == "hover" and world == 1 and not args.no_sweep and policy is None:
-        result["roofline"]["sweep"] = roofline_sweep(make, [65536, 262144, 1048576])
+        rec = bench_race(args.level, args.drones, args.physics, args.racemode, args.precision, E, K, W, world, rank,
+                         local, 2, sharded_gather=world > 1 and not args.no_allgather, policy_spec=args.policy)
+        result.update({"value": rec.pop("value"), "ms_per_step": rec.pop("ms_per_step"),
+                       "data": "synthetic: level preset resets (device Philox), FULLSTATE targets start + U(+-0.3) m"
+                       if not args.policy else "synthetic: level preset resets; setpoints from the reference's PPO actor",
+                       "config": {"workload": rec.pop("workload"), "envs_per_gpu": E, "global_envs": E * world,
+                                  "drones_per_env": args.drones, "parallelism": f"env-sharded dp{world}"}})
+        for k in ("steps", "warmup", "n_gpus", "unit"):
+            rec.pop(k, None)
+        result.update(rec)
+    else:
+        rec, hover_cfg = bench_hover(args, args.precision, E, K, W, world, rank, local,
+                                     sweep=world == 1 and not args.no_sweep,
+                                     sharded_gather=world > 1 and not args.no_allgather)
+        result.update({"value": rec.pop("value"), "ms_per_step": rec.pop("ms_per_step"),
+                       "data": "synthetic: device-RNG airborne initial states around (0,0,1), U[-1,1] RPM actions",
+                       "config": {"workload": f"HoverAviary Physics.{args.physics} 240/30 Hz (8 sub-steps), {E} envs "
+                                              f"x 1 drone per GPU, RPM actions, auto-reset", "envs_per_gpu": E,
+                                  "global_envs": E * world, "drones_per_env": 1,
+                                  "parallelism": f"env-sharded dp{world}"}})
+        result.update(rec)
+
+    if not args.no_configs and args.task == "hover":
+        cf = {}
+        # config 5 at every N (at N = 1 it is BASELINE configs[3])
+        cf["config5"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp32", 4096, RK, RW, world, rank, local, 4,
+                                   sharded_gather=world > 1 and not args.no_allgather)
+        if world == 1:
+            cf["config3"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2)
+            cf["config3_policy"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
+                                              policy_spec="example")
+            r64, _ = bench_hover(args, "fp64", E, min(K, 1000), min(W, 100), 1, 0, local)
+            r64.update({"workload": "the `value` workload with the float64 kernel", "unit": "env-steps/s"})
+            cf["config2_f64"] = r64
+            cf["config1"] = bench_config1(args, local, args.cpu_seconds, not args.no_cpu_baseline)
+        result["configs"] = cf
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(env.cfg, args.cpu_seconds)
+        if args.task == "race":
+            result["cpu_baseline"] = cpu_baseline(race_cfg_of(args), args.cpu_seconds, race=True)
+        else:
+            result["cpu_baseline"] = cpu_baseline(hover_cfg, args.cpu_seconds)
+            if "configs" in result:
+                from gym_pybullet_adrp_amd.envs.race import race_config
+                for name, lv, n, ph, md in (("config5", "level3", 4, "PYB_DW", "COMPETE"),
+                                            ("config3", "level0", 2, "PYB", "COMPARE")):
+                    c = race_config(lv, n, ph, md)
+                    result["configs"][name]["cpu_baseline"] = cpu_baseline(c, args.cpu_seconds / 2, race=True)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if policy is not None:
-        policy.close()
-    env.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def race_cfg_of(args):
+    from gym_pybullet_adrp_amd.envs.race import race_config
+    return race_config(args.level, args.drones, args.physics, args.racemode)
 
 
 if __name__ == "__main__":

@@ -252,8 +252,14 @@ static RaceConst<Real> race_const(const adrp_config& c) {
 template <typename Real>
 static int upload_race_const(adrp_t* h) {
     const RaceConst<Real> k = race_const<Real>(h->cfg);
-    if (hipMalloc(&h->cblk, sizeof k) != hipSuccess) return ADRP_ERR_OOM;
-    if (hipMemcpy(h->cblk, &k, sizeof k, hipMemcpyHostToDevice) != hipSuccess) return ADRP_ERR_DEVICE;
+    // [RaceConst | tick-schedule tables (att, pos)] (race_args)
+    std::vector<uint32_t> ticks(2 * kTickWords);
+    race_tick_tables(ticks.data(), ticks.data() + kTickWords);
+    const size_t off = race_ticks_offset<Real>();
+    if (hipMalloc(&h->cblk, off + ticks.size() * 4) != hipSuccess) return ADRP_ERR_OOM;
+    if (hipMemcpy(h->cblk, &k, sizeof k, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy((char*)h->cblk + off, ticks.data(), ticks.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return ADRP_ERR_DEVICE;
     return ADRP_OK;
 }
 

@@ -80,10 +80,14 @@ inline HoverArgs<Real> hover_args(const adrp_t* h) {
 }
 
 template <typename Real>
+constexpr size_t race_ticks_offset() { return (sizeof(RaceConst<Real>) + 255) & ~size_t(255); }
+
+template <typename Real>
 inline RaceArgs<Real> race_args(const adrp_t* h) {
     RaceArgs<Real> a;
     memset(&a, 0, sizeof a);
     a.c = (const RaceConst<Real>*)h->cblk;
+    a.ticks = (const uint32_t*)((const char*)h->cblk + race_ticks_offset<Real>());
     a.f = (Real*)h->f;
     a.ist = h->ist;
     a.seed = h->cfg.seed;

@@ -76,6 +76,7 @@ struct RaceArgs {
     uint8_t* trunc;
     float* tobs;         // [E][N][D] or null
     const uint8_t* mask; // reset mask or null
+    const uint32_t* ticks; // tick-schedule bit tables (kTickTableN ticks each: att, then pos)
     uint64_t seed;
     int64_t env_offset;
     int E;
@@ -84,9 +85,51 @@ struct RaceArgs {
 // ---------------------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ float clampf_(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
-template <typename Real>
-__device__ __forceinline__ Real clampr_(Real v, Real lo, Real hi) { return v < lo ? lo : (v > hi ? hi : v); }
+// MellingerControl._step_controller's float64 tick schedule (MellingerControl.py:393-411):
+//   cur = tick / 500; att due if cur - last_att / 500 > 0.002; pos due if cur - last_pos / 500 > 0.01.
+// In float64 these tests depend only on the tick differences, except at the boundaries: a difference
+// >= 2 (att) / >= 6 (pos) is always due and <= 0 / <= 4 never (checked for every tick < 2^21); for a
+// difference of exactly 1 / 5 the rounding of tick / 500 decides.  Those two decisions per tick are
+// bit tables computed on the host in float64 (race_tick_tables), so the loop does no fp64 work: each
+// lane keeps a 32-tick window of both tables in registers.
+constexpr int kTickTableN = 1 << 17;                  // ticks covered (262 s of flight per episode)
+constexpr int kTickWords = kTickTableN / 32 + 1;      // + 1 word of padding for the window read
+inline void race_tick_tables(uint32_t* att, uint32_t* pos) {   // host: [kTickWords] each
+    for (int w = 0; w < kTickWords; ++w) att[w] = pos[w] = 0;
+    for (int n = 1; n < kTickTableN; ++n) {
+        const double cur = n / 500.0;
+        if (cur - (n - 1) / 500.0 > 0.002) att[n >> 5] |= 1u << (n & 31);
+        if (n >= 5 && cur - (n - 5) / 500.0 > 0.01) pos[n >> 5] |= 1u << (n & 31);
+    }
+}
+// bits (tick0 .. tick0 + 31) of both tables; past the table the float64 tests themselves
+__device__ __forceinline__ void tick_window(const uint32_t* tab, int n, uint32_t& att, uint32_t& pos) {
+    if (__builtin_expect(__any(n > kTickTableN - 32), 0)) {
+        if (n > kTickTableN - 32) {
+            att = pos = 0;
+            for (int j = 0; j < 32; ++j) {
+                const double cur = double(n + j) / 500.0;
+                att |= (cur - double(n + j - 1) / 500.0 > 0.002 ? 1u : 0u) << j;
+                pos |= (cur - double(n + j - 5) / 500.0 > 0.01 ? 1u : 0u) << j;
+            }
+            return;
+        }
+    }
+    const int w = n >> 5, sh = n & 31;
+    att = __builtin_amdgcn_alignbit(tab[w + 1], tab[w], sh);
+    pos = __builtin_amdgcn_alignbit(tab[kTickWords + w + 1], tab[kTickWords + w], sh);
+}
+
+// clamps: v_med3_f32 (one instruction; the select form is four).  Equal to the reference's
+// `v < lo ? lo : (v > hi ? hi : v)` for every non-NaN v; fp64 keeps the selects
+__device__ __forceinline__ float clampf_(float v, float lo, float hi) { return __builtin_amdgcn_fmed3f(v, lo, hi); }
+__device__ __forceinline__ float clampr_(float v, float lo, float hi) { return __builtin_amdgcn_fmed3f(v, lo, hi); }
+__device__ __forceinline__ double clampr_(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+// one-sided clamps (`x > hi ? hi : x`, `x < lo ? lo : x`) as v_min/v_max for non-NaN x
+__device__ __forceinline__ float minr_(float x, float hi) { return __builtin_fminf(x, hi); }
+__device__ __forceinline__ double minr_(double x, double hi) { return x > hi ? hi : x; }
+__device__ __forceinline__ float maxr_(float x, float lo) { return __builtin_fmaxf(x, lo); }
+__device__ __forceinline__ double maxr_(double x, double lo) { return x < lo ? lo : x; }
 template <typename Real>
 __device__ __forceinline__ Real fmaxr_(Real a, Real b) { return a > b ? a : b; }
 __device__ __forceinline__ float radf_(float d) { return (3.14159265358979323846f / 180.0f) * d; }
@@ -94,6 +137,39 @@ __device__ __forceinline__ float degf_(float r) { return (180.0f / 3.14159265358
 
 template <typename Real>
 __device__ __forceinline__ Real shfl_(Real v, int src, int width) { return __shfl(v, src, width); }
+
+// value of lane k of this lane's group of G adjacent lanes (the drones of one env).  G <= 4: a
+// DPP quad_perm move (one VALU op, no LDS round trip); G = 8: ds_bpermute.  k must fold to a
+// constant (unrolled loops).
+template <int G>
+__device__ __forceinline__ int grp_bcast_i(int v, int k) {
+    if constexpr (G == 1) {
+        return v;
+    } else if constexpr (G == 2) {
+        switch (k) {   // quad_perm [k, k, 2 + k, 2 + k]
+            case 0: return __builtin_amdgcn_mov_dpp(v, 0 | (0 << 2) | (2 << 4) | (2 << 6), 0xf, 0xf, false);
+            default: return __builtin_amdgcn_mov_dpp(v, 1 | (1 << 2) | (3 << 4) | (3 << 6), 0xf, 0xf, false);
+        }
+    } else if constexpr (G == 4) {
+        switch (k) {   // quad_perm [k, k, k, k]
+            case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xf, 0xf, false);
+            case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xf, 0xf, false);
+            case 2: return __builtin_amdgcn_mov_dpp(v, 0xaa, 0xf, 0xf, false);
+            default: return __builtin_amdgcn_mov_dpp(v, 0xff, 0xf, 0xf, false);
+        }
+    } else {
+        return __shfl(v, k, G);
+    }
+}
+template <int G>
+__device__ __forceinline__ float grp_bcast(float v, int k) {
+    return __int_as_float(grp_bcast_i<G>(__float_as_int(v), k));
+}
+template <int G>
+__device__ __forceinline__ double grp_bcast(double v, int k) {
+    const int lo = grp_bcast_i<G>(__double2loint(v), k), hi = grp_bcast_i<G>(__double2hiint(v), k);
+    return __hiloint2double(hi, lo);
+}
 
 // ---------------------------------------------------------------------------------------
 // geometry: URDF collision shapes, GJK distance, ray vs cylinder
@@ -315,8 +391,9 @@ struct RDrone {
     float ctl[4];
     Real mass, inertia[3];
     Real inv_mass, inv_i[3];        // per env.step
-    int tick, last_att, last_pos, tumble, gate, flags;
-    double t_att, t_pos;            // last_att_pid_call / last_pos_pid_call (float64, MellingerControl.py:395-407)
+    int tick, last_att, last_pos, tumble, gate, flags;   // last_*: the ticks of last_{att,pos}_pid_call
+    int tick_base;                  // tick of bit 0 of the tick-schedule windows
+    uint32_t att_bits, pos_bits;    // tick_window(tick_base)
 };
 
 template <typename Real>
@@ -353,8 +430,8 @@ __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, s
     d.tick = ist[RI_TICK * EN + slot]; d.last_att = ist[RI_LAST_ATT * EN + slot];
     d.last_pos = ist[RI_LAST_POS * EN + slot]; d.tumble = ist[RI_TUMBLE * EN + slot];
     d.gate = ist[RI_GATE * EN + slot]; d.flags = ist[RI_FLAGS * EN + slot];
-    d.t_att = double(d.last_att) / 500.0;
-    d.t_pos = double(d.last_pos) / 500.0;
+    d.tick_base = d.tick;
+    tick_window(a.ticks, d.tick, d.att_bits, d.pos_bits);
     d.inv_mass = Real(1) / d.mass;
 #pragma unroll
     for (int k = 0; k < 3; ++k) d.inv_i[k] = Real(1) / d.inertia[k];
@@ -507,16 +584,14 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
         d.tick += 1;
         pwm[0] = pwm[1] = pwm[2] = pwm[3] = Real(0);
     } else {
-        const double cur = double(d.tick) / 500.0;
-        int t;
-        if ((cur - d.t_att > 0.002) && (cur - d.t_pos > 0.01)) {
-            t = 0; d.last_pos = d.tick; d.last_att = d.tick; d.t_pos = cur; d.t_att = cur;
-        } else if (cur - d.t_att > 0.002) {
-            d.last_att = d.tick; d.t_att = cur; t = 2;
-        } else {
-            t = 1;
-        }
-        if ((t & 1) == 0) {   // RATE_DO_EXECUTE(500 Hz, tick)
+        // the float64 schedule from the tick differences and the host bit tables (tick_window)
+        const int da = d.tick - d.last_att, dp = d.tick - d.last_pos, bit = d.tick - d.tick_base;
+        const bool att_due = (da >= 2) | ((da == 1) & (((d.att_bits >> bit) & 1u) != 0));
+        const bool pos_due = (dp >= 6) | ((dp == 5) & (((d.pos_bits >> bit) & 1u) != 0));
+        // t = 0 (both due), 2 (attitude due), 1 (neither); selects, no branches
+        d.last_pos = (att_due & pos_due) ? d.tick : d.last_pos;
+        d.last_att = att_due ? d.tick : d.last_att;
+        if (att_due) {   // t even: RATE_DO_EXECUTE(500 Hz, tick)
             // state.attitudeQuaternion = get_quaternion_from_euler(rpy) -> quat2rotmat: the body
             // rotation itself, except in getEulerFromQuaternion's gimbal branches
             float Rm[9];
@@ -551,8 +626,7 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
             const Real x = F32 ? clampr_(m4[k], Real(0), Real(65535)) * Real(60.0 / 65535)
                                : clampr_(m4[k], Real(0), Real(65535)) / Real(65535) * Real(60);
             const Real volts = Real(-0.0006239) * x * x + Real(0.088) * x;
-            Real pct = F32 ? volts * Real(1.0 / 3) : volts / Real(3);
-            if (pct > Real(1)) pct = Real(1);
+            const Real pct = minr_(F32 ? volts * Real(1.0 / 3) : volts / Real(3), Real(1));
             pwm[k] = pct * Real(65535);
         }
     }
@@ -565,8 +639,7 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        Real t = th[3 - k] + noise[k];
-        if (t < Real(0)) t = Real(0);
+        const Real t = maxr_(th[3 - k] + noise[k], Real(0));
         Real mp = F32 ? (hsqrt_(t * Real(1.0 / 3.16e-10)) - Real(4070.3)) * Real(1.0 / 0.2685)
                       : (sqrt_(t / Real(1) / Real(3.16e-10)) - Real(4070.3)) / Real(0.2685);
         mp = clampr_(mp, Real(20000), Real(65535));
@@ -1243,7 +1316,13 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
 #ifdef ADRP_RACE_TIMING
     uint64_t acc_phys = 0;
 #endif
-    for (int s = 0; s < H.S; ++s) {
+    for (int s0 = 0; s0 < H.S; s0 += 32) {   // chunks of the 32-tick schedule windows (S > 32 only)
+    if (s0 > 0) {
+        d.tick_base = d.tick;
+        tick_window(a.ticks, d.tick, d.att_bits, d.pos_bits);
+    }
+    const int s1 = H.S < s0 + 32 ? H.S : s0 + 32;
+    for (int s = s0; s < s1; ++s) {
 #ifdef ADRP_RACE_TIMING
         RACE_MARK(ta);
 #endif
@@ -1262,7 +1341,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
                 constexpr bool F32 = sizeof(Real) == 4;
 #pragma unroll
                 for (int k = 0; k < G; ++k) {   // all shuffles in flight at once
-                    const Real ox = shfl_(d.pos.x, k, G), oy = shfl_(d.pos.y, k, G), oz = shfl_(d.pos.z, k, G);
+                    const Real ox = grp_bcast<G>(d.pos.x, k), oy = grp_bcast<G>(d.pos.y, k), oz = grp_bcast<G>(d.pos.z, k);
                     const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
                     const Real dxy = hsqrt_(dx * dx + dy * dy);
                     if (k < N && dz > Real(0) && dxy < Real(10)) {
@@ -1314,6 +1393,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
             mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz_fast_u(d.q), noise);
         }
     }
+    }
     RACE_MARK(t2);
     if constexpr (PRE == 1) __syncthreads();   // the helpers' track copy is in LDS
     const TrackSrc<Real, PRE == 1> T{a.f, EN, slot, trk_lds, tl};
@@ -1322,8 +1402,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     Q4<Real> gq[ADRP_MAX_DRONES];
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-        gpos[k] = v3(shfl_(d.pos.x, k, G), shfl_(d.pos.y, k, G), shfl_(d.pos.z, k, G));
-        gq[k] = {shfl_(d.q.x, k, G), shfl_(d.q.y, k, G), shfl_(d.q.z, k, G), shfl_(d.q.w, k, G)};
+        gpos[k] = v3(grp_bcast<G>(d.pos.x, k), grp_bcast<G>(d.pos.y, k), grp_bcast<G>(d.pos.z, k));
+        gq[k] = {grp_bcast<G>(d.q.x, k), grp_bcast<G>(d.q.y, k), grp_bcast<G>(d.q.z, k), grp_bcast<G>(d.q.w, k)};
     }
     const int gate0 = d.gate;
     if (C.num_gates > 0 && gate0 < C.num_gates) {
@@ -1415,9 +1495,12 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     // per-env reduction over the drone lanes
     const int mydone = ((d.flags & 1) || (d.flags & 2)) ? 1 : 0, myfin = (d.flags & 2) ? 1 : 0;
     int all_done = 1, all_fin = 1;
-    for (int k = 0; k < N; ++k) {
-        all_done &= __shfl(mydone, k, G);
-        all_fin &= __shfl(myfin, k, G);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        if (k < N) {
+            all_done &= grp_bcast_i<G>(mydone, k);
+            all_fin &= grp_bcast_i<G>(myfin, k);
+        }
     }
     const bool te = all_done != 0;
     const bool tr = sc0 >= C.trunc_steps;   // step_counter / PYB_FREQ > episode_len_sec, before += S

@@ -24,6 +24,21 @@ from ..utils.spaces import Box
 from .tracks import fill_track
 
 
+def race_config(race_config="level0", num_drones=2, physics="PYB", racemode="COMPARE", num_envs=1, seed=2024):
+    """The adrp_config a MultiRaceAviary(race_config, num_drones, physics, racemode) builds, without a
+    device handle (host-side: bench.py's CPU baseline, tests)."""
+    cfg = _lib.default_config(abi.TASK_RACE)
+    cfg.num_drones = int(num_drones)
+    fill_track(cfg, race_config, int(num_drones))
+    ph = Physics[physics] if isinstance(physics, str) else Physics(physics)
+    rm = RaceMode[racemode] if isinstance(racemode, str) else RaceMode(racemode)
+    cfg.physics = PHYSICS_CODE[ph]
+    cfg.race_mode = abi.RACE_COMPETE if rm == RaceMode.COMPETE else abi.RACE_COMPARE
+    cfg.num_envs = int(num_envs)
+    cfg.seed = int(seed)
+    return cfg
+
+
 class MultiRaceAviary:
     """Batched counterpart of gym_pybullet_adrp.envs.MultiRaceAviary."""
 
@@ -46,8 +61,8 @@ class MultiRaceAviary:
         cfg = _lib.default_config(abi.TASK_RACE)
         cfg.num_drones = int(num_drones)
         self.config = fill_track(cfg, race_config, int(num_drones))
-        cfg.physics = PHYSICS_CODE[physics]
-        cfg.race_mode = abi.RACE_COMPETE if racemode == RaceMode.COMPETE else abi.RACE_COMPARE
+        cfg.physics = PHYSICS_CODE[Physics(physics)]
+        cfg.race_mode = abi.RACE_COMPETE if RaceMode(racemode) == RaceMode.COMPETE else abi.RACE_COMPARE
         cfg.num_envs = int(num_envs)
         cfg.pyb_freq, cfg.ctrl_freq = int(pyb_freq), int(ctrl_freq)
         cfg.autoreset = 1 if autoreset else 0

@@ -20,6 +20,7 @@
 #define PI 3.14159265358979323846
 
 static char g_err[256];
+static void race_init_consts(void);   /* race.c (included at the end) */
 static int fail(const char* msg) {
     snprintf(g_err, sizeof g_err, "%s", msg);
     return ADRP_ERR_INVALID;
@@ -297,6 +298,7 @@ int orc_create(const adrp_config* cfg, orc_t** out) {
         o->ring_head = (int32_t*)calloc(o->E, 4);
         o->contact = (uint8_t*)calloc(o->E, 1);
         race_alloc(o);
+        race_init_consts();
         *out = o;
         return ADRP_OK;
     }
@@ -805,7 +807,6 @@ static void hover_step_env(orc_t* o, int e, const float* act, float* obs_row, fl
         memcpy(b->last_rpm, rpm, sizeof rpm);   /* self.last_clipped_action = clipped_action */
     }
     o->contact[e] = touched;
-    o->contacts += touched;
     hover_obs(o, e, obs_row);
     hover_task(o, e, rew, term, trunc);
     o->step_counter[e] += o->S;                    /* BaseAviary.py:386 */
@@ -824,19 +825,30 @@ int orc_hover_eval(const orc_t* o, float* obs, float* rew, uint8_t* term, uint8_
     return ADRP_OK;
 }
 
+/* Envs are independent: with orc_set_threads(n > 1) the env loop runs on n OpenMP threads
+   (the all-core CPU baseline of bench.py).  Results do not depend on the thread count. */
+static int g_threads = 1;
+void orc_set_threads(int n) { g_threads = n > 0 ? n : 1; }
+int orc_get_threads(void) { return g_threads; }
+
 int orc_step(orc_t* o, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
              float* terminal_obs) {
-    o->contacts = 0;
+    const int E = o->E;
     if (o->cfg.task == ADRP_TASK_RACE) {
         const size_t row = (size_t)o->N * o->D;
-        for (int e = 0; e < o->E; ++e)
+#pragma omp parallel for schedule(dynamic, 4) num_threads(g_threads) if (g_threads > 1)
+        for (int e = 0; e < E; ++e)
             race_step_env(o, e, act + (size_t)e * o->N * 4, obs + e * row, rew + e, term + e, trunc + e,
                           terminal_obs ? terminal_obs + e * row : NULL);
-        return ADRP_OK;
+    } else {
+#pragma omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)
+        for (int e = 0; e < E; ++e)
+            hover_step_env(o, e, act + (size_t)e * o->A, obs + (size_t)e * o->D, rew + e, term + e, trunc + e,
+                           terminal_obs ? terminal_obs + (size_t)e * o->D : NULL);
     }
-    for (int e = 0; e < o->E; ++e)
-        hover_step_env(o, e, act + (size_t)e * o->A, obs + (size_t)e * o->D, rew + e, term + e, trunc + e,
-                       terminal_obs ? terminal_obs + (size_t)e * o->D : NULL);
+    int64_t n = 0;
+    for (int e = 0; e < E; ++e) n += o->contact[e];
+    o->contacts = n;
     return ADRP_OK;
 }
 

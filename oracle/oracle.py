@@ -45,6 +45,8 @@ def _load():
     lib.orc_env_contact.argtypes = [P, I]
     lib.orc_env_contact.restype = ctypes.c_uint8
     lib.orc_default_config.argtypes = [I, P]
+    lib.orc_set_threads.argtypes = [I]
+    lib.orc_get_threads.restype = I
     lib.orc_philox4x32_10.argtypes = [P, P, P]
     lib.orc_euler_from_quat.argtypes = [P, P]
     lib.orc_quat_from_euler.argtypes = [P, P]
@@ -210,6 +212,11 @@ def derived_constants(cfg):
     out = np.zeros(6)
     lib().orc_derived_constants(ctypes.byref(cfg), _ptr(out))
     return out
+
+
+def set_threads(n):
+    """OpenMP threads for the env loop of Oracle.step (1 = the scalar restatement)."""
+    lib().orc_set_threads(int(n))
 
 
 def default_config(task):

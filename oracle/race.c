@@ -217,11 +217,12 @@ static void mellinger_wrapper_reset(rdrone_t* d, const double init_rpy[3], const
 }
 
 /* computeControl(t, pos, rpy, vel, ang_vel, disturbance) -> rpm[4] */
+static lpf_t g_gyro_lpf;   /* written once in orc_create, before any (threaded) step */
+static void race_init_consts(void) { g_gyro_lpf = lpf_coeffs(FIRMWARE_FREQ, 30); }
+
 static void mellinger_compute(rdrone_t* d, const double sp_xyz[3], double sp_yaw, const double pos[3],
                               const double rpy[3], const double vel[3], const double noise[4], double rpm[4]) {
-    static int init = 0;
-    static lpf_t gyro_lpf;
-    if (!init) { gyro_lpf = lpf_coeffs(FIRMWARE_FREQ, 30); init = 1; }   /* ACCEL_LPF_CUTOFF_FREQ (swapped) */
+    const lpf_t gyro_lpf = g_gyro_lpf;   /* ACCEL_LPF_CUTOFF_FREQ (swapped); set by orc_create */
     double rates[3], acc[3];
     for (int k = 0; k < 3; ++k) {
         rates[k] = (rpy[k] - d->prev_rpy[k]) / FIRMWARE_DT;
@@ -842,7 +843,6 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
         }
     }
     o->contact[e] = (uint8_t)touched;
-    o->contacts += touched;
     for (int i = 0; i < N; ++i) race_gate_progress(o, e, i);
     double row0[64 + 6 * ADRP_MAX_DRONES];
     race_write_obs(o, e, obs_env, row0);

@@ -2,7 +2,9 @@
 the observation all-gather.  Each rank steps its shard with the CPU oracle (test
 infrastructure standing in for the per-GPU handle); the gathered global batch must be
 bit-identical to one oracle stepping all envs, because reset draws are keyed by the
-global env id."""
+global env id.  Two workloads: HoverAviary (config 2) and the config-5
+race workload (level3, 4 drones, COMPETE, PYB_DW, disturbances, gate randomisation,
+auto-reset; envs/MultiRaceAviary.py:171-270)."""
 import os
 import socket
 
@@ -14,6 +16,7 @@ import torch.multiprocessing as mp
 
 from gym_pybullet_adrp_amd.sharding import ShardedAviary, shard_range
 from gym_pybullet_adrp_amd.utils import abi
+from gym_pybullet_adrp_amd.utils.enums import PHYSICS_CODE, Physics
 
 E_GLOBAL = 11          # ragged over 2 ranks: 6 + 5
 STEPS = 40
@@ -47,12 +50,28 @@ def _cfg():
     return c
 
 
+def _race_cfg():
+    from gym_pybullet_adrp_amd.envs.tracks import fill_track
+    from oracle import oracle as O
+    c = O.default_config(abi.TASK_RACE)
+    c.num_drones = 4
+    fill_track(c, "level3", 4)
+    c.race_mode = abi.RACE_COMPETE
+    c.physics = PHYSICS_CODE[Physics.PYB_DW]
+    c.seed = 4242
+    c.autoreset = 1
+    return c
+
+
+WORKLOADS = {"hover": (_cfg, 1), "race": (_race_cfg, 4)}
+
+
 class OracleShard:
     """CPU oracle behind the env interface ShardedAviary expects (torch in / torch out)."""
 
-    def __init__(self, num_envs, env_offset):
+    def __init__(self, num_envs, env_offset, kind="hover"):
         from oracle import oracle as O
-        c = _cfg()
+        c = WORKLOADS[kind][0]()
         c.num_envs = num_envs
         c.env_offset = env_offset
         self.o = O.Oracle(c)
@@ -65,28 +84,35 @@ class OracleShard:
         return torch.from_numpy(obs), torch.from_numpy(rew), torch.from_numpy(te), torch.from_numpy(tr), {}
 
 
-def _actions():
-    return np.random.default_rng(5).uniform(-1, 1, (STEPS, E_GLOBAL, 1, 4)).astype(np.float32)
+def _actions(kind="hover"):
+    rng = np.random.default_rng(5)
+    if kind == "hover":
+        return rng.uniform(-1, 1, (STEPS, E_GLOBAL, 1, 4)).astype(np.float32)
+    # FULLSTATE targets, re-drawn every 10 steps; many lie outside the level3 bounds (|x|,|y| > 3, z > 2) or
+    # at the ground, so drones get eliminated, envs terminate and auto-reset inside the run
+    t = rng.uniform([-4, -4, 0.0, -1], [4, 4, 2.6, 1], (STEPS // 10, E_GLOBAL, 4, 4))
+    return np.repeat(t, 10, axis=0).astype(np.float32)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, kind="hover"):
+    import functools
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        env = ShardedAviary(E_GLOBAL, OracleShard)
+        env = ShardedAviary(E_GLOBAL, functools.partial(OracleShard, kind=kind))
         assert (env.offset, env.count) == shard_range(E_GLOBAL, world, rank)
         obs, _ = env.reset()
         g_obs = env.gather(obs, torch.zeros(env.count), torch.zeros(env.count, dtype=torch.bool),
                            torch.zeros(env.count, dtype=torch.bool))[0]
         traj = [g_obs.numpy()]
         rews, terms, truncs = [], [], []
-        for a in _actions():
+        for a in _actions(kind):
             obs, rew, te, tr, _ = env.step(torch.from_numpy(a))      # global batch in, own slice used
             go, gr, gte, gtr = env.gather(obs, rew, te, tr)
             traj.append(go.numpy()); rews.append(gr.numpy()); terms.append(gte.numpy()); truncs.append(gtr.numpy())
         if rank == 0:
-            np.savez(os.path.join(out_dir, "sharded.npz"), obs=np.stack(traj), rew=np.stack(rews),
+            np.savez(os.path.join(out_dir, f"sharded_{kind}.npz"), obs=np.stack(traj), rew=np.stack(rews),
                      term=np.stack(terms), trunc=np.stack(truncs))
         dist.barrier()
     finally:
@@ -99,17 +125,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_two_rank_gloo_matches_single_batch(tmp_path):
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    got = np.load(tmp_path / "sharded.npz")
-    one = OracleShard(E_GLOBAL, 0)
+@pytest.mark.parametrize("kind", ["hover", "race"])
+def test_two_rank_gloo_matches_single_batch(tmp_path, kind):
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), kind), nprocs=2, join=True)
+    got = np.load(tmp_path / f"sharded_{kind}.npz")
+    one = OracleShard(E_GLOBAL, 0, kind)
     obs, _ = one.reset()
     traj, rews, terms, truncs = [obs.numpy()], [], [], []
-    for a in _actions():
+    for a in _actions(kind):
         obs, rew, te, tr, _ = one.step(torch.from_numpy(a))
         traj.append(obs.numpy()); rews.append(rew.numpy()); terms.append(te.numpy()); truncs.append(tr.numpy())
     np.testing.assert_array_equal(got["obs"], np.stack(traj))
     np.testing.assert_array_equal(got["rew"], np.stack(rews))
     np.testing.assert_array_equal(got["term"], np.stack(terms))
     np.testing.assert_array_equal(got["trunc"], np.stack(truncs))
-    assert np.stack(truncs).any(), "the workload should exercise truncation + auto-reset"
+    done = np.stack(terms) if kind == "race" else np.stack(truncs)
+    assert done.any(), "the workload should exercise termination/truncation + auto-reset"

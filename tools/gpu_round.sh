@@ -7,7 +7,7 @@ PHASE="${2:-all}"     # test | prof | all (one gpurun call is capped at 1200 s: 
 PROF="cd /tmp && export TMPDIR=/tmp && rocprofv3"
 RACE4="level3 4 PYB_DW COMPETE 4096"
 T=(
-  "pytest_gpu|600|cd $R && python -m pytest tests -m gpu -x -q"
+  "pytest_gpu|600|cd $R && python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread"
   "smoke|200|cd $R && python -c 'import __graft_entry__ as g; g.smoke()'"
   "bench|300|cd $R && python bench.py"
   "bench_race3|300|cd $R && python bench.py --task race --level level0 --drones 2 --envs 2048 --steps 300 --warmup 30"

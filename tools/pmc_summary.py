@@ -1,6 +1,16 @@
 """Summarise rocprofv3 --pmc passes of a step kernel into per-launch HBM bytes.
 
 usage: python tools/pmc_summary.py OUT.json KEY FETCH_DIR WRITE_DIR [KEY FETCH_DIR WRITE_DIR ...]
+       python tools/pmc_summary.py --valu OUT.json KEY FLOPS_DIR BUSY_DIR [...]
+
+--valu: the VALU roofline of a step kernel from two passes, FLOPS_DIR =
+SQ_INSTS_VALU_FLOPS_FP32, SQ_INSTS_VALU_FLOPS_FP32_TRANS, SQ_INSTS_VALU_FLOPS_FP64, SQ_INSTS_VALU and
+BUSY_DIR = SQ_INSTS_VALU_FMA_F32, SQ_INSTS_VALU_ADD_F32, SQ_INSTS_VALU_MUL_F32, SQ_INSTS_VALU_TRANS_F32,
+SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES + GRBM_GUI_ACTIVE.  flops_per_launch = the FLOPS
+counters (counted per active lane by the SQ); the instruction-mix estimate 64 x (2 FMA + ADD + MUL +
+TRANS) is kept beside it (it counts inactive lanes too).  valu_busy = SQ_ACTIVE_INST_VALU (quad-cycles
+summed over SIMDs) / (CUs x GRBM_GUI_ACTIVE per XCD), rocprof's VALUBusy: the fraction of SIMD-cycles a
+VALU instruction was executing.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is
@@ -28,7 +38,39 @@ def counter(d, name, kernel):
     return statistics.median(steady), len(vals)
 
 
+CUS = 256
+
+
+def valu(out_path, rest):
+    try:
+        rec = json.load(open(out_path))
+    except (OSError, ValueError):
+        rec = {}
+    for i in range(0, len(rest), 3):
+        key, fdir, bdir = rest[i:i + 3]
+        kernel = "race_step_kernel" if key.startswith("race_") else "hover_step_kernel"
+        c = {n: counter(fdir, n, kernel)[0] for n in ("SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS",
+                                                      "SQ_INSTS_VALU_FLOPS_FP64", "SQ_INSTS_VALU")}
+        c.update({n: counter(bdir, n, kernel)[0] for n in (
+            "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32",
+            "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")})
+        # the FLOPS counters count per wave-instruction (their sum equals 2 FMA + ADD + MUL + TRANS): x 64 lanes
+        flops = 64 * (c["SQ_INSTS_VALU_FLOPS_FP32"] + c["SQ_INSTS_VALU_FLOPS_FP32_TRANS"] + c["SQ_INSTS_VALU_FLOPS_FP64"])
+        mix = 64 * (2 * c["SQ_INSTS_VALU_FMA_F32"] + c["SQ_INSTS_VALU_ADD_F32"] + c["SQ_INSTS_VALU_MUL_F32"]
+                    + c["SQ_INSTS_VALU_TRANS_F32"])
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs in the per-dispatch record: per-XCD cycles = / 8
+        busy = c["SQ_ACTIVE_INST_VALU"] / (CUS * c["GRBM_GUI_ACTIVE"] / 8) if c["GRBM_GUI_ACTIVE"] else None
+        rec[key] = {"kernel": kernel, "flops_per_launch": flops, "flops_instruction_mix_estimate": mix,
+                    "valu_insts_per_launch": c["SQ_INSTS_VALU"], "valu_busy": busy, "counters": c,
+                    "method": "rocprofv3 --pmc, two passes (FLOPS counters; instruction mix + busy); median over "
+                              "dispatches after the first 8"}
+        print(key, json.dumps(rec[key]))
+    json.dump(rec, open(out_path, "w"), indent=1)
+
+
 def main():
+    if sys.argv[1] == "--valu":
+        return valu(sys.argv[2], sys.argv[3:])
     out_path, rest = sys.argv[1], sys.argv[2:]
     try:
         rec = json.load(open(out_path))
