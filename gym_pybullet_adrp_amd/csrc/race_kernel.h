@@ -543,14 +543,17 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
     const float My = -70000.0f * eRy + 20000.0f * ewy + 0.0f * d.ierrm[1] + 200.0f * err_d_pitch;
     const float Mz = -60000.0f * eRz + 12000.0f * ewz + 500.0f * d.ierrm[2];
     d.ctl[3] = 132000.0f * current_thrust;
-    if (d.ctl[3] > 0) {
-        d.ctl[0] = float(int16_t(clampf_(Mx, -32000.0f, 32000.0f)));
-        d.ctl[1] = float(int16_t(clampf_(My, -32000.0f, 32000.0f)));
-        d.ctl[2] = float(int16_t(clampf_(-Mz, -32000.0f, 32000.0f)));
-    } else {
-        d.ctl[0] = d.ctl[1] = d.ctl[2] = 0;
+    // thrust <= 0: moments and integrators zeroed.  Selects, not a branch: the branch form made the
+    // compiler merge the two paths' stores into one dynamically addressed store, which put
+    // ierrm[2] / ctl[2] in scratch memory (a scratch load + vmcnt(0) wait on every firmware call)
+    const bool on = d.ctl[3] > 0;
+    d.ctl[0] = on ? float(int16_t(clampf_(Mx, -32000.0f, 32000.0f))) : 0.0f;
+    d.ctl[1] = on ? float(int16_t(clampf_(My, -32000.0f, 32000.0f))) : 0.0f;
+    d.ctl[2] = on ? float(int16_t(clampf_(-Mz, -32000.0f, 32000.0f))) : 0.0f;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { d.ierr[k] = 0; d.ierrm[k] = 0; }
+    for (int k = 0; k < 3; ++k) {
+        d.ierr[k] = on ? d.ierr[k] : 0.0f;
+        d.ierrm[k] = on ? d.ierrm[k] : 0.0f;
     }
 }
 

@@ -23,10 +23,12 @@ static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t*
     auto by_g = [&](auto pre) {
         constexpr int P = decltype(pre)::value;
         switch (G) {
+#ifndef ADRP_DEV_FAST
             case 1: go(race_step_kernel<Real, PH, 1, P>); break;
+            case 8: go(race_step_kernel<Real, PH, 8, P>); break;
+#endif
             case 2: go(race_step_kernel<Real, PH, 2, P>); break;
-            case 4: go(race_step_kernel<Real, PH, 4, P>); break;
-            default: go(race_step_kernel<Real, PH, 8, P>); break;
+            default: go(race_step_kernel<Real, PH, 4, P>); break;
         }
     };
     if (helpers == 2) by_g(std::integral_constant<int, F32 ? 2 : 0>{});
@@ -40,6 +42,14 @@ int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term
     RaceArgs<Real> a = race_args<Real>(h);
     a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
     const int G = race_group(h->N);
+#ifdef ADRP_DEV_FAST   // experiment build (make dev): the benched race instantiations only
+    if (sizeof(Real) != 4 || (h->cfg.physics != ADRP_PHYS_PYB && h->cfg.physics != ADRP_PHYS_PYB_DW) || (G != 2 && G != 4))
+        return seterr(h, ADRP_ERR_INVALID, "dev build: race config not instantiated");
+    if constexpr (sizeof(Real) == 4) {
+        if (h->cfg.physics == ADRP_PHYS_PYB) launch_race_g<Real, ADRP_PHYS_PYB>(a, G, s, h);
+        else launch_race_g<Real, ADRP_PHYS_PYB_DW>(a, G, s, h);
+    }
+#else
     switch (h->cfg.physics) {
         case ADRP_PHYS_PYB: launch_race_g<Real, ADRP_PHYS_PYB>(a, G, s, h); break;
         case ADRP_PHYS_DYN: launch_race_g<Real, ADRP_PHYS_DYN>(a, G, s, h); break;
@@ -48,6 +58,7 @@ int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term
         case ADRP_PHYS_PYB_DW: launch_race_g<Real, ADRP_PHYS_PYB_DW>(a, G, s, h); break;
         default: launch_race_g<Real, ADRP_PHYS_PYB_GND_DRAG_DW>(a, G, s, h); break;
     }
+#endif
     HIPCHK(h, hipGetLastError());
     return ADRP_OK;
 }

@@ -591,6 +591,12 @@ static void pid_inputs(const adrp_config* cfg, const float* act, const double po
 #define BT_MAX_COORD_VEL 100.0   /* btMultiBody m_maxCoordinateVelocity */
 #define BT_ANGULAR_MOTION_THRESHOLD (0.5 * (PI / 2))
 
+/* Unpinned-choice probe (tests/test_closed_form.py): 1 = drop the spatial -> classical
+   "+ w x v" conversion of the base's linear acceleration, i.e. integrate vdot = F/m - damping - w x v.
+   The restatement (0) assumes Bullet converts; the test quantifies what the other reading changes. */
+static int g_omit_wxv = 0;
+void orc_set_bullet_variant(int omit_wxv) { g_omit_wxv = omit_wxv; }
+
 /* returns 1 if the documented ground model acted */
 static int bullet_step(const orc_t* o, body_t* b, const forces_t* F, double mass, v3 inertia) {
     const double dt = o->dt;
@@ -616,7 +622,7 @@ static int bullet_step(const orc_t* o, body_t* b, const forces_t* F, double mass
     v3 acc_lin = vscale(z_lin, -1.0 / mass);
     /* back to world; spatial -> classical linear acceleration */
     v3 wdot = mtv(R_wtb, acc_ang);
-    v3 vdot = mtv(R_wtb, vadd(acc_lin, vcross(w_b, v_b)));
+    v3 vdot = mtv(R_wtb, g_omit_wxv ? acc_lin : vadd(acc_lin, vcross(w_b, v_b)));
     /* applyDeltaVeeMultiDof(output, dt) with the coordinate-velocity clamp */
     double buf[6] = {b->omega.x, b->omega.y, b->omega.z, b->vel.x, b->vel.y, b->vel.z};
     double dv[6] = {wdot.x, wdot.y, wdot.z, vdot.x, vdot.y, vdot.z};

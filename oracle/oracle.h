@@ -71,6 +71,9 @@ void orc_compute_pwms(const double control[4], double pwm[4]);
 void orc_pwms_to_rpms(const double pwm[4], const double noise[4], double rpm[4]);
 int orc_tick_schedule(int n, uint8_t* ticks);
 uint32_t orc_config_size(void);
+/* 1: integrate the base without the spatial -> classical "+ w x v" term (probe of an unpinned
+ * Bullet reading, tests/test_closed_form.py); 0 (default): the restatement */
+void orc_set_bullet_variant(int omit_wxv);
 
 #ifdef __cplusplus
 }

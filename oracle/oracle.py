@@ -45,6 +45,7 @@ def _load():
     lib.orc_env_contact.argtypes = [P, I]
     lib.orc_env_contact.restype = ctypes.c_uint8
     lib.orc_default_config.argtypes = [I, P]
+    lib.orc_set_bullet_variant.argtypes = [I]
     lib.orc_set_threads.argtypes = [I]
     lib.orc_get_threads.restype = I
     lib.orc_philox4x32_10.argtypes = [P, P, P]
@@ -217,6 +218,12 @@ def derived_constants(cfg):
 def set_threads(n):
     """OpenMP threads for the env loop of Oracle.step (1 = the scalar restatement)."""
     lib().orc_set_threads(int(n))
+
+
+def set_bullet_variant(omit_wxv):
+    """1: the base integrates without the spatial -> classical "+ w x v" conversion (probe of an
+    unpinned reading of btMultiBody); 0: the restatement (default)"""
+    lib().orc_set_bullet_variant(int(omit_wxv))
 
 
 def default_config(task):
