@@ -61,6 +61,10 @@ def load():
     lib.adrp_profile_begin.restype = I
     lib.adrp_profile_end.argtypes = [P, P, I]
     lib.adrp_profile_end.restype = I
+    lib.adrp_reseed.argtypes = [P, ctypes.c_uint64, P]
+    lib.adrp_reseed.restype = I
+    lib.adrp_set_wrappers.argtypes = [P, I, I]
+    lib.adrp_set_wrappers.restype = I
     lib.adrp_set_diagnostics.argtypes = [P, I]
     lib.adrp_set_diagnostics.restype = I
     lib.adrp_diagnostic_contact_count.argtypes = [P, I]
@@ -165,6 +169,17 @@ class Handle:
 
     def step_bytes(self):
         return self.lib.adrp_step_bytes(self.h)
+
+    def reseed(self, seed):
+        """re-key the random streams as a handle created with `seed` (episode counters zeroed)"""
+        seed = int(seed) & (2 ** 64 - 1)
+        self._check(self.lib.adrp_reseed(self.h, seed, self._stream()), "adrp_reseed")
+        self.cfg.seed = seed
+
+    def set_wrappers(self, reward_wrapper, obs_wrapper):
+        self._check(self.lib.adrp_set_wrappers(self.h, int(bool(reward_wrapper)), int(obs_wrapper)), "adrp_set_wrappers")
+        self.cfg.track.reward_wrapper = int(bool(reward_wrapper))
+        self.cfg.track.obs_wrapper = int(obs_wrapper)
 
     def set_diagnostics(self, enable=True):
         self._check(self.lib.adrp_set_diagnostics(self.h, 1 if enable else 0), "adrp_set_diagnostics")

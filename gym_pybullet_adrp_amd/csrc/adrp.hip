@@ -198,6 +198,7 @@ static RaceConst<Real> race_const(const adrp_config& c) {
     k.trunc_steps = trunc_steps(t.episode_len_sec, c.pyb_freq);
     k.disturbances = t.disturbances ? 1 : 0;
     k.reward_wrapper = t.reward_wrapper ? 1 : 0;
+    k.obs_wrapper = t.obs_wrapper == 1 || t.obs_wrapper == 2 ? t.obs_wrapper : 0;
     k.random_gates = t.random_gates_obstacles ? 1 : 0;
     k.random_state = t.random_drone_state ? 1 : 0;
     k.random_inertia = t.random_drone_inertia ? 1 : 0;
@@ -256,7 +257,7 @@ static int upload_race_const(adrp_t* h) {
     std::vector<uint32_t> ticks(2 * kTickWords);
     race_tick_tables(ticks.data(), ticks.data() + kTickWords);
     const size_t off = race_ticks_offset<Real>();
-    if (hipMalloc(&h->cblk, off + ticks.size() * 4) != hipSuccess) return ADRP_ERR_OOM;
+    if (!h->cblk && hipMalloc(&h->cblk, off + ticks.size() * 4) != hipSuccess) return ADRP_ERR_OOM;
     if (hipMemcpy(h->cblk, &k, sizeof k, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy((char*)h->cblk + off, ticks.data(), ticks.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return ADRP_ERR_DEVICE;
@@ -270,8 +271,10 @@ extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
     static const char* ph[] = {"PYB", "DYN", "PYB_GND", "PYB_DRAG", "PYB_DW", "PYB_GND_DRAG_DW"};
     const int p = cfg->physics >= 0 && cfg->physics <= 5 ? cfg->physics : 0;
     if (cfg->task == ADRP_TASK_RACE) {
-        snprintf(buf, sizeof buf, "race_step<%s,%s,G%d>", cfg->precision ? "f64" : "f32", ph[p],
-                 race_group(cfg->num_drones));
+        const char* q = getenv("ADRP_RACE_QUAD");
+        const bool quad = !cfg->precision && !(q && atoi(q) == 0);
+        snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s>", cfg->precision ? "f64" : "f32", ph[p],
+                 race_group(cfg->num_drones), quad ? ",Q4" : "");
         return buf;
     }
     const int A = hover_act_dim(cfg->act_type);
@@ -341,7 +344,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
         delete h;
         return rc;
     };
-    if (hipSetDevice(device) != hipSuccess) return cleanup(seterr(h, ADRP_ERR_DEVICE, "hipSetDevice failed"));
+    DeviceGuard g(device);
     const size_t ring_bytes = size_t(h->B) * h->A * h->E * sizeof(float);
     if (hipMalloc(&h->f, h->nf_base * EN * h->real_size) != hipSuccess ||
         (ring_bytes && hipMalloc((void**)&h->ring, ring_bytes) != hipSuccess) ||
@@ -356,6 +359,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     if (const char* env = getenv("ADRP_STAGE_ROWS")) h->stage_rows = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RESET_HELPER")) h->reset_helper = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RACE_HELPERS")) h->race_helpers = atoi(env) != 0;
+    if (const char* env = getenv("ADRP_RACE_QUAD")) h->race_quad = atoi(env) != 0;
     const int rc = race ? (h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h))
                         : (h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h));
     if (rc != ADRP_OK) return cleanup(seterr(h, rc, "constant block upload failed"));
@@ -365,7 +369,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
 
 extern "C" void adrp_destroy(adrp_t* h) {
     if (!h) return;
-    hipSetDevice(h->device);
+    DeviceGuard g(h->device);
     hipDeviceSynchronize();
     for (auto e : h->ev_start) hipEventDestroy(e);
     for (auto e : h->ev_stop) hipEventDestroy(e);
@@ -373,12 +377,34 @@ extern "C" void adrp_destroy(adrp_t* h) {
     delete h;
 }
 
+extern "C" int adrp_reseed(adrp_t* h, uint64_t seed, void* stream) {
+    if (!h) return seterr(h, ADRP_ERR_INVALID, "adrp_reseed: NULL handle");
+    DeviceGuard g(h->device);
+    h->cfg.seed = seed;   // read into the kernel arguments at every launch
+    const size_t EN = size_t(h->E) * h->N;
+    static_assert(RI_EPISODE == 1 && HI_EPISODE == 1, "episode counters are int row 1 in both tasks");
+    HIPCHK(h, hipMemsetAsync(h->ist + EN, 0, EN * sizeof(int32_t), (hipStream_t)stream));
+    return ADRP_OK;
+}
+
+extern "C" int adrp_set_wrappers(adrp_t* h, int reward_wrapper, int obs_wrapper) {
+    if (!h) return seterr(h, ADRP_ERR_INVALID, "adrp_set_wrappers: NULL handle");
+    if (h->cfg.task != ADRP_TASK_RACE) return seterr(h, ADRP_ERR_INVALID, "wrappers are MultiRaceAviary's");
+    if (obs_wrapper < 0 || obs_wrapper > 2) return seterr(h, ADRP_ERR_INVALID, "obs_wrapper must be 0, 1 or 2");
+    DeviceGuard g(h->device);
+    HIPCHK(h, hipDeviceSynchronize());   // no step in flight reads the old block
+    h->cfg.track.reward_wrapper = reward_wrapper ? 1 : 0;
+    h->cfg.track.obs_wrapper = obs_wrapper;
+    const int rc = h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h);
+    return rc == ADRP_OK ? rc : seterr(h, rc, "constant block upload failed");
+}
+
 extern "C" int adrp_obs_dim(const adrp_t* h) { return h ? h->D : ADRP_ERR_INVALID; }
 extern "C" int adrp_act_dim(const adrp_t* h) { return h ? h->A : ADRP_ERR_INVALID; }
 
 extern "C" int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev, void* stream) {
     if (!h || !obs_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_reset: NULL argument");
-    HIPCHK(h, hipSetDevice(h->device));
+    DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     if (h->cfg.task == ADRP_TASK_RACE)
         return h->real_size == 8 ? race_reset<double>(h, env_mask_dev, obs_dev, s)
@@ -391,7 +417,7 @@ extern "C" int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float*
                          uint8_t* trunc_dev, float* terminal_obs_dev, void* stream) {
     if (!h || !act_dev || !obs_dev || !rew_dev || !term_dev || !trunc_dev)
         return seterr(h, ADRP_ERR_INVALID, "adrp_step: NULL argument");
-    HIPCHK(h, hipSetDevice(h->device));
+    DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     if (h->cfg.task == ADRP_TASK_RACE)
         return h->real_size == 8 ? race_step<double>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s)
@@ -485,7 +511,7 @@ extern "C" const char* adrp_state_field(const adrp_t* h, int is_int, int index) 
 
 extern "C" int adrp_get_state(adrp_t* h, void* f_dev, int32_t* i_dev, void* stream) {
     if (!h || !f_dev || !i_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_get_state: NULL argument");
-    HIPCHK(h, hipSetDevice(h->device));
+    DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t EN = size_t(h->E) * h->N, nb = h->nf_base * EN, nr = size_t(h->B) * h->A * h->E;
     HIPCHK(h, hipMemcpyAsync(f_dev, h->f, nb * h->real_size, hipMemcpyDeviceToDevice, s));
@@ -500,7 +526,7 @@ extern "C" int adrp_get_state(adrp_t* h, void* f_dev, int32_t* i_dev, void* stre
 
 extern "C" int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev, void* stream) {
     if (!h || !f_dev || !i_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_set_state: NULL argument");
-    HIPCHK(h, hipSetDevice(h->device));
+    DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t EN = size_t(h->E) * h->N, nb = h->nf_base * EN, nr = size_t(h->B) * h->A * h->E;
     HIPCHK(h, hipMemcpyAsync(h->f, f_dev, nb * h->real_size, hipMemcpyDeviceToDevice, s));
@@ -547,7 +573,7 @@ extern "C" int64_t adrp_step_bytes(const adrp_t* h) {
 // ---------------------------------------------------------------------------------------------
 extern "C" int adrp_profile_begin(adrp_t* h, int max_launches) {
     if (!h || max_launches < 0 || max_launches > (1 << 20)) return seterr(h, ADRP_ERR_INVALID, "max_launches");
-    HIPCHK(h, hipSetDevice(h->device));
+    DeviceGuard g(h->device);
     while ((int)h->ev_start.size() < max_launches) {
         hipEvent_t a, b;
         HIPCHK(h, hipEventCreate(&a));
@@ -562,7 +588,7 @@ extern "C" int adrp_profile_begin(adrp_t* h, int max_launches) {
 
 extern "C" int adrp_profile_end(adrp_t* h, float* kernel_ms, int cap) {
     if (!h) return ADRP_ERR_INVALID;
-    HIPCHK(h, hipSetDevice(h->device));
+    DeviceGuard g(h->device);
     const int n = std::min(h->prof_n, cap);
     for (int k = 0; k < n; ++k) {
         HIPCHK(h, hipEventSynchronize(h->ev_stop[k]));

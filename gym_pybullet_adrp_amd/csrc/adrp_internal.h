@@ -14,6 +14,8 @@
 #include "../../include/adrp.h"
 #include "hover_kernel.h"
 #include "race_kernel.h"
+#include "race_quad.h"
+#include "device_guard.h"
 
 using namespace adrp;
 
@@ -34,6 +36,7 @@ struct adrp_handle {
     bool stage_rows = true;       // LDS-staged obs rows when E % 64 == 0 (ADRP_STAGE_ROWS=0 disables)
     bool reset_helper = true;     // staged kernels: reset states from a helper wave (ADRP_RESET_HELPER=0)
     bool race_helpers = true;     // race fp32: helper waves (track copy, draws) (ADRP_RACE_HELPERS=0)
+    bool race_quad = true;        // race fp32: four lanes per drone (race_quad.h) (ADRP_RACE_QUAD=0: one lane)
     int diagnostics = 0;
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;

@@ -13,6 +13,7 @@
 
 #include "../../include/adrp.h"
 #include "policy_kernel.h"
+#include "device_guard.h"
 
 using namespace adrp;
 
@@ -123,7 +124,8 @@ extern "C" int adrp_policy_create(int device, int in_dim, int hidden1, int hidde
     p->in_dim = in_dim; p->h1 = hidden1; p->h2 = hidden2; p->relu = activation == ADRP_POLICY_RELU;
     if (const char* env = getenv("ADRP_POLICY_RT")) p->row_tiles = atoi(env);
     const std::vector<float> blob = build_blob(in_dim, hidden1, hidden2, w1, b1, w2, b2, w3, b3, &p->L);
-    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&p->blob, blob.size() * sizeof(float)) != hipSuccess) {
+    DeviceGuard g(device);
+    if (hipMalloc((void**)&p->blob, blob.size() * sizeof(float)) != hipSuccess) {
         delete p;
         return seterr(nullptr, ADRP_ERR_OOM, "hipMalloc failed");
     }
@@ -138,7 +140,7 @@ extern "C" int adrp_policy_create(int device, int in_dim, int hidden1, int hidde
 
 extern "C" void adrp_policy_destroy(adrp_policy_t* p) {
     if (!p) return;
-    hipSetDevice(p->device);
+    DeviceGuard g(p->device);
     hipDeviceSynchronize();
     hipFree(p->blob);
     delete p;
@@ -153,7 +155,7 @@ extern "C" int adrp_policy_act(adrp_policy_t* p, const float* obs_dev, int rows,
     if (mode == ADRP_POLICY_RELATIVE && p->in_dim < 6)
         return seterr(nullptr, ADRP_ERR_INVALID, "RELATIVE mode reads the pose from obs[0:3] and obs[5]");
     if (rows == 0) return ADRP_OK;
-    if (hipSetDevice(p->device) != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, "hipSetDevice failed");
+    DeviceGuard g(p->device);
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
     switch (p->h1 / 16) {

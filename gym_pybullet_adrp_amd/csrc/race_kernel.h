@@ -47,7 +47,7 @@ enum RaceInt { RI_STEP = 0, RI_EPISODE, RI_TICK, RI_LAST_ATT, RI_LAST_POS, RI_TU
 template <typename Real>
 struct RaceConst {
     int N, S, physics, link_lag, compete, num_gates, num_obstacles, trunc_steps;
-    int disturbances, reward_wrapper, random_gates, random_state, random_inertia, D, autoreset;
+    int disturbances, reward_wrapper, obs_wrapper, random_gates, random_state, random_inertia, D, autoreset;
     Real dt, gravity, kf, km, hover_unused;
     Real px[4], py[4], pz[4];
     Real gnd_kf, prop_r4, gnd_clip, drag[3], dw1, dw2, dw3, prop_r;
@@ -657,15 +657,17 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
 template <typename Real>
 __device__ __forceinline__ Real clamp100r(Real x) { return clampr_(x, Real(-100), Real(100)); }
 
+// Rq = rot(d.q), Rl = rot(d.ql) on entry; on return Rq = rot(new q), Rl = rot(new ql) (= the entry
+// Rq): a caller that carries both across sub-steps computes one rotation matrix per sub-step
 template <typename Real, int PH>
-__device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDrone<Real>& d, V3<Real> F_ext,
-                                                 V3<Real> T_ext) {
+__device__ __forceinline__ void race_pyb_substep_r(const RaceConst<Real>& C, RDrone<Real>& d, V3<Real> F_ext,
+                                                   V3<Real> T_ext, M3<Real>& Rq, M3<Real>& Rl) {
     constexpr bool GND = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
-    const M3<Real> R = rot(d.q);
+    const M3<Real> R = Rq;
     // cached link basis: GND modes refresh it (getLinkStates(computeForwardKinematics=1))
     // before the ground-effect forces, after the motor forces (BaseAviary.py:739-744)
-    const M3<Real> Rs = C.link_lag ? rot(d.ql) : R;
+    const M3<Real> Rs = C.link_lag ? Rl : R;
     Real sum_f = 0, t2 = 0;
     V3<Real> P = v3(Real(0), Real(0), Real(0));
 #pragma unroll
@@ -745,6 +747,14 @@ __device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDron
         d.pos.z -= low;
         if (d.vel.z < Real(0)) d.vel.z = Real(0);
     }
+    Rl = R;
+    Rq = Rn;
+}
+template <typename Real, int PH>
+__device__ __forceinline__ void race_pyb_substep(const RaceConst<Real>& C, RDrone<Real>& d, V3<Real> F_ext,
+                                                 V3<Real> T_ext) {
+    M3<Real> Rq = rot(d.q), Rl = rot(d.ql);
+    race_pyb_substep_r<Real, PH>(C, d, F_ext, T_ext, Rq, Rl);
 }
 
 template <typename Real>
@@ -951,7 +961,8 @@ struct TrackJobs {
     uint32_t res[kRaceBlock];
 };
 
-template <typename Real, class TS>
+// SH: lanes per drone = 1 << SH (race_quad.h: 4); every lane reads its drone's owner lane's result
+template <typename Real, class TS, int SH = 0>
 __device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds,
                                                  bool live, Real cut, Real ccut, uint32_t& gin, uint32_t& oin,
                                                  TrackJobs& q, int tl, int G, int N, int E) {
@@ -996,7 +1007,7 @@ __device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const
         }
     }
     __syncthreads();
-    const uint32_t r = q.res[tl];
+    const uint32_t r = q.res[(tl >> SH) << SH];
     gin |= r & 15u;
     oin |= (r >> 4) & 15u;
     return (r >> 8) & 1u;
@@ -1298,7 +1309,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     {
 #pragma clang fp contract(off)
         Real qs, qc;
-        sincos_(Real(av.w) * Real(0.5), &qs, &qc);          // get_quaternion_from_euler(0, 0, yaw)
+        // get_quaternion_from_euler(0, 0, yaw); DroneObservationWrapper zeroes the yaw (wrapper.py:51-57)
+        sincos_(Real(C.obs_wrapper ? 0.0f : av.w) * Real(0.5), &qs, &qc);
         const float qz = float(qs), qw = float(qc);
         const float yaw_deg = degf_(atan2f(2.0f * (qw * qz + 0.0f * 0.0f), 1 - 2 * (0.0f * 0.0f + qz * qz)));
         xc_x = cosf(radf_(yaw_deg));
@@ -1505,7 +1517,11 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
             all_fin &= grp_bcast_i<G>(myfin, k);
         }
     }
-    const bool te = all_done != 0;
+    // DroneObservationWrapper: terminated once drone 0's current gate >= 2 (wrapper.py:61-63)
+    const int gate_d0 = grp_bcast_i<G>(d.gate, 0);
+    const bool te_env = all_done != 0;
+    const bool te = te_env || (C.obs_wrapper && gate_d0 >= 2);
+    const bool te_rw = C.obs_wrapper == 1 ? te : te_env;   // what the RewardWrapper sees
     const bool tr = sc0 >= C.trunc_steps;   // step_counter / PYB_FREQ > episode_len_sec, before += S
     // ---- RewardWrapper (wrapper.py:121-186), drone 0 ----
     float reward = 0.0f;
@@ -1526,7 +1542,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
             }
             r_passed = Real(5);
         }
-        const Real r_col = (te && !all_fin) ? Real(-1) : Real(0), r_lab = (te && all_fin) ? Real(10) : Real(0);
+        const Real r_col = (te_rw && !all_fin) ? Real(-1) : Real(0), r_lab = (te_rw && all_fin) ? Real(10) : Real(0);
         const Real pxy = sqrt_((tgt[0] - prv[0]) * (tgt[0] - prv[0]) + (tgt[1] - prv[1]) * (tgt[1] - prv[1]));
         const Real cxy = sqrt_((tgt[0] - row0[0]) * (tgt[0] - row0[0]) + (tgt[1] - row0[1]) * (tgt[1] - row0[1]));
         const Real pz = fabs_(tgt[2] - prv[2]), cz = fabs_(tgt[2] - row0[2]);

@@ -1,0 +1,523 @@
+// race_quad.h — MultiRaceAviary env.step, fp32, four lanes per drone (gfx950).
+//
+// The one-lane kernel (race_kernel.h) puts a drone on a lane, so config 4 (16,384 drones) is 256
+// waves: one per CU, on one of its four SIMDs, each issuing one VALU instruction per 4 cycles
+// through a ~1000-instruction dependent chain per 500 Hz sub-step.  Here a drone owns a quad of
+// lanes (lane = 4 * drone + ql), so the same batch is 1024 waves, one per SIMD, and the chain of
+// each wave is shorter wherever the quad splits the work of one drone:
+//   * downwash: lane ql evaluates the partner drone ql (ds_bpermute of its position), the
+//     contributions are summed in partner order as in the one-lane loop;
+//   * Euler angles of the controller input: lane ql evaluates angle min(ql, 2) (one atan2 instead
+//     of three), and keeps that axis's rate history and 2-pole gyro filter state;
+//   * the PWM -> thrust -> noise -> RPM chain: lane ql runs motor ql, the firmware's thrust
+//     reorder [3,2,1,0] is one DPP quad mirror, the RPMs come back by DPP quad broadcasts;
+//   * the rotation matrices of the current and the cached link pose are carried across sub-steps
+//     (one quaternion -> matrix per sub-step instead of three);
+//   * the sub-step disturbance draws are made by the quad's lanes up front (sub-steps s = ql mod 4)
+//     into LDS, and the env's actual track is copied to LDS for the post-loop queries.
+// Everything else (the Bullet step, the firmware controllerMellinger, rays, obs, contacts,
+// reward, reset) runs redundantly on the quad's four lanes; lane ql = 0 owns the stores.  The
+// per-element arithmetic is the one-lane kernel's, operation for operation (the same functions
+// with the same contraction scopes), so the two layouts agree (tests/test_race_gpu.py
+// test_quad_matches_lane).
+#pragma once
+
+#include "race_kernel.h"
+
+namespace adrp {
+
+constexpr int kQuadDrones = kRaceBlock / 4;   // drones per 64-lane block
+
+// DPP quad moves (one VALU op): value of quad lane k (k must fold to a constant), and the mirror
+// lane 3 - ql
+__device__ __forceinline__ int qbc_i(int v, int k) {
+    switch (k) {
+        case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xf, 0xf, false);
+        case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xf, 0xf, false);
+        case 2: return __builtin_amdgcn_mov_dpp(v, 0xaa, 0xf, 0xf, false);
+        default: return __builtin_amdgcn_mov_dpp(v, 0xff, 0xf, 0xf, false);
+    }
+}
+__device__ __forceinline__ float qbc(float v, int k) { return __int_as_float(qbc_i(__float_as_int(v), k)); }
+__device__ __forceinline__ float qmirror(float v) {   // quad_perm [3, 2, 1, 0]
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x1b, 0xf, 0xf, false));
+}
+
+// value of drone k of this lane's env (its quad lane ql): the env's G quads are 4G <= 32 aligned
+// lanes, so ds_swizzle's bit mode (within 32 lanes: src = (lane & and) | or) addresses it without
+// an index register.  k must fold to a constant.
+template <int G>
+__device__ __forceinline__ int grpq_i(int v, int k) {
+    if constexpr (G == 1) {
+        return v;
+    } else {
+        constexpr int am = 31 & ~((G - 1) << 2);   // or_mask = 4k sits at bits [9:5] of the pattern
+        switch (k) {
+            case 0: return __builtin_amdgcn_ds_swizzle(v, am);
+            case 1: return __builtin_amdgcn_ds_swizzle(v, am | (1 << 7));
+            case 2: return __builtin_amdgcn_ds_swizzle(v, am | (2 << 7));
+            case 3: return __builtin_amdgcn_ds_swizzle(v, am | (3 << 7));
+            case 4: return __builtin_amdgcn_ds_swizzle(v, am | (4 << 7));
+            case 5: return __builtin_amdgcn_ds_swizzle(v, am | (5 << 7));
+            case 6: return __builtin_amdgcn_ds_swizzle(v, am | (6 << 7));
+            default: return __builtin_amdgcn_ds_swizzle(v, am | (7 << 7));
+        }
+    }
+}
+template <int G>
+__device__ __forceinline__ float grpq(float v, int k) { return __int_as_float(grpq_i<G>(__float_as_int(v), k)); }
+
+// this lane's controller Euler angle (axis a = min(ql, 2)) of euler_xyz_fast_u(q): the same
+// atan2 / asin expressions, one per lane; the rare gimbal-lock branch evaluates all three
+__device__ __forceinline__ float euler_axis_q4(Q4<float> q, int a) {
+    const float sarg = -2.0f * (q.x * q.z - q.w * q.y);
+    if (__builtin_expect(__any(fabs_(sarg) >= 0.99999f), 0)) {
+        const V3<float> r = euler_xyz_fast(q);
+        return a == 0 ? r.x : (a == 1 ? r.y : r.z);
+    }
+    const float sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
+    const float y0 = 2.0f * (q.y * q.z + q.w * q.x), x0 = squ - sqx - sqy + sqz;
+    const float y2 = 2.0f * (q.x * q.y + q.w * q.z), x2 = squ + sqx - sqy - sqz;
+    const float x1 = __builtin_amdgcn_sqrtf((1.0f - sarg) * (1.0f + sarg));   // fasin_(sarg)
+    const float yy = a == 0 ? y0 : (a == 1 ? sarg : y2), xx = a == 0 ? x0 : (a == 1 ? x1 : x2);
+    return fatan2_(yy, xx);
+}
+
+// MellingerControl.computeControl (154-262) for the quad: lane ql owns axis min(ql, 2) of the
+// rates / gyro filter (rpy_a, prv, l1, l2) and motor ql of the PWM chain (noise_m).  Same
+// arithmetic as mellinger_compute<float> (FP contraction off), split across the quad.
+__device__ __forceinline__ void mellinger_q4(RDrone<float>& d, const Lpf& lpf, const float sp[3], float xc_x,
+                                             float xc_y, float rpy_a, float& prv, float& l1, float& l2, float noise_m,
+                                             int ql, const M3<float>& Rq) {
+#pragma clang fp contract(off)
+    const float rate = (rpy_a - prv) * 500.0f;
+    prv = rpy_a;
+    const float acc_z = (d.vel.z - d.prev_vel[2]) * float(500.0 / 9.8) + 1.0f;
+    d.prev_vel[0] = d.vel.x; d.prev_vel[1] = d.vel.y; d.prev_vel[2] = d.vel.z;
+    const float g_a = lpf_apply(lpf, l1, l2, float(rate * 57.29577951308232f));
+    const float gyro[3] = {qbc(g_a, 0), qbc(g_a, 1), qbc(g_a, 2)};
+    float pwm;
+    if (acc_z < -0.5f) d.tumble += 1; else d.tumble = 0;
+    if (d.tumble >= 30) {
+        d.tick += 1;
+        pwm = 0.0f;
+    } else {
+        const int da = d.tick - d.last_att, dp = d.tick - d.last_pos, bit = d.tick - d.tick_base;
+        const bool att_due = (da >= 2) | ((da == 1) & (((d.att_bits >> bit) & 1u) != 0));
+        const bool pos_due = (dp >= 6) | ((dp == 5) & (((d.pos_bits >> bit) & 1u) != 0));
+        d.last_pos = (att_due & pos_due) ? d.tick : d.last_pos;
+        d.last_att = att_due ? d.tick : d.last_att;
+        if (att_due) {
+            float Rm[9];
+            const float sarg = -2.0f * (d.q.x * d.q.z - d.q.w * d.q.y);
+            Rm[0] = Rq.a00; Rm[1] = Rq.a01; Rm[2] = Rq.a02;
+            Rm[3] = Rq.a10; Rm[4] = Rq.a11; Rm[5] = Rq.a12;
+            Rm[6] = Rq.a20; Rm[7] = Rq.a21; Rm[8] = Rq.a22;
+            if (__builtin_expect(__any(!(fabs_(sarg) < 0.99999f)), 0)) {
+                if (!(fabs_(sarg) < 0.99999f)) {
+                    const V3<float> rpy = euler_xyz_fast(d.q);
+                    float sr, cr, sp_, cp, sy, cy;
+                    sincosf(rpy.x, &sr, &cr);
+                    sincosf(rpy.y, &sp_, &cp);
+                    sincosf(rpy.z, &sy, &cy);
+                    Rm[0] = cy * cp; Rm[1] = cy * sp_ * sr - sy * cr; Rm[2] = cy * sp_ * cr + sy * sr;
+                    Rm[3] = sy * cp; Rm[4] = sy * sp_ * sr + cy * cr; Rm[5] = sy * sp_ * cr - cy * sr;
+                    Rm[6] = -sp_; Rm[7] = cp * sr; Rm[8] = cp * cr;
+                }
+            }
+            const float pos[3] = {d.pos.x, d.pos.y, d.pos.z};
+            const float vel[3] = {d.vel.x, d.vel.y, d.vel.z};
+            mellinger_fw(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
+        }
+        d.tick += 1;
+        // _compute_pwms (423-442), motor ql of [t-r+p+y, t-r-p-y, t+r-p+y, t+r+p-y]
+        const float r = d.ctl[0] / 2.0f, p = d.ctl[1] / 2.0f, y = d.ctl[2], th = d.ctl[3];
+        const float m = ((th + (ql < 2 ? -r : r)) + ((ql == 0 || ql == 3) ? p : -p)) + ((ql & 1) ? -y : y);
+        const float x = clampr_(m, 0.0f, 65535.0f) * float(60.0 / 65535);
+        const float volts = -0.0006239f * x * x + 0.088f * x;
+        pwm = minr_(volts * float(1.0 / 3), 1.0f) * 65535.0f;
+    }
+    // clip -> thrust -> reorder [3,2,1,0] -> + noise -> _thr2pwm -> rpm (246-262)
+    const float rp = 0.2685f * clampr_(pwm, 20000.0f, 65535.0f) + 4070.3f;
+    const float thr = qmirror(3.16e-10f * rp * rp);
+    const float t = maxr_(thr + noise_m, 0.0f);
+    const float mp = clampr_((hsqrt_(t * float(1.0 / 3.16e-10)) - 4070.3f) * float(1.0 / 0.2685), 20000.0f, 65535.0f);
+    const float rnew = 0.2685f * mp + 4070.3f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        d.prev[k] = d.rpm[k];
+        d.rpm[k] = qbc(rnew, k);
+    }
+}
+
+// the block's LDS copy of its drones' env tracks, [field][drone] (owner lane l -> drone l / 4)
+struct TrackSrcQ {
+    const float* lds;
+    int qd;
+    __device__ __forceinline__ float operator()(int field) const { return lds[(field - RF_GATE) * kQuadDrones + qd]; }
+    __device__ __forceinline__ TrackSrcQ lane(int l, int, int, int) const { return TrackSrcQ{lds, l >> 2}; }
+};
+
+template <typename T3>
+__device__ __forceinline__ float sel3(const T3& v, int a) { return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]); }
+
+// Block = 64 lanes = 16 drones (kQuadDrones); one wave.  DRAWS: the disturbance draws of the
+// step's S <= kRacePreS sub-steps go through LDS (disturbances on); else none are needed, or (S
+// larger) each lane draws in the loop.
+template <int PH, int G, bool DRAWS>
+__global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
+    using Real = float;
+    RACE_MARK(t0);
+    const RaceConst<Real>& C = *a.c;
+    __shared__ float pre_draws[DRAWS ? kRacePreS * 7 * kQuadDrones : 1];   // [s][7][drone]
+    __shared__ float trk_lds[kTrackFields * kQuadDrones];                  // [field][drone]
+    __shared__ float4 rows4[kQuadDrones * kRaceMaxD / 4];
+    __shared__ TrackJobs tjobs;
+    const int tl = threadIdx.x;
+    const int ql = tl & 3, qd = tl >> 2;                 // quad lane, drone within the block
+    const int cax = ql < 3 ? ql : 2;                     // this lane's Euler axis
+    RaceConst<Real> H;
+    H.S = C.S; H.link_lag = C.link_lag; H.disturbances = C.disturbances;
+    H.dt = C.dt; H.gravity = C.gravity; H.kf = C.kf; H.km = C.km;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { H.px[i] = C.px[i]; H.py[i] = C.py[i]; H.pz[i] = C.pz[i]; }
+    H.gnd_kf = C.gnd_kf; H.prop_r4 = C.prop_r4; H.gnd_clip = C.gnd_clip;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        H.drag[i] = C.drag[i]; H.dist_lo[i] = C.dist_lo[i]; H.dist_hi[i] = C.dist_hi[i];
+        H.dyn_i[i] = C.dyn_i[i]; H.dyn_inv_i[i] = C.dyn_inv_i[i];
+    }
+    H.dw1 = C.dw1; H.dw2 = C.dw2; H.dw3 = C.dw3; H.prop_r = C.prop_r;
+    H.dyn_mass = C.dyn_mass; H.dyn_inv_mass = C.dyn_inv_mass; H.dyn_arm = C.dyn_arm;
+    H.coll_hh = C.coll_hh; H.coll_r = C.coll_r; H.coll_zoff = C.coll_zoff; H.ang_max = C.ang_max;
+    H.noise_std = C.noise_std;
+    const int dl = blockIdx.x * kQuadDrones + qd;        // drone lane of the one-lane layout
+    const int e_raw = dl / G, d_raw = dl % G;
+    const int N = C.N;
+    const bool active = e_raw < a.E && d_raw < N;
+    const bool owner = active && ql == 0;
+    const int e = e_raw < a.E ? e_raw : a.E - 1;
+    const int dn = d_raw < N ? d_raw : 0;
+    const size_t EN = size_t(a.E) * N;
+    const size_t slot = size_t(e) * N + dn;
+    const uint64_t gid = uint64_t(a.env_offset + e);
+    // the env's actual track: 7 of its 28 fields per lane, into LDS after the loop
+    float trk[(kTrackFields + 3) / 4];
+#pragma unroll
+    for (int i = 0; i < (kTrackFields + 3) / 4; ++i) {
+        const int k = ql + 4 * i;
+        trk[i] = k < kTrackFields ? ld(a.f, RF_GATE + k, EN, slot) : 0.0f;
+    }
+    RDrone<Real> d;
+    load_drone(a, EN, slot, d);
+    const int sc0 = a.ist[RI_STEP * EN + slot];
+    const int episode = a.ist[RI_EPISODE * EN + slot];
+    const uint32_t ep = uint32_t(episode - 1);
+    const float4 av = reinterpret_cast<const float4*>(a.act)[slot];
+    const float sp[3] = {av.x, av.y, av.z};
+    float xc_x, xc_y;
+    {
+#pragma clang fp contract(off)
+        Real qs, qc;
+        sincos_(Real(C.obs_wrapper ? 0.0f : av.w) * Real(0.5), &qs, &qc);   // DroneObservationWrapper: yaw 0
+        const float qz = float(qs), qw = float(qc);
+        const float yaw_deg = degf_(atan2f(2.0f * (qw * qz + 0.0f * 0.0f), 1 - 2 * (0.0f * 0.0f + qz * qz)));
+        xc_x = cosf(radf_(yaw_deg));
+        xc_y = sinf(radf_(yaw_deg));
+    }
+    Lpf lpf;
+    {
+#pragma clang fp contract(off)
+        const float fr = 500.0f / 30.0f;
+        const float ohm = tanf(3.14159265358979323846f / fr);
+        const float c = 1.0f + 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm;
+        lpf.b0 = ohm * ohm / c; lpf.b1 = 2.0f * lpf.b0; lpf.b2 = lpf.b0;
+        lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
+        lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
+    }
+    if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
+        for (int s = ql; s < H.S; s += 4) {
+            Real fd[3], nz[4];
+            race_substep_draws(H, a.seed, gid, ep, dn, uint32_t(sc0 + s), fd, nz);
+            float* dst = pre_draws + s * 7 * kQuadDrones + qd;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) dst[k * kQuadDrones] = fd[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dst[(3 + k) * kQuadDrones] = nz[k];
+        }
+        __syncthreads();
+    }
+    // lane-distributed controller state: axis cax of the rate history and the gyro filter
+    float prv = sel3(d.prev_rpy, cax), l1 = sel3(d.lpf1, cax), l2 = sel3(d.lpf2, cax);
+    M3<Real> Rq = rot(d.q), Rl = rot(d.ql);
+    RACE_MARK(t1);
+#ifdef ADRP_RACE_TIMING
+    uint64_t acc_phys = 0;
+#endif
+    for (int s0 = 0; s0 < H.S; s0 += 32) {
+    if (s0 > 0) {
+        d.tick_base = d.tick;
+        tick_window(a.ticks, d.tick, d.att_bits, d.pos_bits);
+    }
+    const int s1 = H.S < s0 + 32 ? H.S : s0 + 32;
+    for (int s = s0; s < s1; ++s) {
+#ifdef ADRP_RACE_TIMING
+        RACE_MARK(ta);
+#endif
+        const uint32_t idx = uint32_t(sc0 + s);
+        if (PH != ADRP_PHYS_PYB) d.kpos = d.pos;
+        float noise_m = 0.0f;
+        if constexpr (PH == ADRP_PHYS_DYN) {
+            race_dyn_substep(H, d);
+            Rq = rot(d.q);
+        } else {
+            V3<Real> Fx = v3(Real(0), Real(0), Real(0)), Tx = v3(Real(0), Real(0), Real(0));
+            if constexpr (PH == ADRP_PHYS_PYB_DW || PH == ADRP_PHYS_PYB_GND_DRAG_DW) {
+                // _downwash (BaseAviary.py:792-818): lane ql evaluates partner drones ql, ql + 4;
+                // the sum runs in partner order with the one-lane loop's fused update
+                float al[(G + 3) / 4], ex[(G + 3) / 4];
+#pragma unroll
+                for (int j = 0; j < (G + 3) / 4; ++j) {
+                    const int k = ql + 4 * j;
+                    const int src = (tl & ~(4 * G - 1)) + 4 * (k < G ? k : 0);
+                    const Real ox = __shfl(d.pos.x, src), oy = __shfl(d.pos.y, src), oz = __shfl(d.pos.z, src);
+                    const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
+                    const Real dxy = hsqrt_(dx * dx + dy * dy);
+                    al[j] = 0.0f;
+                    ex[j] = 0.0f;
+                    if (k < N && dz > Real(0) && dxy < Real(10)) {
+                        const Real kk = H.prop_r * rcp_(Real(4) * dz);
+                        al[j] = H.dw1 * kk * kk;
+                        const Real beta = H.dw2 * dz + H.dw3;
+                        const Real qq = dxy * rcp_(beta);
+                        ex[j] = fexp_(Real(-0.5) * qq * qq);
+                    }
+                }
+                Real fz = 0;
+#pragma unroll
+                for (int k = 0; k < G; ++k) fz -= qbc(al[k / 4], k % 4) * qbc(ex[k / 4], k % 4);
+                const M3<Real>& Rs = H.link_lag && !(PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? Rl : Rq;
+                Fx = fz * col2(Rs);
+            }
+            if (H.disturbances) {
+                V3<Real> fd;
+                if constexpr (DRAWS) {
+                    const float* src = pre_draws + s * 7 * kQuadDrones + qd;
+                    fd = v3(src[0], src[kQuadDrones], src[2 * kQuadDrones]);
+                    noise_m = src[(3 + ql) * kQuadDrones];
+                } else {
+                    Real f3[3], nz[4];
+                    race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, nz);
+                    fd = v3(f3[0], f3[1], f3[2]);
+                    noise_m = nz[0];
+#pragma unroll
+                    for (int k = 1; k < 4; ++k) noise_m = ql == k ? nz[k] : noise_m;
+                }
+                const V3<Real> lo = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? d.pos : d.lpos;
+                Fx = Fx + fd;
+                Tx = cross(d.kpos - lo, fd);
+            }
+            race_pyb_substep_r<Real, PH>(H, d, Fx, Tx, Rq, Rl);
+        }
+#ifdef ADRP_RACE_TIMING
+        RACE_MARK(tb);
+        acc_phys += tb - ta;
+#endif
+        d.kpos = d.pos;
+        if (d.flags & 1) {      // eliminated: motors off (233-235)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d.rpm[k] = d.prev[k] = Real(0);
+        } else {
+            mellinger_q4(d, lpf, sp, xc_x, xc_y, euler_axis_q4(d.q, cax), prv, l1, l2, noise_m, ql, Rq);
+        }
+    }
+    }
+    RACE_MARK(t2);
+    // gather the distributed controller state back (all lanes active)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        d.prev_rpy[k] = qbc(prv, k);
+        d.lpf1[k] = qbc(l1, k);
+        d.lpf2[k] = qbc(l2, k);
+    }
+#pragma unroll
+    for (int i = 0; i < (kTrackFields + 3) / 4; ++i) {
+        const int k = ql + 4 * i;
+        if (k < kTrackFields) trk_lds[k * kQuadDrones + qd] = trk[i];
+    }
+    __syncthreads();
+    const TrackSrcQ T{trk_lds, qd};
+    // ---- _gate_progress (471-506) ----
+    V3<Real> gpos[ADRP_MAX_DRONES];
+    Q4<Real> gq[ADRP_MAX_DRONES];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        gpos[k] = v3(grpq<G>(d.pos.x, k), grpq<G>(d.pos.y, k), grpq<G>(d.pos.z, k));
+        gq[k] = {grpq<G>(d.q.x, k), grpq<G>(d.q.y, k), grpq<G>(d.q.z, k), grpq<G>(d.q.w, k)};
+    }
+    const int gate0 = d.gate;
+    if (C.num_gates > 0 && gate0 < C.num_gates) {
+        const Real gx = T(RF_GATE + 4 * gate0), gy = T(RF_GATE + 4 * gate0 + 1);
+        const Real rotg = T(RF_GATE + 4 * gate0 + 3);
+        const Real h = C.gate_type[gate0] == 0 ? Real(1.0) : Real(0.525), half = Real(0.1875);
+        Real sn, cs;
+        sincos_(rotg, &sn, &cs);
+        const Real dx = Real(0.05) * cs, dy = Real(0.05) * sn;
+        const Real br = fabs_(C.coll_zoff) + hsqrt_(C.coll_r * C.coll_r + C.coll_hh * C.coll_hh) + Real(1e-5);
+        uint32_t near = 0;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const Real ex = gpos[k].x - gx, ey = gpos[k].y - gy;
+            const Real ta = fmaxr_(fabs_(cs * ex + sn * ey) - Real(0.15), Real(0)), tb = -sn * ex + cs * ey;
+            const Real tz = fmaxr_(fabs_(gpos[k].z - h) - half, Real(0));
+            if (k < N && ta * ta + tb * tb + tz * tz < br * br) near |= 1u << k;
+        }
+        bool passed = false;
+        for (int r = -3; r <= 3 && !passed && ((near >> dn) & 1u); ++r) {
+            const V3<Real> p0 = v3(gx + Real(r) * dx, gy + Real(r) * dy, h - half);
+            const V3<Real> p1 = v3(gx + Real(r) * dx, gy + Real(r) * dy, h + half);
+            Real best = Real(2);
+            int who = -1;
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if ((near >> k) & 1u) {
+                    const Shape<Real> sk = drone_shape(C, gpos[k], gq[k]);
+                    const Real fr = ray_cylinder(sk, p0, p1);
+                    if (fr < best) { best = fr; who = k; }
+                }
+            }
+            if (who == dn && best < Real(0.9999)) passed = true;
+        }
+        if (passed) d.gate += 1;
+    }
+    if (gate0 >= C.num_gates) d.flags |= 2;
+    RACE_MARK(t3);
+    // ---- obs row, elimination (674-698) ----
+    const V3<Real> wv = PH == ADRP_PHYS_DYN ? d.angv : d.w;
+    float* const rows = reinterpret_cast<float*>(rows4);
+    float* row = rows + ((qd / G) * N + dn) * C.D;
+    Real row0[15];
+    const Shape<Real> ds = drone_shape(C, d.pos, d.q);
+    uint32_t gin, oin;
+    bool crashed = track_query_wave<Real, TrackSrcQ, 2>(C, T, ds, owner, Real(0.45), Real(1e-6), gin, oin, tjobs, tl, G,
+                                                       N, a.E);
+    race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, owner, row0, gin, oin);
+    if (C.compete && owner) {
+        int idx = 0;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            if (k < N && k != dn) {
+                const V3<Real> orpy = euler_xyz_fast(gq[k]);
+                float* p = row + 49 + 6 * idx;
+                p[0] = gpos[k].x; p[1] = gpos[k].y; p[2] = gpos[k].z;
+                p[3] = orpy.x; p[4] = orpy.y; p[5] = orpy.z;
+                ++idx;
+            }
+        }
+    }
+    RACE_MARK(t4);
+    {
+        const M3<Real>& R = ds.R;
+        const Real low = ds.c.z - ds.h.z * fabs_(R.a22) - ds.r * sqrt_(R.a02 * R.a02 + R.a12 * R.a12);
+        if (low <= Real(1e-6)) crashed = true;
+        if (C.compete) {
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                if (k < N && k != dn && !crashed) {
+                    const V3<Real> dc = gpos[k] - d.pos;
+                    const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
+                    if (dot(dc, dc) < (Real(2) * dr + Real(1e-4)) * (Real(2) * dr + Real(1e-4))) {
+                        const Shape<Real> sk = drone_shape(C, gpos[k], gq[k]);
+                        crashed = gjk_within(ds, sk, Real(1e-6));
+                    }
+                }
+            }
+        }
+    }
+    RACE_MARK(t5);
+    const bool oob = fabs_(d.pos.x) > C.bounds[0] || fabs_(d.pos.y) > C.bounds[1] || fabs_(d.pos.z) > C.bounds[2];
+    const bool unstable = fabs_(wv.x) > Real(20) || fabs_(wv.y) > Real(20) || fabs_(wv.z) > Real(20);
+    if (oob || unstable || crashed) d.flags |= 1;
+    const int mydone = ((d.flags & 1) || (d.flags & 2)) ? 1 : 0, myfin = (d.flags & 2) ? 1 : 0;
+    int all_done = 1, all_fin = 1;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const int dk = grpq_i<G>(mydone, k), fk = grpq_i<G>(myfin, k);
+        if (k < N) {
+            all_done &= dk;
+            all_fin &= fk;
+        }
+    }
+    const int gate_d0 = grpq_i<G>(d.gate, 0);
+    const bool te_env = all_done != 0;
+    const bool te = te_env || (C.obs_wrapper && gate_d0 >= 2);   // DroneObservationWrapper (wrapper.py:61-63)
+    const bool te_rw = C.obs_wrapper == 1 ? te : te_env;
+    const bool tr = sc0 >= C.trunc_steps;
+    // ---- RewardWrapper (wrapper.py:121-186), drone 0 ----
+    float reward = 0.0f;
+    int wr_gate = a.ist[RI_WR_GATE * EN + slot];
+    if (C.reward_wrapper && dn == 0) {
+        const int gate_id = d.gate;
+        Real tgt[3] = {ld(a.f, RF_WR_TARGET, EN, slot), ld(a.f, RF_WR_TARGET + 1, EN, slot), ld(a.f, RF_WR_TARGET + 2, EN, slot)};
+        const Real prvp[3] = {ld(a.f, RF_WR_PREV, EN, slot), ld(a.f, RF_WR_PREV + 1, EN, slot), ld(a.f, RF_WR_PREV + 2, EN, slot)};
+        Real r_passed = 0;
+        if (gate_id > wr_gate % 4) {
+            wr_gate = gate_id;
+            if (gate_id < 4 && gate_id < C.num_gates) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) tgt[k] = g == gate_id ? row0[3 + 3 * g + k] : tgt[k];
+            }
+            r_passed = Real(5);
+        }
+        const Real r_col = (te_rw && !all_fin) ? Real(-1) : Real(0), r_lab = (te_rw && all_fin) ? Real(10) : Real(0);
+        const Real pxy = sqrt_((tgt[0] - prvp[0]) * (tgt[0] - prvp[0]) + (tgt[1] - prvp[1]) * (tgt[1] - prvp[1]));
+        const Real cxy = sqrt_((tgt[0] - row0[0]) * (tgt[0] - row0[0]) + (tgt[1] - row0[1]) * (tgt[1] - row0[1]));
+        const Real pz = fabs_(tgt[2] - prvp[2]), cz = fabs_(tgt[2] - row0[2]);
+        reward = float((pxy - cxy) + (pz - cz) + r_passed + r_col + r_lab);
+        if (owner)
+            for (int k = 0; k < 3; ++k) { st(a.f, RF_WR_TARGET + k, EN, slot, tgt[k]); st(a.f, RF_WR_PREV + k, EN, slot, row0[k]); }
+    }
+#ifdef ADRP_RACE_TIMING
+    RACE_MARK(t6);
+    if (threadIdx.x == 0) {
+        RACE_ACC(0, t1 - t0); RACE_ACC(1, acc_phys); RACE_ACC(2, (t2 - t1) - acc_phys); RACE_ACC(3, t3 - t2);
+        RACE_ACC(4, t4 - t3); RACE_ACC(5, t5 - t4); RACE_ACC(6, t6 - t5); RACE_ACC(7, t6 - t0); RACE_ACC(8, 1);
+    }
+#endif
+    if (owner) {
+        if (dn == 0) {
+            a.rew[e] = reward;
+            a.term[e] = te;
+            a.trunc[e] = tr;
+        }
+        if (C.autoreset && (te || tr)) {
+            if (a.tobs) {
+                float* trow = a.tobs + slot * size_t(C.D);
+                for (int k = 0; k < C.D; ++k) trow[k] = row[k];
+            }
+            race_reset_lane(a, C, e, dn, EN, slot, episode, row);
+        } else {
+            store_drone(a, EN, slot, d, false);
+            a.ist[RI_STEP * EN + slot] = sc0 + C.S;
+            if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
+        }
+    }
+    // ---- coalesced copy-out of the block's rows ----
+    __syncthreads();
+    const int e0 = blockIdx.x * (kQuadDrones / G);
+    const int ne = a.E - e0 < kQuadDrones / G ? a.E - e0 : kQuadDrones / G;
+    const int total = ne * N * C.D;
+    float* dst = a.obs + size_t(e0) * N * C.D;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        float4* dst4 = reinterpret_cast<float4*>(dst);
+        const int n4 = total >> 2;
+        for (int i = tl; i < n4; i += kRaceBlock) store_out(dst4 + i, rows4[i]);
+        for (int i = 4 * n4 + tl; i < total; i += kRaceBlock) dst[i] = rows[i];
+    } else {
+        for (int i = tl; i < total; i += kRaceBlock) dst[i] = rows[i];
+    }
+}
+
+}  // namespace adrp

@@ -115,10 +115,17 @@ class HoverAviary:
 
     # ---- gymnasium-style API, batched ----
     def reset(self, seed: int = None, options: dict = None, mask=None):
-        """Reset all envs (or those with mask[e] != 0). Returns (obs [E,1,D], info)."""
+        """Reset all envs (or those with mask[e] != 0); `seed` re-keys the random streams first.
+        Returns (obs [E,1,D], info)."""
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        if seed is not None:
+            # BaseAviary.reset(seed) reseeds np_random, then resets: here the Philox key of every env
+            # (a fresh env built with this seed gives the same episodes from here on)
+            if m is not None:
+                raise ValueError("reset(seed=...) re-keys every env: call it without a mask")
+            self.h.reseed(seed)
         self.h.reset(self._obs, m)
         return self._obs, {"answer": 42}
 

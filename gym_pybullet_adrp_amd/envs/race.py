@@ -114,10 +114,17 @@ class MultiRaceAviary:
 
     # ---- gymnasium-style API, batched ----
     def reset(self, seed: int = None, options: dict = None, mask=None):
-        """Reset all envs (or those with mask[e] != 0). Returns (obs [E,N,D], info)."""
+        """Reset all envs (or those with mask[e] != 0); `seed` re-keys the random streams first.
+        Returns (obs [E,N,D], info)."""
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        if seed is not None:
+            # BaseAviary.reset(seed) reseeds np_random, then resets: here the Philox key of every env
+            # (a fresh env built with this seed gives the same episodes from here on)
+            if m is not None:
+                raise ValueError("reset(seed=...) re-keys every env: call it without a mask")
+            self.h.reseed(seed)
         self.h.reset(self._obs, m)
         return self._obs, {"answer": 42}
 
@@ -133,6 +140,20 @@ class MultiRaceAviary:
 
     def close(self):
         self.h.close()
+
+    # ---- fused wrappers (utils/wrapper.py; gym_pybullet_adrp_amd.utils.wrapper) ----
+    @property
+    def reward_wrapper(self):
+        return bool(self.cfg.track.reward_wrapper)
+
+    @property
+    def obs_wrapper(self):
+        return int(self.cfg.track.obs_wrapper)
+
+    def set_wrappers(self, reward_wrapper: bool, obs_wrapper: int):
+        """RewardWrapper on/off; DroneObservationWrapper 0 off, 1 inside the RewardWrapper, 2 outside
+        (include/adrp.h adrp_set_wrappers).  Takes effect from the next step."""
+        self.h.set_wrappers(reward_wrapper, obs_wrapper)
 
     # ---- state ----
     @property

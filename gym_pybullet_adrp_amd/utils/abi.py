@@ -5,7 +5,7 @@ value adrp_default_config() writes into ``struct_size``.
 """
 import ctypes
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_DRONES = 8
 MAX_GATES = 4
 MAX_OBSTACLES = 4
@@ -68,6 +68,7 @@ class AdrpTrack(ctypes.Structure):
         ("race_mass", _d),
         ("race_inertia", _arr(_d, 3)),
         ("reward_wrapper", _i32),
+        ("obs_wrapper", _i32),
     ]
 
 

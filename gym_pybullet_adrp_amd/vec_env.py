@@ -36,6 +36,7 @@ class AviaryVecEnv(_VecEnvBase):
         self.render_mode = None
         self.as_torch = as_torch
         self._actions = None
+        self._seed = None
         if _VecEnvBase is not object:  # pragma: no cover
             _VecEnvBase.__init__(self, self.num_envs, self.observation_space, self.action_space)
 
@@ -45,7 +46,8 @@ class AviaryVecEnv(_VecEnvBase):
 
     # ---- VecEnv API ----
     def reset(self):
-        obs, _ = self.env.reset()
+        seed, self._seed = self._seed, None
+        obs, _ = self.env.reset(seed=seed)
         return self._out(obs).copy() if not self.as_torch else obs.clone()
 
     def step_async(self, actions):
@@ -77,7 +79,10 @@ class AviaryVecEnv(_VecEnvBase):
         self.env.close()
 
     def seed(self, seed=None):
-        return [None] * self.num_envs
+        """SB3 VecEnv.seed: applied at the next reset (one Philox key for the batch; envs differ by
+        their global env id)"""
+        self._seed = seed
+        return [seed] * self.num_envs
 
     def get_images(self):
         raise NotImplementedError("rendering is out of scope (DESIGN.md)")

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ADRP_ABI_VERSION 1
+#define ADRP_ABI_VERSION 2
 
 #define ADRP_MAX_DRONES 8
 #define ADRP_MAX_GATES 4      /* MultiRaceAviary._computeObs hard-codes 4 (MultiRaceAviary.py:591-651) */
@@ -115,6 +115,11 @@ typedef struct adrp_track {
     double race_inertia[3];
     int32_t reward_wrapper;                          /* 0: env reward (0, MultiRaceAviary.py:665-670);
                                                         1: RewardWrapper (utils/wrapper.py:121-186) */
+    int32_t obs_wrapper;                             /* DroneObservationWrapper (utils/wrapper.py:38-65):
+                                                        yaw actions forced to 0, terminated once drone 0's
+                                                        current gate >= 2.  0: off; 1: inside the
+                                                        RewardWrapper (its terminal terms see the early
+                                                        termination); 2: outside it */
 } adrp_track;
 
 typedef struct adrp_config {
@@ -170,6 +175,17 @@ const char* adrp_last_error(const adrp_t* h);
  * 49 / 49+6(N-1) Race) and action width A (4, 3 or 1). */
 int adrp_obs_dim(const adrp_t* h);
 int adrp_act_dim(const adrp_t* h);
+
+/* Re-key the handle's random streams (reset randomisation, level1-3 disturbances) as a fresh
+ * handle created with `seed` has them: sets the seed and zeroes every env's episode counter
+ * (stream-ordered).  Follow it with a full adrp_reset, as BaseAviary.reset(seed=...) reseeds and
+ * resets (envs/BaseAviary.py:223-258).  A captured graph keeps the seed it was captured with. */
+int adrp_reseed(adrp_t* h, uint64_t seed, void* stream);
+
+/* MultiRaceAviary only: switch the RewardWrapper / DroneObservationWrapper fused into the step
+ * (adrp_track.reward_wrapper / .obs_wrapper) on an existing handle, as wrapping the reference env
+ * with RewardWrapper(env) / DroneObservationWrapper(env) does (utils/wrapper.py).  Synchronises. */
+int adrp_set_wrappers(adrp_t* h, int reward_wrapper, int obs_wrapper);
 
 /* Reset the envs selected by env_mask_dev (uint8 [E], NULL = all) and write their
  * observations into obs_dev (float [E,N,D]); rows of unselected envs are left as is. */

@@ -74,6 +74,8 @@ uint32_t orc_config_size(void);
 /* 1: integrate the base without the spatial -> classical "+ w x v" term (probe of an unpinned
  * Bullet reading, tests/test_closed_form.py); 0 (default): the restatement */
 void orc_set_bullet_variant(int omit_wxv);
+/* DroneObservationWrapper termination (oracle/race.c obs_wrapper_term) */
+void orc_obs_wrapper_term(int mode, int term_env, int gate0, uint8_t* term, int* term_rw);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,7 @@ def _load():
     lib.orc_env_contact.restype = ctypes.c_uint8
     lib.orc_default_config.argtypes = [I, P]
     lib.orc_set_bullet_variant.argtypes = [I]
+    lib.orc_obs_wrapper_term.argtypes = [I, I, I, P, P]
     lib.orc_set_threads.argtypes = [I]
     lib.orc_get_threads.restype = I
     lib.orc_philox4x32_10.argtypes = [P, P, P]
@@ -218,6 +219,13 @@ def derived_constants(cfg):
 def set_threads(n):
     """OpenMP threads for the env loop of Oracle.step (1 = the scalar restatement)."""
     lib().orc_set_threads(int(n))
+
+
+def obs_wrapper_term(mode, term_env, gate0):
+    """DroneObservationWrapper termination -> (terminated, terminated as the RewardWrapper sees it)"""
+    t = ctypes.c_uint8(0); r = ctypes.c_int(0)
+    lib().orc_obs_wrapper_term(int(mode), int(term_env), int(gate0), ctypes.byref(t), ctypes.byref(r))
+    return bool(t.value), bool(r.value)
 
 
 def set_bullet_variant(omit_wxv):

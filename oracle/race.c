@@ -785,6 +785,18 @@ static double race_reward_wrapper(int* wr_gate, double target[3], double prev[3]
     return (pxy - cxy) + (pz - cz) + r_passed + r_col + r_lab;
 }
 
+/* DroneObservationWrapper.step (wrapper.py:61-63): terminated once self.env.current_gate[0] >= 2.
+   Stacked with the RewardWrapper, mode 1 = RewardWrapper(DroneObservationWrapper(env)) (the reward's
+   terminal terms see the early termination), 2 = DroneObservationWrapper(RewardWrapper(env)). */
+static void obs_wrapper_term(int mode, int term_env, int gate0, uint8_t* term, int* term_rw) {
+    const int early = mode && gate0 >= 2;
+    *term = (uint8_t)(term_env || early);
+    *term_rw = mode == 1 ? (term_env || early) : term_env;
+}
+void orc_obs_wrapper_term(int mode, int term_env, int gate0, uint8_t* term, int* term_rw) {
+    obs_wrapper_term(mode, term_env, gate0, term, term_rw);
+}
+
 static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, float* rew, uint8_t* term,
                           uint8_t* trunc, float* tobs_env) {
     const adrp_config* c = &o->cfg;
@@ -839,7 +851,8 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
             const float* a = act + (size_t)i * 4;
             double sp[3] = {a[0], a[1], a[2]};
             memcpy(d->prev_rpm, d->rpm, sizeof d->rpm);
-            mellinger_compute(d, sp, (double)a[3], pos, rpy, vel, noise, d->rpm);
+            /* DroneObservationWrapper.step zeroes the yaw of every ndarray action (wrapper.py:51-57) */
+            mellinger_compute(d, sp, t->obs_wrapper ? 0.0 : (double)a[3], pos, rpy, vel, noise, d->rpm);
         }
     }
     o->contact[e] = (uint8_t)touched;
@@ -858,13 +871,16 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
     int all_fin = 1;
     *term = (uint8_t)race_terminated(t, N, (const double(*)[3])pos, (const double(*)[3])angv, contact, elim, fin);
     for (int i = 0; i < N; ++i) { ds[i].elim = elim[i]; all_fin &= fin[i]; }
+    int term_rw;
+    obs_wrapper_term(t->obs_wrapper, *term, ds[0].gate, term, &term_rw);
     *trunc = (uint8_t)race_truncated(c, o->step_counter[e]);
     double r = 0;
     if (t->reward_wrapper) {
         renv_t* re = &o->re[e];
         /* info["task_completed"] does not exist in the reference (KeyError, Q23):
-           defined here as "every drone finished" */
-        r = race_reward_wrapper(&re->wr_gate, re->wr_target, re->wr_prev, row0, *term, all_fin);
+           defined here as "every drone finished".  RewardWrapper(DroneObservationWrapper(env))
+           (obs_wrapper 1) sees the wrapper's early termination, the other order (2) does not. */
+        r = race_reward_wrapper(&re->wr_gate, re->wr_target, re->wr_prev, row0, term_rw, all_fin);
     }
     *rew = (float)r;
     o->step_counter[e] += o->S;                /* (268) */

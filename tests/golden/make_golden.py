@@ -167,6 +167,11 @@ def install_stubs():
         def __init__(self, env):
             self.env = env
 
+        def __getattr__(self, name):   # gymnasium 0.28 (pyproject.toml:21): public attributes forward
+            if name.startswith("_") or name == "env":
+                raise AttributeError(f"accessing private attribute '{name}' is prohibited")
+            return getattr(self.env, name)
+
     class Box:
         def __init__(self, low, high, shape=None, dtype=np.float32):
             self.low = np.broadcast_to(np.asarray(low), shape) if shape else np.asarray(low)
@@ -657,6 +662,60 @@ def race_fixtures(pb, m):
     return out
 
 
+def obswrap_fixtures(pb, m):
+    """DroneObservationWrapper (utils/wrapper.py:38-65) on a scripted env: the in-place yaw zeroing
+    of ndarray actions, the early termination at current_gate[0] >= 2, and both stackings with the
+    RewardWrapper (the reward's terminal terms see the early termination only from outside)."""
+    rng = np.random.default_rng(21)
+    T, N = 30, 2
+
+    class _Scripted(sys.modules["gymnasium"].Env):
+        def __init__(self, seq, gates, obs0):
+            self.seq, self.gates, self.obs0, self.k = seq, gates, obs0, 0
+            self.current_gate = gates[0]
+        def reset(self, *a, **k):
+            self.k = 0
+            self.current_gate = self.gates[0]
+            return self.obs0, {}
+        def step(self, action):
+            r = self.seq[self.k]
+            self.current_gate = self.gates[self.k + 1]
+            self.k += 1
+            return r
+    obs_seq = np.zeros((T + 1, N, 49))
+    obs_seq[:, :, :12] = rng.uniform(-1, 1, (T + 1, N, 12))
+    obs_seq[:, :, 12:28] = np.tile(np.array(RACE_CFG["gates"])[:, [0, 1, 2, 5]].ravel(), (T + 1, N, 1))
+    gates = np.zeros((T + 1, N), int)
+    gates[:, 0] = [0] * 5 + [1] * 7 + [2] * 13 + [3] * 6      # drone 0 reaches gate 2 at step 12
+    gates[:, 1] = [0] * 9 + [1] * 22
+    obs_seq[:, :, 48] = gates
+    term_env = np.zeros(T, bool); term_env[[7, 22]] = True
+    seq = [(obs_seq[t + 1], 0.0, bool(term_env[t]), False, {"task_completed": False}) for t in range(T)]
+    acts = rng.uniform(-1, 1, (T, N, 4))
+    acts_after = np.zeros_like(acts)
+    term_out = np.zeros(T, bool)
+    W = m.wrapper
+    env = W.DroneObservationWrapper(_Scripted(seq, gates, obs_seq[0]))
+    env.reset()
+    for t in range(T):
+        a = acts[t].copy()
+        _, _, term_out[t], _, _ = env.step(a)
+        acts_after[t] = a
+    rew = {}
+    for name, make in (("inner", lambda e: W.RewardWrapper(W.DroneObservationWrapper(e))),
+                       ("outer", lambda e: W.DroneObservationWrapper(W.RewardWrapper(e)))):
+        env = make(_Scripted(seq, gates, obs_seq[0]))
+        env.reset()
+        r = []
+        for t in range(T):
+            if obs_seq[t + 1, 0, 48] >= 4:
+                break
+            r.append(env.step(acts[t].copy())[1])
+        rew[name] = np.array(r)
+    return dict(ow_obs=obs_seq, ow_gates=gates, ow_term_env=term_env, ow_act=acts, ow_act_after=acts_after,
+                ow_term=term_out, ow_rew_inner=rew["inner"], ow_rew_outer=rew["outer"])
+
+
 def pid_fixtures(pb, m):
     """DSLPIDControl (control/DSLPIDControl.py:82-259) and the HoverAviary PID / VEL /
     ONE_D_PID action types (BaseRLAviary.py:193-235), fully reference code."""
@@ -825,6 +884,12 @@ def main():
         np.savez_compressed(path, **px)
         print("wrote", path, len(px), "arrays")
         return
+    if os.environ.get("GOLDEN_ONLY") == "obswrap":
+        px = obswrap_fixtures(pb, m)
+        path = os.path.join(HERE, "obswrap_golden.npz")
+        np.savez_compressed(path, **px)
+        print("wrote", path, len(px), "arrays")
+        return
     if os.environ.get("GOLDEN_ONLY") == "pid":
         px = pid_fixtures(pb, m)
         path = os.path.join(HERE, "pid_golden.npz")
@@ -853,6 +918,10 @@ def main():
     print("wrote", path, len(px), "arrays")
     px = logger_fixtures(pb, m)
     path = os.path.join(HERE, "logger_golden.npz")
+    np.savez_compressed(path, **px)
+    print("wrote", path, len(px), "arrays")
+    px = obswrap_fixtures(pb, m)
+    path = os.path.join(HERE, "obswrap_golden.npz")
     np.savez_compressed(path, **px)
     print("wrote", path, len(px), "arrays")
 

@@ -127,16 +127,84 @@ def test_teacher_forced_step(physics):
 
 @pytest.mark.parametrize("physics", [Physics.PYB, Physics.DYN, Physics.PYB_GND_DRAG_DW])
 def test_fp64_kernel_tight(physics):
+    """the float64 kernel: states within 1e-9, and reward / terminated / truncated exactly (the flags
+    are threshold tests on a state that agrees to 1e-9; none of the sampled states sits that close)"""
     E = 512
     rng = np.random.default_rng(7)
     env, orc = pair(E, physics, precision="fp64", autoreset=False)
     random_states(rng, E, env, orc)
     for t in range(5):
         act = rng.uniform(-1, 1, (E, 1, 4)).astype(np.float32)
-        orc.step(act)
-        env.step(torch.from_numpy(act))
+        _, rew_o, te_o, tr_o, _ = orc.step(act)
+        _, rew_g, te_g, tr_g, _ = env.step(torch.from_numpy(act))
         torch.cuda.synchronize()
         compare_state(env, orc, 1e-9, active_fields(physics))
+        np.testing.assert_array_equal(te_g.cpu().numpy(), te_o)
+        np.testing.assert_array_equal(tr_g.cpu().numpy(), tr_o)
+        np.testing.assert_allclose(rew_g.cpu().numpy(), rew_o, rtol=1e-6, atol=1e-7)
+
+
+def test_benched_kernel_teacher_forced():
+    """the instantiation bench.py times (BASELINE config 2): hover_step<f32,PYB,A4,B15,cf2x> with
+    auto-reset and the helper wave, E = 4096, teacher-forced per env.step at the 1e-4 bar.  Envs that
+    end their episode in a step are reset in the same launch on both sides: their reset obs and the
+    terminal obs are compared instead (the next-episode state is a Philox draw, exact)."""
+    E = 4096
+    rng = np.random.default_rng(31)
+    noise = {"xyz": [0.1, 0.1, 0.1], "rpy": 0.05, "vel": 0.1, "omega": 0.1}
+    env, orc = pair(E, Physics.PYB, seed=2024, initial_xyzs=[0, 0, 1.0], init_noise=noise)
+    assert _lib.kernel_name(env.cfg) == "hover_step<f32,PYB,A4,B15,cf2x>" and env.cfg.autoreset == 1
+    env.reset()
+    orc.reset()
+    random_states(rng, E, env, orc, tilt=0.3)
+    resets = 0
+    for t in range(6):
+        act = rng.uniform(-1, 1, (E, 1, 4)).astype(np.float32)
+        obs_o, rew_o, te_o, tr_o, tobs_o = orc.step(act)
+        obs_g, rew_g, te_g, tr_g, info = env.step(torch.from_numpy(act))
+        torch.cuda.synchronize()
+        og = obs_g.cpu().numpy()
+        np.testing.assert_array_equal(te_g.cpu().numpy(), te_o)
+        done = te_o | tr_o
+        mism = (tr_g.cpu().numpy() != tr_o).sum()
+        assert mism <= 2, f"{mism} truncation flags differ"   # |roll| ~ 0.4 float rounding only
+        same = ~done & (tr_g.cpu().numpy() == tr_o)
+        for sl in (slice(0, 3), slice(3, 6), slice(6, 9), slice(9, 12)):
+            d = np.linalg.norm(og[same, 0, sl] - obs_o[same, 0, sl], axis=1)
+            assert (d / np.maximum(np.linalg.norm(obs_o[same, 0, sl], axis=1), 1e-3)).max() <= 1e-4
+        np.testing.assert_array_equal(og[..., 12:], obs_o[..., 12:])             # action ring
+        both = done & (tr_g.cpu().numpy() == tr_o)
+        resets += int(both.sum())
+        np.testing.assert_allclose(og[both], obs_o[both], rtol=1e-6, atol=1e-6)  # reset obs (Philox)
+        tg = info["terminal_observation"].cpu().numpy()
+        np.testing.assert_allclose(tg[both, :, :12], tobs_o[both, :, :12], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(rew_g.cpu().numpy()[same], rew_o[same], rtol=1e-4, atol=1e-5)
+        f, i = orc.get_state()
+        env.set_state(torch.from_numpy(f.astype(np.float32)), torch.from_numpy(i))
+        orc.set_state(f.astype(np.float32).astype(np.float64), i)
+    assert resets > 0
+
+
+@pytest.mark.parametrize("precision,rtol", [("fp32", 1e-4), ("fp64", 1e-9)])
+def test_single_env(precision, rtol):
+    """BASELINE configs[0]: one HoverAviary env (E = 1, a 64-lane block with one live lane),
+    free-running 100 env.steps from the reference default start against the oracle"""
+    env, orc = pair(1, Physics.PYB, precision=precision, autoreset=False)
+    o_g, _ = env.reset()
+    o_o = orc.reset()
+    np.testing.assert_allclose(o_g.cpu().numpy(), o_o, atol=1e-6)
+    rng = np.random.default_rng(12)
+    for t in range(100):
+        act = rng.uniform(-0.2, 0.6, (1, 1, 4)).astype(np.float32)
+        obs_o, rew_o, te_o, tr_o, _ = orc.step(act)
+        obs_g, rew_g, te_g, tr_g, _ = env.step(torch.from_numpy(act))
+        if t % 10 == 0:
+            compare_state(env, orc, rtol, active_fields(Physics.PYB))
+        f, i = orc.get_state()
+        real = np.float64 if precision == "fp64" else np.float32
+        env.set_state(torch.from_numpy(f.astype(real)), torch.from_numpy(i))
+        orc.set_state(f.astype(real).astype(np.float64), i)
+        assert bool(te_g[0]) == bool(te_o[0]) and bool(tr_g[0]) == bool(tr_o[0])
 
 
 def test_free_running_and_autoreset():

@@ -339,3 +339,158 @@ def test_helper_waves_bit_identical(monkeypatch, E, N, level, physics, mode):
         outs.append(torch.stack(seq))
         env.close()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_obs_wrapper_autoreset(mode):
+    """DroneObservationWrapper fused into the kernel (utils/wrapper.py:38-65) with the RewardWrapper
+    stacked inside (mode 2) or outside (mode 1): yaw actions ignored, envs whose drone 0 is at gate
+    >= 2 terminate in the same launch and auto-reset; rewards, flags and reset obs match the oracle."""
+    from gym_pybullet_adrp_amd.utils.wrapper import DroneObservationWrapper, RewardWrapper
+    E, N = 64, 2
+    env = MultiRaceAviary("level0", num_drones=N, num_envs=E, seed=13, autoreset=True)
+    wenv = RewardWrapper(DroneObservationWrapper(env)) if mode == 1 else DroneObservationWrapper(RewardWrapper(env))
+    assert (env.reward_wrapper, env.obs_wrapper) == (True, mode)
+    orc = O.Oracle(env.cfg.copy())
+    assert orc.cfg.track.obs_wrapper == mode and orc.cfg.track.reward_wrapper == 1
+    wenv.reset()
+    obs0 = orc.reset()
+    rng = np.random.default_rng(6)
+    act = targets(rng, obs0, E, N)
+    act[..., 3] = rng.uniform(-3, 3, (E, N))            # ignored by the wrapper
+    for _ in range(8):
+        orc.step(act)
+    sync(env, orc)
+    f, i = orc.get_state()
+    names, inames = orc.field_names()
+    g = i[inames.index("gate")].reshape(E, N)
+    g[::3, 0] = 2                                         # a third of the envs: drone 0 past gate 2
+    i[inames.index("gate")] = g.ravel()
+    orc.set_state(f, i)
+    env.set_state(torch.from_numpy(f.astype(np.float32)), torch.from_numpy(i))
+    for k in range(3):
+        obs_o, rew_o, te_o, tr_o, tobs_o = orc.step(act)
+        obs_g, rew_g, te_g, tr_g, info = wenv.step(torch.from_numpy(act).to(env.device))
+        te = te_g.cpu().numpy()
+        np.testing.assert_array_equal(te, te_o)
+        if k == 0:
+            assert te[::3].all()
+        np.testing.assert_allclose(rew_g.cpu().numpy(), rew_o, rtol=1e-3, atol=1e-4)
+        if te_o.any():
+            np.testing.assert_allclose(obs_g.cpu().numpy()[te_o], obs_o[te_o], atol=2e-6)     # reset obs
+            np.testing.assert_allclose(info["terminal_observation"].cpu().numpy()[te_o][..., :3],
+                                       tobs_o[te_o][..., :3], rtol=1e-3, atol=1e-3)
+        sync(env, orc)
+    env.close()
+
+
+@pytest.mark.parametrize("E,N,level,physics,mode", [(2048, 2, "level0", Physics.PYB, RaceMode.COMPARE),
+                                                    (4096, 4, "level3", Physics.PYB_DW, RaceMode.COMPETE)])
+def test_full_size_subset_vs_oracle(E, N, level, physics, mode):
+    """BASELINE configs 3 / 4 at full size: after 0.8 s of flight on the GPU, 48 random envs are
+    teacher-forced one env.step against the oracle (one single-env oracle per sampled env, keyed by
+    its global env id, so the level3 disturbance draws are the same): state within the closed-loop
+    2e-3 bar, gates / ticks / step counters exact, elimination only at grazing contacts."""
+    rng = np.random.default_rng(17)
+    env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=7, autoreset=False)
+    obs, _ = env.reset()
+    act = targets(rng, obs.cpu().numpy(), E, N)
+    at = torch.from_numpy(act).to(env.device)
+    for _ in range(20):
+        env.step(at)
+    f, i = env.get_state()
+    f, i = f.double().cpu().numpy(), i.cpu().numpy()
+    sub = np.sort(rng.choice(E, 48, replace=False))
+    orcs = []
+    for e in sub:
+        c = env.cfg.copy()
+        c.num_envs, c.env_offset = 1, int(e)
+        o = O.Oracle(c)
+        o.reset()
+        sl = slice(e * N, (e + 1) * N)
+        o.set_state(np.ascontiguousarray(f[:, sl]), np.ascontiguousarray(i[:, sl]))
+        o.step(act[e:e + 1])
+        orcs.append(o)
+    env.step(at)
+    fg, ig = env.get_state()
+    fg, ig = fg.double().cpu().numpy(), ig.cpu().numpy()
+    names, inames = orcs[0].field_names()
+    idx = {n: k for k, n in enumerate(names)}
+    for o, e in zip(orcs, sub):
+        fo, io = o.get_state()
+        sl = slice(e * N, (e + 1) * N)
+        for g, fields in GROUPS.items():
+            rows = [idx[n] for n in fields]
+            err = np.linalg.norm(fg[rows, sl] - fo[rows], axis=0) / np.maximum(np.linalg.norm(fo[rows], axis=0), FLOORS[g])
+            assert err.max() <= RTOL["fp32"], f"env {e} {g}: {err.max():.3e}"
+        for k in ("step_counter", "episode", "gate", "tick", "last_att_tick", "last_pos_tick"):
+            np.testing.assert_array_equal(ig[inames.index(k), sl], io[inames.index(k)], err_msg=f"env {e} {k}")
+        kf = inames.index("flags")
+        for n in np.flatnonzero(ig[kf, sl] != io[kf]):
+            assert abs(contact_margin(o.cfg, fo, names, n)) < 1e-4, f"env {e} drone {n}: flags differ"
+    env.close()
+
+
+@pytest.mark.parametrize("level,N,physics,mode", [("level0", 2, Physics.PYB, RaceMode.COMPARE),
+                                                  ("level3", 4, Physics.PYB_DW, RaceMode.COMPETE),
+                                                  ("level2", 3, Physics.PYB_GND_DRAG_DW, RaceMode.COMPETE)])
+def test_quad_matches_lane(monkeypatch, level, N, physics, mode):
+    """the fp32 race step in its two layouts, four lanes per drone (default, race_quad.h) and one
+    (ADRP_RACE_QUAD=0), teacher-forced from the same states: the per-element arithmetic is the same,
+    so one env.step agrees to float rounding and every discrete output is identical"""
+    E = 256
+    rng = np.random.default_rng(23)
+    orc = None
+    outs = []
+    for quad in ("1", "0"):
+        monkeypatch.setenv("ADRP_RACE_QUAD", quad)
+        env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=3,
+                              autoreset=True, reward="wrapper")
+        if orc is None:
+            orc = O.Oracle(env.cfg.copy())
+            obs0 = orc.reset()
+            act = targets(rng, obs0, E, N)
+            for _ in range(15):
+                orc.step(act)
+            f, i = orc.get_state()
+            f = f.astype(np.float32)
+        env.reset()
+        env.set_state(torch.from_numpy(f), torch.from_numpy(i))
+        o, r, te, tr, _ = env.step(torch.from_numpy(act).to(env.device))
+        fs, is_ = env.get_state()
+        outs.append((o.cpu().numpy().copy(), r.cpu().numpy().copy(), te.cpu().numpy().copy(), tr.cpu().numpy().copy(),
+                     fs.cpu().numpy(), is_.cpu().numpy()))
+        env.close()
+    (o1, r1, te1, tr1, f1, i1), (o0, r0, te0, tr0, f0, i0) = outs
+    np.testing.assert_array_equal(i1, i0)
+    np.testing.assert_array_equal(te1, te0)
+    np.testing.assert_array_equal(tr1, tr0)
+    np.testing.assert_array_equal(o1[..., 28:32], o0[..., 28:32])
+    np.testing.assert_array_equal(o1[..., 44:49], o0[..., 44:49])
+    np.testing.assert_allclose(o1, o0, rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(r1, r0, rtol=1e-3, atol=1e-4)
+
+
+def test_reset_seed_rekeys():
+    """reset(seed=s) gives the episodes a fresh env built with seed=s gives (BaseAviary.reset(seed)
+    reseeds np_random; here the Philox key and the episode counters), bit for bit"""
+    E, N = 64, 2
+    a = MultiRaceAviary("level3", num_drones=N, num_envs=E, seed=5, autoreset=True)
+    b = MultiRaceAviary("level3", num_drones=N, num_envs=E, seed=9, autoreset=True)
+    oa, _ = a.reset()
+    oa = oa.clone()
+    ob, _ = b.reset()
+    act = torch.from_numpy(targets(np.random.default_rng(1), oa.cpu().numpy(), E, N)).to(a.device)
+    for _ in range(3):
+        b.step(act)
+    ob, _ = b.reset(seed=5)
+    assert torch.equal(oa, ob)
+    for _ in range(10):
+        ra, rb = a.step(act), b.step(act)
+        assert torch.equal(ra[0], rb[0]) and torch.equal(ra[2], rb[2])
+    oc, _ = b.reset(seed=6)
+    assert not torch.equal(oc, oa)
+    with pytest.raises(ValueError):
+        b.reset(seed=5, mask=torch.ones(E, dtype=torch.uint8))
+    a.close()
+    b.close()

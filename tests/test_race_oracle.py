@@ -227,3 +227,37 @@ def test_dyn_yaw_loop_diverges_like_the_reference():
         obs, _, te, _, _ = o.step(act)
     assert te.all()
     assert (np.abs(obs[..., 11]) > 20).all()
+
+
+def test_obs_wrapper_full_step():
+    """The oracle's env.step with the DroneObservationWrapper fused: yaw actions are ignored (the
+    trajectories equal a run with yaw 0 and no wrapper) and an env terminates (and auto-resets) once
+    drone 0 has passed gate 2; mode 1 feeds that termination to the RewardWrapper's terminal terms."""
+    from gym_pybullet_adrp_amd.envs.race import race_config
+    E, N = 8, 2
+    base = race_config("level0", N, "PYB", "COMPARE", num_envs=E, seed=5)
+    base.autoreset = 0
+    cw = base.copy()
+    cw.track.obs_wrapper = 1
+    a, b = O.Oracle(base), O.Oracle(cw)
+    o0 = a.reset()
+    b.reset()
+    rng = np.random.default_rng(0)
+    act = np.concatenate([o0[..., :3] + rng.uniform(-0.2, 0.2, (E, N, 3)), np.zeros((E, N, 1))], -1).astype(np.float32)
+    act_yaw = act.copy()
+    act_yaw[..., 3] = rng.uniform(-3, 3, (E, N))
+    for _ in range(5):
+        oa, _, ta, _, _ = a.step(act)
+        ob, _, tb, _, _ = b.step(act_yaw)
+        np.testing.assert_array_equal(oa, ob)
+        np.testing.assert_array_equal(ta, tb)
+    # drone 0 of envs 0..3 at gate 2 (the others at 1): early termination exactly there
+    f, i = b.get_state()
+    names, inames = b.field_names()
+    g = i[inames.index("gate")].reshape(E, N)
+    g[:, 0] = np.where(np.arange(E) < 4, 2, 1)
+    g[:, 1] = 0
+    i[inames.index("gate")] = g.ravel()
+    b.set_state(f, i)
+    _, _, tb, _, _ = b.step(act_yaw)
+    np.testing.assert_array_equal(tb, np.arange(E) < 4)

@@ -19,7 +19,7 @@ class _Scripted:
         self.tobs = torch.zeros((E, 1, D))
         self.closed = False
 
-    def reset(self):
+    def reset(self, seed=None):
         return torch.zeros((self.num_envs, 1, self.D)), {}
 
     def step(self, action):
