@@ -416,13 +416,17 @@ def test_full_size_subset_vs_oracle(E, N, level, physics, mode):
     fg, ig = fg.double().cpu().numpy(), ig.cpu().numpy()
     names, inames = orcs[0].field_names()
     idx = {n: k for k, n in enumerate(names)}
+    # the firmware's int16 moment truncation carries O(1e-4) rad/s differences through the step (module
+    # docstring); over 192 sampled drones some hover with |omega| ~ 1e-2, so omega gets a 0.1 rad/s floor
+    floors = dict(FLOORS, omega=0.1)
     for o, e in zip(orcs, sub):
         fo, io = o.get_state()
         sl = slice(e * N, (e + 1) * N)
         for g, fields in GROUPS.items():
             rows = [idx[n] for n in fields]
-            err = np.linalg.norm(fg[rows, sl] - fo[rows], axis=0) / np.maximum(np.linalg.norm(fo[rows], axis=0), FLOORS[g])
-            assert err.max() <= RTOL["fp32"], f"env {e} {g}: {err.max():.3e}"
+            err = np.linalg.norm(fg[rows, sl] - fo[rows], axis=0) / np.maximum(np.linalg.norm(fo[rows], axis=0), floors[g])
+            assert err.max() <= RTOL["fp32"], (f"env {e} {g}: {err.max():.3e}; flags {io[inames.index('flags')]} "
+                                               f"gpu {fg[rows, sl].T} cpu {fo[rows].T} z {fo[idx['pos_z']]}")
         for k in ("step_counter", "episode", "gate", "tick", "last_att_tick", "last_pos_tick"):
             np.testing.assert_array_equal(ig[inames.index(k), sl], io[inames.index(k)], err_msg=f"env {e} {k}")
         kf = inames.index("flags")
@@ -485,11 +489,16 @@ def test_reset_seed_rekeys():
         b.step(act)
     ob, _ = b.reset(seed=5)
     assert torch.equal(oa, ob)
+    assert torch.equal(a.get_state()[0], b.get_state()[0]) and torch.equal(a.get_state()[1], b.get_state()[1])
     for _ in range(10):
         ra, rb = a.step(act), b.step(act)
         assert torch.equal(ra[0], rb[0]) and torch.equal(ra[2], rb[2])
-    oc, _ = b.reset(seed=6)
-    assert not torch.equal(oc, oa)
+    # the reset obs is computed at the nominal poses (MultiRaceAviary.py:127-167), so it does not show
+    # the randomisation: the states do
+    b.reset(seed=5)
+    fa0 = b.get_state()[0].clone()
+    b.reset(seed=6)
+    assert not torch.equal(b.get_state()[0], fa0)
     with pytest.raises(ValueError):
         b.reset(seed=5, mask=torch.ones(E, dtype=torch.uint8))
     a.close()
