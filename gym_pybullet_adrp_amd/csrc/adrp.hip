@@ -199,6 +199,18 @@ static RaceConst<Real> race_const(const adrp_config& c) {
     k.disturbances = t.disturbances ? 1 : 0;
     k.reward_wrapper = t.reward_wrapper ? 1 : 0;
     k.obs_wrapper = t.obs_wrapper == 1 || t.obs_wrapper == 2 ? t.obs_wrapper : 0;
+    {   // lpf2pInit(gyrolpf, 500, 30): the firmware's filter.c in C float (host libm, no contraction:
+        // the same values the oracle's restatement computes)
+#pragma clang fp contract(off)
+        const float fr = 500.0f / 30.0f;
+        const float ohm = tanf(3.14159265358979323846f / fr);
+        const float cc = 1.0f + 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm;
+        k.lpf[0] = ohm * ohm / cc;
+        k.lpf[1] = 2.0f * k.lpf[0];
+        k.lpf[2] = k.lpf[0];
+        k.lpf[3] = 2.0f * (ohm * ohm - 1.0f) / cc;
+        k.lpf[4] = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / cc;
+    }
     k.random_gates = t.random_gates_obstacles ? 1 : 0;
     k.random_state = t.random_drone_state ? 1 : 0;
     k.random_inertia = t.random_drone_inertia ? 1 : 0;
@@ -625,6 +637,9 @@ extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
     }
     return ADRP_OK;
 }
+// per-workgroup phases of the fp32 four-lane race kernel: n slots of [setup, physics, controller,
+// rays, obs, contacts, tail, total] s_memtime cycles (RACE_WAVE), written by the last launch
+extern "C" int adrp_race_wave_read(unsigned long long* out, int n) { return wave_read_race_f32(out, n); }
 #endif
 
 extern "C" int adrp_diagnostic_contact_count(adrp_t* h, int reset) {

@@ -30,10 +30,16 @@ __device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-p
 #define RACE_SET(var) var = __builtin_amdgcn_s_memtime()
 #define RACE_ACC(i, dt) do { atomicAdd(&g_race_phase[i], (unsigned long long)(dt)); \
         atomicMax(&g_race_phase[10 + (i)], (unsigned long long)(dt)); } while (0)
+// race kernels: one slot of 8 phases per workgroup, plain stores (the same-address atomics of
+// RACE_ACC from 1024 waves serialise in L2 and stretch the phases they are meant to measure)
+constexpr int kWaveSlots = 16384;
+__device__ unsigned long long g_race_wave[kWaveSlots * 8];
+#define RACE_WAVE(i, dt) do { if (blockIdx.x < kWaveSlots) g_race_wave[blockIdx.x * 8 + (i)] = (unsigned long long)(dt); } while (0)
 #else
 #define RACE_MARK(var)
 #define RACE_SET(var)
 #define RACE_ACC(i, dt)
+#define RACE_WAVE(i, dt)
 #endif
 
 

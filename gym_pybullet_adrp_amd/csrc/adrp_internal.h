@@ -117,6 +117,7 @@ int phase_read_hover_f32(unsigned long long* out, int reset);
 int phase_read_hover_f64(unsigned long long* out, int reset);
 int phase_read_race_f32(unsigned long long* out, int reset);
 int phase_read_race_f64(unsigned long long* out, int reset);
+int wave_read_race_f32(unsigned long long* out, int n);
 #define ADRP_PHASE_READER(name)                                                                  \
     int name(unsigned long long* out, int reset) {                                               \
         if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_race_phase), 32 * sizeof(unsigned long long)) != hipSuccess) \
@@ -126,5 +127,11 @@ int phase_read_race_f64(unsigned long long* out, int reset);
             if (hipMemcpyToSymbol(HIP_SYMBOL(g_race_phase), z, sizeof z) != hipSuccess) return ADRP_ERR_DEVICE; \
         }                                                                                        \
         return ADRP_OK;                                                                          \
+    }
+#define ADRP_WAVE_READER(name)                                                                   \
+    int name(unsigned long long* out, int n) {                                                   \
+        if (n < 0 || n > kWaveSlots) return ADRP_ERR_INVALID;                                    \
+        return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_race_wave), size_t(n) * 8 * sizeof(unsigned long long)) \
+                       == hipSuccess ? ADRP_OK : ADRP_ERR_DEVICE;                                 \
     }
 #endif

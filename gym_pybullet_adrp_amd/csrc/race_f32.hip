@@ -7,4 +7,5 @@ template int race_reset<float>(adrp_t*, const uint8_t*, float*, hipStream_t);
 
 #ifdef ADRP_RACE_TIMING
 ADRP_PHASE_READER(phase_read_race_f32)
+ADRP_WAVE_READER(wave_read_race_f32)
 #endif

@@ -62,6 +62,7 @@ struct RaceConst {
     Real init_pos[ADRP_MAX_DRONES][3], init_rpy[ADRP_MAX_DRONES][3], init_vel[ADRP_MAX_DRONES][3],
         init_pqr[ADRP_MAX_DRONES][3];
     Real race_mass, race_inertia[3];
+    float lpf[5];   // gyro lpf2p b0, b1, b2, a1, a2 (host float, as the firmware's filter.c computes them)
 };
 
 template <typename Real>
@@ -401,7 +402,8 @@ __device__ __forceinline__ Real ld(const Real* f, int field, size_t EN, size_t s
 template <typename Real>
 __device__ __forceinline__ void st(Real* f, int field, size_t EN, size_t slot, Real v) { f[size_t(field) * EN + slot] = v; }
 
-template <typename Real>
+// TW: also load the tick-schedule window (a caller that issued it early passes false and sets it)
+template <typename Real, bool TW = true>
 __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, size_t slot, RDrone<Real>& d) {
     const Real* f = a.f;
 #define L_(k) ld(f, (k), EN, slot)
@@ -430,8 +432,10 @@ __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, s
     d.tick = ist[RI_TICK * EN + slot]; d.last_att = ist[RI_LAST_ATT * EN + slot];
     d.last_pos = ist[RI_LAST_POS * EN + slot]; d.tumble = ist[RI_TUMBLE * EN + slot];
     d.gate = ist[RI_GATE * EN + slot]; d.flags = ist[RI_FLAGS * EN + slot];
-    d.tick_base = d.tick;
-    tick_window(a.ticks, d.tick, d.att_bits, d.pos_bits);
+    if constexpr (TW) {
+        d.tick_base = d.tick;
+        tick_window(a.ticks, d.tick, d.att_bits, d.pos_bits);
+    }
     d.inv_mass = Real(1) / d.mass;
 #pragma unroll
     for (int k = 0; k < 3; ++k) d.inv_i[k] = Real(1) / d.inertia[k];
@@ -961,13 +965,13 @@ struct TrackJobs {
     uint32_t res[kRaceBlock];
 };
 
+// the GJK part of track_query_wave for the bounds pass's result (gin, oin, amb, camb_all).
 // SH: lanes per drone = 1 << SH (race_quad.h: 4); every lane reads its drone's owner lane's result
 template <typename Real, class TS, int SH = 0>
-__device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds,
-                                                 bool live, Real cut, Real ccut, uint32_t& gin, uint32_t& oin,
-                                                 TrackJobs& q, int tl, int G, int N, int E) {
-    uint32_t amb, camb_all;
-    track_bounds(C, T, ds, cut, true, ccut, gin, oin, amb, camb_all);
+__device__ __forceinline__ bool track_gjk_pool(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds,
+                                               bool live, Real cut, Real ccut, uint32_t& gin, uint32_t& oin,
+                                               uint32_t amb, uint32_t camb_all, TrackJobs& q, int tl, int G, int N,
+                                               int E) {
     if (!live) amb = 0;
     const int n = __popc(amb);
     int incl = n;   // inclusive scan of the queue lengths
@@ -1012,6 +1016,14 @@ __device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const
     oin |= (r >> 4) & 15u;
     return (r >> 8) & 1u;
 }
+template <typename Real, class TS>
+__device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds,
+                                                 bool live, Real cut, Real ccut, uint32_t& gin, uint32_t& oin,
+                                                 TrackJobs& q, int tl, int G, int N, int E) {
+    uint32_t amb, camb_all;
+    track_bounds(C, T, ds, cut, true, ccut, gin, oin, amb, camb_all);
+    return track_gjk_pool<Real, TS, 0>(C, T, ds, live, cut, ccut, gin, oin, amb, camb_all, q, tl, G, N, E);
+}
 
 // ---------------------------------------------------------------------------------------
 // obs row (MultiRaceAviary._computeObs, 566-661) written straight to global memory
@@ -1019,8 +1031,10 @@ __device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const
 template <typename Real, class TS>
 __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const TS& T,
                                              V3<Real> pos, Q4<Real> q, V3<Real> vel, V3<Real> w, int gate,
-                                             float* row, bool write, Real* row0, uint32_t gin, uint32_t oin) {
+                                             float* row, bool write, Real* row0, uint32_t gin, uint32_t oin,
+                                             V3<Real>* rpy_out = nullptr) {
     const V3<Real> rpy = euler_xyz_fast_u(q);
+    if (rpy_out) *rpy_out = rpy;
     const Real k12[12] = {pos.x, pos.y, pos.z, rpy.x, rpy.y, rpy.z, vel.x, vel.y, vel.z, w.x, w.y, w.z};
     if (write)
 #pragma unroll
@@ -1316,16 +1330,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         xc_x = cosf(radf_(yaw_deg));
         xc_y = sinf(radf_(yaw_deg));
     }
-    Lpf lpf;
-    {   // lpf2pInit(gyrolpf, 500, 30) (float)
-#pragma clang fp contract(off)
-        const float fr = 500.0f / 30.0f;
-        const float ohm = tanf(3.14159265358979323846f / fr);
-        const float c = 1.0f + 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm;
-        lpf.b0 = ohm * ohm / c; lpf.b1 = 2.0f * lpf.b0; lpf.b2 = lpf.b0;
-        lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
-        lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
-    }
+    const Lpf lpf = {C.lpf[0], C.lpf[1], C.lpf[2], C.lpf[3], C.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
     if constexpr (PRE == 2) __syncthreads();   // the helpers' first half of the draws is in LDS
     RACE_MARK(t1);
 #ifdef ADRP_RACE_TIMING
@@ -1469,13 +1474,17 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     const Shape<Real> ds = drone_shape(C, d.pos, d.q);
     uint32_t gin, oin;
     bool crashed = track_query_wave(C, T, ds, active, Real(0.45), Real(1e-6), gin, oin, tjobs, tl, G, N, a.E);
-    race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, active, row0, gin, oin);
-    if (C.compete && active) {   // other drones' pos + rpy (653-659)
+    V3<Real> rpy;
+    race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, active, row0, gin, oin, &rpy);
+    if (C.compete) {   // other drones' pos + rpy (653-659): the rpy of their own obs rows
+        V3<Real> grpy[ADRP_MAX_DRONES];
+#pragma unroll
+        for (int k = 0; k < G; ++k) grpy[k] = v3(grp_bcast<G>(rpy.x, k), grp_bcast<G>(rpy.y, k), grp_bcast<G>(rpy.z, k));
         int idx = 0;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            if (k < N && k != dn) {
-                const V3<Real> orpy = euler_xyz_fast_u(gq[k]);
+            if (active && k < N && k != dn) {
+                const V3<Real> orpy = grpy[k];
                 float* p = row + 49 + 6 * idx;
                 p[0] = float(gpos[k].x); p[1] = float(gpos[k].y); p[2] = float(gpos[k].z);
                 p[3] = float(orpy.x); p[4] = float(orpy.y); p[5] = float(orpy.z);

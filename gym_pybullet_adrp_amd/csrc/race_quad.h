@@ -127,7 +127,9 @@ __device__ __forceinline__ void mellinger_q4(RDrone<float>& d, const Lpf& lpf, c
             }
             const float pos[3] = {d.pos.x, d.pos.y, d.pos.z};
             const float vel[3] = {d.vel.x, d.vel.y, d.vel.z};
+#ifndef ADRP_EXP_NOFW   // measurement-only switch (phase profile without the firmware)
             mellinger_fw(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
+#endif
         }
         d.tick += 1;
         // _compute_pwms (423-442), motor ql of [t-r+p+y, t-r-p-y, t+r-p+y, t+r+p-y]
@@ -157,6 +159,72 @@ struct TrackSrcQ {
     __device__ __forceinline__ float operator()(int field) const { return lds[(field - RF_GATE) * kQuadDrones + qd]; }
     __device__ __forceinline__ TrackSrcQ lane(int l, int, int, int) const { return TrackSrcQ{lds, l >> 2}; }
 };
+
+__device__ __forceinline__ uint32_t quad_or(uint32_t v) {   // OR over the quad (DPP quad_perm [1,0,3,2], [2,3,0,1])
+    v |= uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0xb1, 0xf, 0xf, false));
+    v |= uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x4e, 0xf, 0xf, false));
+    return v;
+}
+
+// track_bounds with the track dealt over the quad: lane ql tests gate ql and obstacle ql (same
+// per-part arithmetic), the bit masks are OR-ed over the quad
+template <class TS>
+__device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const TS& T, const Shape<float>& ds,
+                                                float cut, float ccut, int ql, uint32_t& gin, uint32_t& oin,
+                                                uint32_t& amb, uint32_t& camb_all) {
+    using Real = float;
+    const Real tol = Real(1e-5);
+    const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
+    const V3<Real> p = ds.c;
+    amb = 0; camb_all = 0;
+    gin = 0; oin = 0;
+    const int g = ql;
+    if (g < C.num_gates) {
+        const V3<Real> dp = p - v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
+        Real sn, cs;
+        sincos_(T(RF_GATE + 4 * g + 3), &sn, &cs);
+        const V3<Real> lg = v3(cs * dp.x + sn * dp.y, -sn * dp.x + cs * dp.y, dp.z);
+        const int low = C.gate_type[g] > 0;
+        bool in = false;
+        uint32_t gamb = 0, camb = 0;
+#pragma unroll
+        for (int k = 0; k < kGateParts; ++k) {
+            V3<Real> off, h;
+            M3<Real> R;
+            Real r;
+            int cyl;
+            gate_part(k, low, off, R, h, r, cyl);
+            const Real pd = point_part_dist(mulT(R, lg - off), h, r, cyl);
+            in |= pd < cut - tol;
+            if (pd - dr < cut + tol) gamb |= 1u << k;
+            if (pd - dr < ccut + tol) camb |= 1u << k;
+        }
+        if (in) gin |= 1u << g;
+        amb |= ((in ? 0u : gamb) | camb) << (g * kGateParts);
+        camb_all |= camb << (g * kGateParts);
+    }
+    const int o = ql;
+    if (o < C.num_obstacles) {
+        const V3<Real> dp = p - v3(T(RF_OBST + 3 * o), T(RF_OBST + 3 * o + 1), T(RF_OBST + 3 * o + 2));
+        bool in = false;
+        uint32_t gamb = 0, camb = 0;
+#pragma unroll
+        for (int k = 0; k < kObstParts; ++k) {
+            V3<Real> off, h;
+            Real r;
+            int cyl;
+            obst_part(k, off, h, r, cyl);
+            const Real pd = point_part_dist(dp - off, h, r, cyl);
+            in |= pd < cut - tol;
+            if (pd - dr < cut + tol) gamb |= 1u << k;
+            if (pd - dr < ccut + tol) camb |= 1u << k;
+        }
+        if (in) oin |= 1u << o;
+        amb |= ((in ? 0u : gamb) | camb) << (kObstBit0 + o * kObstParts);
+        camb_all |= camb << (kObstBit0 + o * kObstParts);
+    }
+    gin = quad_or(gin); oin = quad_or(oin); amb = quad_or(amb); camb_all = quad_or(camb_all);
+}
 
 template <typename T3>
 __device__ __forceinline__ float sel3(const T3& v, int a) { return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]); }
@@ -201,6 +269,14 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
     const size_t EN = size_t(a.E) * N;
     const size_t slot = size_t(e) * N + dn;
     const uint64_t gid = uint64_t(a.env_offset + e);
+    // the draw keys and the tick first: the draws wait for these loads only, and the tick-schedule
+    // window (a second, dependent load) is issued before the bulk of the state
+    const int sc0 = a.ist[RI_STEP * EN + slot];
+    const int episode = a.ist[RI_EPISODE * EN + slot];
+    const uint32_t ep = uint32_t(episode - 1);
+    const int tick0 = a.ist[RI_TICK * EN + slot];
+    uint32_t att0, pos0;
+    tick_window(a.ticks, tick0, att0, pos0);
     // the env's actual track: 7 of its 28 fields per lane, into LDS after the loop
     float trk[(kTrackFields + 3) / 4];
 #pragma unroll
@@ -209,10 +285,10 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
         trk[i] = k < kTrackFields ? ld(a.f, RF_GATE + k, EN, slot) : 0.0f;
     }
     RDrone<Real> d;
-    load_drone(a, EN, slot, d);
-    const int sc0 = a.ist[RI_STEP * EN + slot];
-    const int episode = a.ist[RI_EPISODE * EN + slot];
-    const uint32_t ep = uint32_t(episode - 1);
+    load_drone<Real, false>(a, EN, slot, d);
+    d.tick_base = tick0;
+    d.att_bits = att0;
+    d.pos_bits = pos0;
     const float4 av = reinterpret_cast<const float4*>(a.act)[slot];
     const float sp[3] = {av.x, av.y, av.z};
     float xc_x, xc_y;
@@ -225,16 +301,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
         xc_x = cosf(radf_(yaw_deg));
         xc_y = sinf(radf_(yaw_deg));
     }
-    Lpf lpf;
-    {
-#pragma clang fp contract(off)
-        const float fr = 500.0f / 30.0f;
-        const float ohm = tanf(3.14159265358979323846f / fr);
-        const float c = 1.0f + 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm;
-        lpf.b0 = ohm * ohm / c; lpf.b1 = 2.0f * lpf.b0; lpf.b2 = lpf.b0;
-        lpf.a1 = 2.0f * (ohm * ohm - 1.0f) / c;
-        lpf.a2 = (1.0f - 2.0f * cosf(3.14159265358979323846f / 4.0f) * ohm + ohm * ohm) / c;
-    }
+    const Lpf lpf = {C.lpf[0], C.lpf[1], C.lpf[2], C.lpf[3], C.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
     if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
         for (int s = ql; s < H.S; s += 4) {
             Real fd[3], nz[4];
@@ -399,15 +466,21 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
     Real row0[15];
     const Shape<Real> ds = drone_shape(C, d.pos, d.q);
     uint32_t gin, oin;
-    bool crashed = track_query_wave<Real, TrackSrcQ, 2>(C, T, ds, owner, Real(0.45), Real(1e-6), gin, oin, tjobs, tl, G,
-                                                       N, a.E);
-    race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, owner, row0, gin, oin);
-    if (C.compete && owner) {
+    uint32_t amb, camb_all;
+    track_bounds_q4(C, T, ds, Real(0.45), Real(1e-6), ql, gin, oin, amb, camb_all);
+    bool crashed = track_gjk_pool<Real, TrackSrcQ, 2>(C, T, ds, owner, Real(0.45), Real(1e-6), gin, oin, amb, camb_all,
+                                                     tjobs, tl, G, N, a.E);
+    V3<Real> rpy;
+    race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, owner, row0, gin, oin, &rpy);
+    if (C.compete) {   // other drones' pos + rpy (653-659): the rpy of their own obs rows
+        V3<Real> grpy[ADRP_MAX_DRONES];
+#pragma unroll
+        for (int k = 0; k < G; ++k) grpy[k] = v3(grpq<G>(rpy.x, k), grpq<G>(rpy.y, k), grpq<G>(rpy.z, k));
         int idx = 0;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            if (k < N && k != dn) {
-                const V3<Real> orpy = euler_xyz_fast(gq[k]);
+            if (owner && k < N && k != dn) {
+                const V3<Real> orpy = grpy[k];
                 float* p = row + 49 + 6 * idx;
                 p[0] = gpos[k].x; p[1] = gpos[k].y; p[2] = gpos[k].z;
                 p[3] = orpy.x; p[4] = orpy.y; p[5] = orpy.z;
@@ -482,8 +555,8 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
 #ifdef ADRP_RACE_TIMING
     RACE_MARK(t6);
     if (threadIdx.x == 0) {
-        RACE_ACC(0, t1 - t0); RACE_ACC(1, acc_phys); RACE_ACC(2, (t2 - t1) - acc_phys); RACE_ACC(3, t3 - t2);
-        RACE_ACC(4, t4 - t3); RACE_ACC(5, t5 - t4); RACE_ACC(6, t6 - t5); RACE_ACC(7, t6 - t0); RACE_ACC(8, 1);
+        RACE_WAVE(0, t1 - t0); RACE_WAVE(1, acc_phys); RACE_WAVE(2, (t2 - t1) - acc_phys); RACE_WAVE(3, t3 - t2);
+        RACE_WAVE(4, t4 - t3); RACE_WAVE(5, t5 - t4); RACE_WAVE(6, t6 - t5); RACE_WAVE(7, t6 - t0);
     }
 #endif
     if (owner) {

@@ -28,7 +28,9 @@ if len(sys.argv) > 5:
 
 lib = ctypes.CDLL(_lib.LIB_PATH)
 lib.adrp_race_phase_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+lib.adrp_race_wave_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 buf = (ctypes.c_ulonglong * 32)()
+QUAD = os.environ.get("ADRP_RACE_QUAD", "1") != "0"
 
 for level, n, phys, mode, E in CONFIGS:
     env = MultiRaceAviary(level, num_drones=n, physics=Physics[phys], racemode=RaceMode[mode], num_envs=E, seed=7)
@@ -56,6 +58,27 @@ for level, n, phys, mode, E in CONFIGS:
     torch.cuda.synchronize()
     lib.adrp_race_phase_read(buf, 1)
     nk = 100
+    if QUAD:   # four-lane kernel: per-workgroup slots (no same-address atomics)
+        G = 1 if n <= 1 else 2 if n <= 2 else 4 if n <= 4 else 8
+        nb = (E * G * 4 + 63) // 64
+        wbuf = (ctypes.c_ulonglong * (nb * 8))()
+        means, maxs = [], []
+        env.h.profile_begin(nk)
+        for k in range(nk):
+            step(acts[k % 16])
+            torch.cuda.synchronize()
+            assert lib.adrp_race_wave_read(wbuf, nb) == 0
+            w = np.array(list(wbuf), dtype=np.float64).reshape(nb, 8)
+            means.append(w.mean(0))
+            maxs.append(w.max(0))
+        ms = env.h.profile_end(nk)
+        print(json.dumps({"config": f"{level} N={n} {phys} {mode} E={E}", "kernel": _lib.kernel_name(env.cfg),
+                          "kernel_us_timing_build": float(np.mean(ms)) * 1e3,
+                          "mean_cycles_per_wave": {p: round(x) for p, x in zip(PHASES, np.mean(means, 0))},
+                          "max_cycles_per_launch": {p: round(x) for p, x in zip(PHASES, np.mean(maxs, 0))}}),
+              flush=True)
+        env.close()
+        continue
     sums = np.zeros(32)
     mx = np.zeros(8)
     gjk_max = 0
