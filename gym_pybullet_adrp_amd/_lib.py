@@ -65,6 +65,10 @@ def load():
     lib.adrp_reseed.restype = I
     lib.adrp_set_wrappers.argtypes = [P, I, I]
     lib.adrp_set_wrappers.restype = I
+    lib.adrp_enable_commands.argtypes = [P]
+    lib.adrp_race_command.argtypes = [P, P, P, P]
+    lib.adrp_get_command_state.argtypes = [P, P, P, P]
+    lib.adrp_set_command_state.argtypes = [P, P, P, P]
     lib.adrp_set_diagnostics.argtypes = [P, I]
     lib.adrp_set_diagnostics.restype = I
     lib.adrp_diagnostic_contact_count.argtypes = [P, I]
@@ -149,7 +153,8 @@ class Handle:
         self._check(self.lib.adrp_reset(self.h, _p(mask), _p(obs), self._stream()), "adrp_reset")
 
     def step(self, act, obs, rew, term, trunc, tobs=None):
-        rc = self._step(self.h, act.data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
+        """act None: command mode, the setpoints the last command() left"""
+        rc = self._step(self.h, None if act is None else act.data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
                         trunc.data_ptr(), None if tobs is None else tobs.data_ptr(),
                         torch.cuda.current_stream(self.device).cuda_stream)
         if rc != 0:
@@ -169,6 +174,32 @@ class Handle:
 
     def step_bytes(self):
         return self.lib.adrp_step_bytes(self.h)
+
+    # ---- high-level command mode (include/adrp.h adrp_enable_commands) ----
+    CMD_NF, CMD_NI, CMD_ARGS = 63, 3, 14
+
+    def enable_commands(self):
+        self._check(self.lib.adrp_enable_commands(self.h), "adrp_enable_commands")
+        self.commands = True
+
+    def command(self, cmd, args):
+        """cmd int32 [E, N] (ADRP_CMD_*), args float64 [E, N, 14], device tensors"""
+        cmd = cmd.to(device=self.device, dtype=torch.int32).contiguous()
+        args = args.to(device=self.device, dtype=torch.float64).contiguous()
+        assert cmd.numel() == self.E * self.N and args.numel() == self.E * self.N * self.CMD_ARGS
+        self._check(self.lib.adrp_race_command(self.h, _p(cmd), _p(args), self._stream()), "adrp_race_command")
+
+    def get_command_state(self):
+        f = torch.empty((self.CMD_NF, self.E * self.N), dtype=torch.float32, device=self.device)
+        i = torch.empty((self.CMD_NI, self.E * self.N), dtype=torch.int32, device=self.device)
+        self._check(self.lib.adrp_get_command_state(self.h, _p(f), _p(i), self._stream()), "adrp_get_command_state")
+        return f, i
+
+    def set_command_state(self, f, i):
+        f = f.to(device=self.device, dtype=torch.float32).contiguous()
+        i = i.to(device=self.device, dtype=torch.int32).contiguous()
+        assert f.shape == (self.CMD_NF, self.E * self.N) and i.shape == (self.CMD_NI, self.E * self.N)
+        self._check(self.lib.adrp_set_command_state(self.h, _p(f), _p(i), self._stream()), "adrp_set_command_state")
 
     def reseed(self, seed):
         """re-key the random streams as a handle created with `seed` (episode counters zeroed)"""

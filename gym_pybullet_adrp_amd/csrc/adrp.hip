@@ -386,6 +386,7 @@ extern "C" void adrp_destroy(adrp_t* h) {
     for (auto e : h->ev_start) hipEventDestroy(e);
     for (auto e : h->ev_stop) hipEventDestroy(e);
     hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters); hipFree(h->cblk);
+    hipFree(h->cmdf); hipFree(h->cmdi);
     delete h;
 }
 
@@ -427,7 +428,7 @@ extern "C" int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev
 
 extern "C" int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* term_dev,
                          uint8_t* trunc_dev, float* terminal_obs_dev, void* stream) {
-    if (!h || !act_dev || !obs_dev || !rew_dev || !term_dev || !trunc_dev)
+    if (!h || (!act_dev && !h->cmdf) || !obs_dev || !rew_dev || !term_dev || !trunc_dev)
         return seterr(h, ADRP_ERR_INVALID, "adrp_step: NULL argument");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
@@ -436,6 +437,58 @@ extern "C" int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float*
                                  : race_step<float>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s);
     return h->real_size == 8 ? hover_step<double>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s)
                              : hover_step<float>(h, act_dev, obs_dev, rew_dev, term_dev, trunc_dev, terminal_obs_dev, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// high-level command mode (commander.h)
+// ---------------------------------------------------------------------------------------------
+extern "C" int adrp_enable_commands(adrp_t* h) {
+    if (!h) return seterr(h, ADRP_ERR_INVALID, "adrp_enable_commands: NULL handle");
+    if (h->cfg.task != ADRP_TASK_RACE) return seterr(h, ADRP_ERR_INVALID, "commands are MultiRaceAviary's");
+    if (h->cmdf) return ADRP_OK;
+    DeviceGuard g(h->device);
+    const size_t EN = size_t(h->E) * h->N;
+    HIPCHK(h, hipDeviceSynchronize());   // no step in flight
+    if (hipMalloc((void**)&h->cmdf, ADRP_CMD_NF * EN * sizeof(float)) != hipSuccess ||
+        hipMalloc((void**)&h->cmdi, ADRP_CMD_NI * EN * sizeof(int32_t)) != hipSuccess) {
+        hipFree(h->cmdf); hipFree(h->cmdi);
+        h->cmdf = nullptr; h->cmdi = nullptr;
+        return seterr(h, ADRP_ERR_OOM, "hipMalloc failed (command state)");
+    }
+    // what reset() leaves (MellingerControl.py:119-150): an idle planner, override on, an unset
+    // setpoint, the commander at the nominal initial pose
+    const int rc = h->real_size == 8 ? race_cmd_init<double>(h, nullptr) : race_cmd_init<float>(h, nullptr);
+    if (rc != ADRP_OK) return rc;
+    HIPCHK(h, hipDeviceSynchronize());
+    return ADRP_OK;
+}
+
+extern "C" int adrp_race_command(adrp_t* h, const int32_t* cmd_dev, const double* args_dev, void* stream) {
+    if (!h || !cmd_dev || !args_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_race_command: NULL argument");
+    if (!h->cmdf) return seterr(h, ADRP_ERR_INVALID, "adrp_race_command: call adrp_enable_commands first");
+    DeviceGuard g(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    return h->real_size == 8 ? race_command<double>(h, cmd_dev, args_dev, s) : race_command<float>(h, cmd_dev, args_dev, s);
+}
+
+extern "C" int adrp_get_command_state(adrp_t* h, float* f_dev, int32_t* i_dev, void* stream) {
+    if (!h || !f_dev || !i_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_get_command_state: NULL argument");
+    if (!h->cmdf) return seterr(h, ADRP_ERR_INVALID, "command mode is off (adrp_enable_commands)");
+    DeviceGuard g(h->device);
+    const size_t EN = size_t(h->E) * h->N;
+    HIPCHK(h, hipMemcpyAsync(f_dev, h->cmdf, ADRP_CMD_NF * EN * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    HIPCHK(h, hipMemcpyAsync(i_dev, h->cmdi, ADRP_CMD_NI * EN * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return ADRP_OK;
+}
+
+extern "C" int adrp_set_command_state(adrp_t* h, const float* f_dev, const int32_t* i_dev, void* stream) {
+    if (!h || !f_dev || !i_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_set_command_state: NULL argument");
+    if (!h->cmdf) return seterr(h, ADRP_ERR_INVALID, "command mode is off (adrp_enable_commands)");
+    DeviceGuard g(h->device);
+    const size_t EN = size_t(h->E) * h->N;
+    HIPCHK(h, hipMemcpyAsync(h->cmdf, f_dev, ADRP_CMD_NF * EN * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    HIPCHK(h, hipMemcpyAsync(h->cmdi, i_dev, ADRP_CMD_NI * EN * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return ADRP_OK;
 }
 
 namespace adrp {

@@ -37,6 +37,8 @@ struct adrp_handle {
     bool reset_helper = true;     // staged kernels: reset states from a helper wave (ADRP_RESET_HELPER=0)
     bool race_helpers = true;     // race fp32: helper waves (track copy, draws) (ADRP_RACE_HELPERS=0)
     bool race_quad = true;        // race fp32: four lanes per drone (race_quad.h) (ADRP_RACE_QUAD=0: one lane)
+    float* cmdf = nullptr;        // race command mode (adrp_enable_commands): [ADRP_CMD_NF][E*N]
+    int32_t* cmdi = nullptr;      // [ADRP_CMD_NI][E*N]
     int diagnostics = 0;
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -96,6 +98,8 @@ inline RaceArgs<Real> race_args(const adrp_t* h) {
     a.seed = h->cfg.seed;
     a.env_offset = h->cfg.env_offset;
     a.E = h->E;
+    a.cf = h->cmdf;
+    a.ci = h->cmdi;
     return a;
 }
 
@@ -110,6 +114,10 @@ int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term
               hipStream_t s);
 template <typename Real>
 int race_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s);
+template <typename Real>
+int race_command(adrp_t* h, const int32_t* cmd, const double* args, hipStream_t s);
+template <typename Real>
+int race_cmd_init(adrp_t* h, hipStream_t s);
 
 #ifdef ADRP_RACE_TIMING
 // each kernel translation unit is its own code object with its own g_race_phase

@@ -4,6 +4,8 @@
 
 template int race_step<double>(adrp_t*, const float*, float*, float*, uint8_t*, uint8_t*, float*, hipStream_t);
 template int race_reset<double>(adrp_t*, const uint8_t*, float*, hipStream_t);
+template int race_command<double>(adrp_t*, const int32_t*, const double*, hipStream_t);
+template int race_cmd_init<double>(adrp_t*, hipStream_t);
 
 #ifdef ADRP_RACE_TIMING
 ADRP_PHASE_READER(phase_read_race_f64)

@@ -14,6 +14,7 @@
 
 #include "../../include/adrp.h"
 #include "adrp_device.h"
+#include "commander.h"
 
 namespace adrp {
 
@@ -78,6 +79,10 @@ struct RaceArgs {
     float* tobs;         // [E][N][D] or null
     const uint8_t* mask; // reset mask or null
     const uint32_t* ticks; // tick-schedule bit tables (kTickTableN ticks each: att, then pos)
+    float* cf;           // command mode: [ADRP_CMD_NF][E*N] (commander.h), else null
+    int32_t* ci;         // [ADRP_CMD_NI][E*N]
+    const int32_t* cmd;  // race_command_kernel: [E*N] ADRP_CMD_*
+    const double* cargs; // [E*N][ADRP_CMD_ARGS]
     uint64_t seed;
     int64_t env_offset;
     int E;
@@ -492,20 +497,51 @@ __device__ __forceinline__ float lpf_apply(const Lpf& l, float& d1, float& d2, f
 // FULLSTATE setpoint modes (MellingerControl.py:510-543): x,y,z,quat abs; rates 0
 // FAST (fp32 kernel): hardware reciprocals for the firmware's divisions; the fp64 kernel
 // keeps the C float divisions bit-for-bit
-template <typename Real, bool FAST = (sizeof(Real) == 4)>
+// CMD (command mode, commander.h): the setpoint comes from the command state cs: position, velocity,
+// acceleration, attitude rates and the mode (SP_FULLSTATE: desiredYaw from the quaternion;
+// SP_COMMANDER: attitude.yaw; SP_UNSET: the zeroed setpoint_t, every mode modeDisable -> thrust
+// direction (-sin 0, -sin 0, 1), desiredYaw 0); xc_x / xc_y are then computed here.
+template <typename Real, bool FAST = (sizeof(Real) == 4), bool CMD = false>
 __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3], float xc_x, float xc_y,
                                              const float gyro[3], const float pos[3], const float vel[3],
-                                             const float Rm[9]) {
+                                             const float Rm[9], const CmdState* cs = nullptr) {
 #pragma clang fp contract(off)
     const float dt = float(1.0f / 500);
-    const float rx = sp[0] - pos[0], ry = sp[1] - pos[1], rz = sp[2] - pos[2];
-    const float vx = 0.0f - vel[0], vy = 0.0f - vel[1], vz = 0.0f - vel[2];
+    float rx, ry, rz, vx, vy, vz, tx, ty, tz;
+    float spr = 0.0f, spp = 0.0f, spy = 0.0f;   // setpoint attitude rates [deg/s]
+    if constexpr (CMD) {
+        rx = cs->sp_pos[0] - pos[0]; ry = cs->sp_pos[1] - pos[1]; rz = cs->sp_pos[2] - pos[2];
+        vx = cs->sp_vel[0] - vel[0]; vy = cs->sp_vel[1] - vel[1]; vz = cs->sp_vel[2] - vel[2];
+        spr = cs->sp_rate[0]; spp = cs->sp_rate[1]; spy = cs->sp_rate[2];
+    } else {
+        rx = sp[0] - pos[0]; ry = sp[1] - pos[1]; rz = sp[2] - pos[2];
+        vx = 0.0f - vel[0]; vy = 0.0f - vel[1]; vz = 0.0f - vel[2];
+    }
     d.ierr[2] = clampf_(d.ierr[2] + rz * dt, -0.4f, 0.4f);
     d.ierr[0] = clampf_(d.ierr[0] + rx * dt, -2.0f, 2.0f);
     d.ierr[1] = clampf_(d.ierr[1] + ry * dt, -2.0f, 2.0f);
-    const float tx = 0.027f * 0.0f + 0.4f * rx + 0.2f * vx + 0.05f * d.ierr[0];
-    const float ty = 0.027f * 0.0f + 0.4f * ry + 0.2f * vy + 0.05f * d.ierr[1];
-    const float tz = 0.027f * (0.0f + 9.81f) + 1.25f * rz + 0.4f * vz + 0.05f * d.ierr[2];
+    if constexpr (CMD) {
+        float yaw_deg = 0.0f;
+        if (cs->mode != SP_UNSET) {
+            tx = 0.027f * cs->sp_acc[0] + 0.4f * rx + 0.2f * vx + 0.05f * d.ierr[0];
+            ty = 0.027f * cs->sp_acc[1] + 0.4f * ry + 0.2f * vy + 0.05f * d.ierr[1];
+            tz = 0.027f * (cs->sp_acc[2] + 9.81f) + 1.25f * rz + 0.4f * vz + 0.05f * d.ierr[2];
+        } else {
+            tx = -sinf(radf_(0.0f)); ty = -sinf(radf_(0.0f)); tz = 1.0f;
+        }
+        if (cs->mode == SP_COMMANDER) {
+            yaw_deg = cs->sp_yaw;
+        } else if (cs->mode == SP_FULLSTATE) {
+            const float qz = cs->sp_qz, qw = cs->sp_qw;
+            yaw_deg = degf_(atan2f(2.0f * (qw * qz + 0.0f * 0.0f), 1 - 2 * (0.0f * 0.0f + qz * qz)));
+        }
+        xc_x = cosf(radf_(yaw_deg));
+        xc_y = sinf(radf_(yaw_deg));
+    } else {
+        tx = 0.027f * 0.0f + 0.4f * rx + 0.2f * vx + 0.05f * d.ierr[0];
+        ty = 0.027f * 0.0f + 0.4f * ry + 0.2f * vy + 0.05f * d.ierr[1];
+        tz = 0.027f * (0.0f + 9.81f) + 1.25f * rz + 0.4f * vz + 0.05f * d.ierr[2];
+    }
     // R columns
     const float Rx0 = Rm[0], Rx1 = Rm[3], Rx2 = Rm[6];
     const float Ry0 = Rm[1], Ry1 = Rm[4], Ry2 = Rm[7];
@@ -528,18 +564,18 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
     const float eRy = -((xd0 * Rz0 + xd1 * Rz1 + xd2 * Rz2) - (Rx0 * zd0 + Rx1 * zd1 + Rx2 * zd2));
     const float eRz = (yd0 * Rx0 + yd1 * Rx1 + yd2 * Rx2) - (Ry0 * xd0 + Ry1 * xd1 + Ry2 * xd2);
     const float rate_roll = radf_(gyro[0]), rate_pitch = -radf_(gyro[1]), rate_yaw = radf_(gyro[2]);
-    const float ewx = radf_(0.0f) - rate_roll, ewy = -radf_(0.0f) - rate_pitch, ewz = radf_(0.0f) - rate_yaw;
+    const float ewx = radf_(spr) - rate_roll, ewy = -radf_(spp) - rate_pitch, ewz = radf_(spy) - rate_yaw;
     float err_d_roll = 0, err_d_pitch = 0;
     if (d.pw_roll == d.pw_roll) {
-        err_d_roll = FAST ? ((radf_(0.0f) - d.psp_roll) - (rate_roll - d.pw_roll)) * 500.0f
-                          : ((radf_(0.0f) - d.psp_roll) - (rate_roll - d.pw_roll)) / dt;
-        err_d_pitch = FAST ? (-(radf_(0.0f) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) * 500.0f
-                           : (-(radf_(0.0f) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) / dt;
+        err_d_roll = FAST ? ((radf_(spr) - d.psp_roll) - (rate_roll - d.pw_roll)) * 500.0f
+                          : ((radf_(spr) - d.psp_roll) - (rate_roll - d.pw_roll)) / dt;
+        err_d_pitch = FAST ? (-(radf_(spp) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) * 500.0f
+                           : (-(radf_(spp) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) / dt;
     }
     d.pw_roll = rate_roll;
     d.pw_pitch = rate_pitch;
-    d.psp_roll = radf_(0.0f);
-    d.psp_pitch = radf_(0.0f);
+    d.psp_roll = radf_(spr);
+    d.psp_pitch = radf_(spp);
     d.ierrm[0] = clampf_(d.ierrm[0] + (-eRx) * dt, -1.0f, 1.0f);
     d.ierrm[1] = clampf_(d.ierrm[1] + (-eRy) * dt, -1.0f, 1.0f);
     d.ierrm[2] = clampf_(d.ierrm[2] + (-eRz) * dt, -1500.0f, 1500.0f);
@@ -562,9 +598,14 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
 }
 
 // MellingerControl.computeControl (154-262) -> rpm (float64 wrapper arithmetic in Real)
-template <typename Real>
+// CMD: command mode (commander.h) — _update_state into cs->st_*, and while the commander drives
+// the setpoint (override off) _update_setpoint(tick / 500) before _step_controller (MellingerControl.py:
+// 216-241); coef = the drone's polynomial block (CF_COEF).
+template <typename Real, bool CMD = false>
 __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lpf, const float sp[3], float xc_x,
-                                                  float xc_y, V3<Real> rpy, const Real noise[4]) {
+                                                  float xc_y, V3<Real> rpy, const Real noise[4],
+                                                  CmdState* cs = nullptr, const float* coef = nullptr, size_t EN = 0,
+                                                  size_t slot = 0) {
 #pragma clang fp contract(off)   // numpy / C arithmetic of the reference wrapper and firmware
     constexpr bool F32 = sizeof(Real) == 4;   // fp32 kernel: reciprocal multiplies; fp64: numpy's divisions
     const Real fdt = Real(0.002);
@@ -585,6 +626,12 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
     float gyro[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) gyro[k] = lpf_apply(lpf, d.lpf1[k], d.lpf2[k], float(rates[k] * r2d));
+    if constexpr (CMD) {
+        cs->st_pos[0] = float(d.pos.x); cs->st_pos[1] = float(d.pos.y); cs->st_pos[2] = float(d.pos.z);
+        cs->st_vel[0] = float(d.vel.x); cs->st_vel[1] = float(d.vel.y); cs->st_vel[2] = float(d.vel.z);
+        cs->st_yaw = float(rpy.z * r2d);
+        if (!cs->ovr) hl_update_setpoint(*cs, coef, EN, slot, float(double(d.tick) / 500.0));
+    }
     Real pwm[4];
     if (float(acc_z) < -0.5f) d.tumble += 1; else d.tumble = 0;
     if (d.tumble >= 30) {
@@ -622,7 +669,7 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
             }
             const float pos[3] = {float(d.pos.x), float(d.pos.y), float(d.pos.z)};
             const float vel[3] = {float(d.vel.x), float(d.vel.y), float(d.vel.z)};
-            mellinger_fw(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
+            mellinger_fw<Real, sizeof(Real) == 4, CMD>(d, sp, xc_x, xc_y, gyro, pos, vel, Rm, cs);
         }
         d.tick += 1;
         // _compute_pwms (423-442)
@@ -1198,6 +1245,52 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
     a.ist[RI_STEP * EN + slot] = 0;
     a.ist[RI_EPISODE * EN + slot] = episode + 1;
     a.ist[RI_WR_GATE * EN + slot] = 0;
+    if (a.cf) {   // command mode: MellingerControl.reset with the initial obs row (commander.h hl_reset)
+        CmdState cs;
+        hl_reset(cs, float(npos.x), float(npos.y), float(npos.z), float(nrpy.z * Real(57.29577951308232)));
+        cmd_store(a.cf, a.ci, EN, slot, cs);
+        for (int k = 0; k < 32; ++k) a.cf[size_t(CF_COEF + k) * EN + slot] = 0.0f;
+    }
+}
+
+// command state of every drone as reset() leaves it (adrp_enable_commands): the initial obs is taken
+// at the nominal pose, so this is exact for envs that have not stepped since their reset
+template <typename Real>
+__global__ void __launch_bounds__(kRaceBlock) race_cmd_init_kernel(RaceArgs<Real> a) {
+    const RaceConst<Real>& C = *a.c;
+    const size_t EN = size_t(a.E) * C.N;
+    const size_t slot = size_t(blockIdx.x) * kRaceBlock + threadIdx.x;
+    if (slot >= EN) return;
+    const int dn = int(slot % C.N);
+    const Real d2r = Real(0.017453292519943295);
+    const Q4<Real> nq = quat_from_euler_fast(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
+    const V3<Real> nrpy = euler_xyz_fast(nq);
+    CmdState cs;
+    hl_reset(cs, float(C.init_pos[dn][0]), float(C.init_pos[dn][1]), float(C.init_pos[dn][2]),
+             float(nrpy.z * Real(57.29577951308232)));
+    cmd_store(a.cf, a.ci, EN, slot, cs);
+    for (int k = 0; k < 32; ++k) a.cf[size_t(CF_COEF + k) * EN + slot] = 0.0f;
+}
+
+// one command message per drone before the sub-steps (MultiRaceAviary.py:190-210; eliminated
+// drones get STOP [step_counter]): commander.h hl_command on the stored command state
+template <typename Real>
+__global__ void __launch_bounds__(kRaceBlock) race_command_kernel(RaceArgs<Real> a) {
+    const RaceConst<Real>& C = *a.c;
+    const size_t EN = size_t(a.E) * C.N;
+    const size_t slot = size_t(blockIdx.x) * kRaceBlock + threadIdx.x;
+    if (slot >= EN) return;
+    CmdState cs;
+    cmd_load(a.cf, a.ci, EN, slot, cs);
+    const double* args = a.cargs + slot * ADRP_CMD_ARGS;
+    if (a.ist[RI_FLAGS * EN + slot] & 1) {
+        double st[ADRP_CMD_ARGS] = {};
+        st[ADRP_CMD_TIME_SLOT] = double(a.ist[RI_STEP * EN + slot]);
+        hl_command(cs, a.cf + size_t(CF_COEF) * EN, EN, slot, ADRP_CMD_STOP, st, false);
+    } else {
+        hl_command(cs, a.cf + size_t(CF_COEF) * EN, EN, slot, a.cmd[slot], args, C.obs_wrapper != 0);
+    }
+    cmd_store(a.cf, a.ci, EN, slot, cs);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1241,11 +1334,14 @@ __device__ __forceinline__ void race_substep_draws(const RaceConst<Real>& H, uin
 // threads per block): 2 = the sub-step draws (disturbances on, S <= kRacePreS), 1 = no draws to
 // make, so they copy the env's actual track (28 fields per lane) into LDS for the post-loop
 // queries instead (A/B: the copy pays without disturbances, but not on top of the draws).
-template <typename Real, int PH, int G, int PRE>
+// CMD: command mode (adrp_enable_commands): the setpoint comes from the command state (commander.h),
+// with a non-null act first turned into a FULLSTATE command; no helper waves.
+template <typename Real, int PH, int G, int PRE, bool CMD = false>
 __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) race_step_kernel(RaceArgs<Real> a) {
     RACE_MARK(t0);
     const RaceConst<Real>& C = *a.c;
     static_assert(!PRE || sizeof(Real) == 4, "pre-computed draws: fp32 kernel only");
+    static_assert(!(CMD && PRE), "command mode: no helper waves");
     __shared__ float pre_draws[PRE == 2 ? kRacePreS * 7 * kRaceBlock : 1];
     __shared__ float trk_lds[PRE == 1 ? kTrackFields * kRaceBlock : 1];
     // the block's obs rows, laid out as in global memory (its envs' rows are contiguous there),
@@ -1317,7 +1413,20 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     const int episode = a.ist[RI_EPISODE * EN + slot];
     const uint32_t ep = uint32_t(episode - 1);
     // FULLSTATE setpoint (MultiRaceAviary.py:190-194; _sendFullStateCmd 510-543)
-    const float4 av = reinterpret_cast<const float4*>(a.act)[slot];
+    const float4 av = CMD && !a.act ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : reinterpret_cast<const float4*>(a.act)[slot];
+    CmdState cs;
+    float* const coefp = CMD ? a.cf + size_t(CF_COEF) * EN : nullptr;
+    if constexpr (CMD) {   // the step's command message (MultiRaceAviary.py:190-210)
+        cmd_load(a.cf, a.ci, EN, slot, cs);
+        double ca[ADRP_CMD_ARGS] = {};
+        ca[ADRP_CMD_TIME_SLOT] = double(sc0);
+        if (d.flags & 1) {
+            hl_command(cs, coefp, EN, slot, ADRP_CMD_STOP, ca, false);
+        } else if (a.act) {
+            ca[0] = av.x; ca[1] = av.y; ca[2] = av.z; ca[9] = av.w;
+            hl_command(cs, coefp, EN, slot, ADRP_CMD_FULLSTATE, ca, C.obs_wrapper != 0);
+        }
+    }
     const float sp[3] = {av.x, av.y, av.z};
     float xc_x, xc_y;
     {
@@ -1410,7 +1519,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
                     race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, noise);
                 }
             }
-            mellinger_compute(d, lpf, sp, xc_x, xc_y, euler_xyz_fast_u(d.q), noise);
+            mellinger_compute<Real, CMD>(d, lpf, sp, xc_x, xc_y, euler_xyz_fast_u(d.q), noise, &cs, coefp, EN, slot);
         }
     }
     }
@@ -1582,6 +1691,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
             store_drone(a, EN, slot, d, false);
             a.ist[RI_STEP * EN + slot] = sc0 + C.S;
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
+            if constexpr (CMD) cmd_store(a.cf, a.ci, EN, slot, cs);
         }
     }
     // ---- coalesced copy-out of the block's rows (envs e0 .. e0 + ne - 1) ----

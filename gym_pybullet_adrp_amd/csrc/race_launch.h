@@ -31,8 +31,24 @@ static void launch_race_q4(const RaceArgs<float>& a, int G, hipStream_t s, adrp_
     else by_g(std::false_type{});
 }
 
+// command mode: the lane kernel with the commander (commander.h), G = 8 lanes per env for every N
+// (one instantiation per physics mode and precision; the commander path is for scripted
+// controllers, not the benched RL step)
+template <typename Real, int PH>
+static void launch_race_cmd(const RaceArgs<Real>& a, hipStream_t s, adrp_t* h) {
+    const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * 8 + kRaceBlock - 1) / kRaceBlock));
+    auto kernel = race_step_kernel<Real, PH, 8, 0, true>;
+    if (h->prof_n < h->prof_cap) {
+        hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
+        ++h->prof_n;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
+    }
+}
+
 template <typename Real, int PH>
 static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
+    if (h->cmdf) return launch_race_cmd<Real, PH>(a, s, h);
     if constexpr (sizeof(Real) == 4) {
         if (h->race_quad) return launch_race_q4<PH>(a, G, s, h);
     }
@@ -100,6 +116,25 @@ int race_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s) {
     a.mask = mask; a.obs = obs;
     const dim3 grid((unsigned)((size_t(h->E) * h->N + kRaceBlock - 1) / kRaceBlock));
     hipLaunchKernelGGL((race_reset_kernel<Real>), grid, dim3(kRaceBlock), 0, s, a);
+    HIPCHK(h, hipGetLastError());
+    return ADRP_OK;
+}
+
+template <typename Real>
+int race_command(adrp_t* h, const int32_t* cmd, const double* args, hipStream_t s) {
+    RaceArgs<Real> a = race_args<Real>(h);
+    a.cmd = cmd; a.cargs = args;
+    const dim3 grid((unsigned)((size_t(h->E) * h->N + kRaceBlock - 1) / kRaceBlock));
+    hipLaunchKernelGGL((race_command_kernel<Real>), grid, dim3(kRaceBlock), 0, s, a);
+    HIPCHK(h, hipGetLastError());
+    return ADRP_OK;
+}
+
+template <typename Real>
+int race_cmd_init(adrp_t* h, hipStream_t s) {
+    RaceArgs<Real> a = race_args<Real>(h);
+    const dim3 grid((unsigned)((size_t(h->E) * h->N + kRaceBlock - 1) / kRaceBlock));
+    hipLaunchKernelGGL((race_cmd_init_kernel<Real>), grid, dim3(kRaceBlock), 0, s, a);
     HIPCHK(h, hipGetLastError());
     return ADRP_OK;
 }

@@ -47,7 +47,7 @@ class MultiRaceAviary:
                  racemode: RaceMode = RaceMode.COMPARE, obs: ObservationType = ObservationType.KIN,
                  act: ActionType = ActionType.PID, *, num_envs: int = 1, device: int = 0, precision: str = "fp32",
                  seed: int = 0, autoreset: bool = True, env_offset: int = 0, link_frame_lag: bool = True,
-                 reward: str = "env"):
+                 reward: str = "env", commands: bool = False):
         if drone_model not in (DroneModel.CF2X,):
             raise ValueError(f"DroneModel {drone_model} not supported (cf2x_IROS.urdf constants only)")
         if gui or record:
@@ -96,6 +96,9 @@ class MultiRaceAviary:
         self._trunc = torch.zeros(E, dtype=torch.bool, device=self.device)
         self._act_shape = (E, N, 4)
         self._info = {"answer": 42, "terminal_observation": self._tobs}
+        self.commands = False
+        if commands:
+            self.enable_commands()
 
     # ---- spaces (MultiRaceAviary.py:284-343) ----
     def _actionSpace(self):
@@ -128,8 +131,33 @@ class MultiRaceAviary:
         self.h.reset(self._obs, m)
         return self._obs, {"answer": 42}
 
+    def enable_commands(self):
+        """High-level command mode (include/adrp.h adrp_enable_commands): step() then also takes
+        (Command, args) tuples, run through the firmware's high-level commander (commands.py).
+        Enabled implicitly by the first tuple action; exact for envs that have not stepped since
+        their reset (the reference's controllers start from the initial obs)."""
+        if not self.commands:
+            self.h.enable_commands()
+            self.commands = True
+
+    def command(self, actions):
+        """Send one (Command, args) per drone without stepping: a list per env of N tuples (the
+        reference's list for E = 1), or (codes [E,N], args [E,N,14]) already encoded."""
+        from ..commands import encode_commands
+        self.enable_commands()
+        if isinstance(actions, tuple) and len(actions) == 2 and hasattr(actions[0], "shape"):
+            codes, args = actions
+        else:
+            codes, args = encode_commands(actions, self.num_envs, self.NUM_DRONES)
+        self.h.command(torch.as_tensor(codes), torch.as_tensor(args))
+
     def step(self, action):
-        """action [E,N,4]: absolute FULLSTATE target (x, y, z, yaw) per drone."""
+        """action [E,N,4]: absolute FULLSTATE target (x, y, z, yaw) per drone; or per drone a
+        (Command, args) tuple (MultiRaceAviary.py:190-210; lists per env, commands.py)."""
+        if isinstance(action, (list, tuple)) and not _numeric(action):
+            self.command(action)
+            self.h.step(None, self._obs, self._rew, self._term, self._trunc, self._tobs)
+            return self._obs, self._rew, self._term, self._trunc, self._info
         act = action
         if not (isinstance(act, torch.Tensor) and act.dtype == torch.float32 and act.device == self.device
                 and act.is_contiguous() and act.shape == self._act_shape):
@@ -173,3 +201,18 @@ class MultiRaceAviary:
 
     def step_bytes(self):
         return self.h.step_bytes()
+
+    def get_command_state(self):
+        return self.h.get_command_state()
+
+    def set_command_state(self, f, i):
+        self.h.set_command_state(f, i)
+
+
+def _numeric(x):
+    """a nested list / tuple of numbers (an ndarray-like action), not (Command, args) tuples"""
+    try:
+        np.asarray(x, dtype=np.float64)
+        return True
+    except (TypeError, ValueError):
+        return False

@@ -73,6 +73,35 @@ extern "C" {
 #define ADRP_RACE_COMPARE 0
 #define ADRP_RACE_COMPETE 1
 
+/* High-level commands: utils/enums.py:58-70 (Command), as MultiRaceAviary.step sends them to
+ * each drone's MellingerControl (envs/MultiRaceAviary.py:190-210, control/MellingerControl.py:17-61).
+ * adrp_race_command args: ADRP_CMD_ARGS float64 per drone.  Slots 0..12 hold the command's own
+ * arguments, flattened in the reference's order; slot 13 holds the reference's args[-1], which
+ * low_level_control hands to process_command_queue as the commander clock (MellingerControl.py:57,
+ * 292-303) — for FULLSTATE that is its timestep, for TAKEOFF [h, d] it is d. */
+#define ADRP_CMD_NONE 0         /* ignored (low_level_control: else -> continue) */
+#define ADRP_CMD_FULLSTATE 1    /* pos[3], vel[3], acc[3], yaw, rpy_rate[3]            (491-543) */
+#define ADRP_CMD_TAKEOFF 2      /* height, duration                                    (547-561) */
+#define ADRP_CMD_TAKEOFFYAW 3   /* height, duration, yaw                               (565-580) */
+#define ADRP_CMD_TAKEOFFVEL 4   /* height, velocity, relative                          (584-599) */
+#define ADRP_CMD_LAND 5         /* height, duration                                    (603-617) */
+#define ADRP_CMD_LANDYAW 6      /* height, duration, yaw                               (621-636) */
+#define ADRP_CMD_LANDVEL 7      /* height, velocity, relative                          (640-655) */
+#define ADRP_CMD_STOP 8         /* -                                                   (659-668) */
+#define ADRP_CMD_GOTO 9         /* x, y, z, yaw, duration, relative                    (672-689) */
+#define ADRP_CMD_NOTIFY 10      /* - (notifySetpointStop)                              (691-699) */
+#define ADRP_CMD_ARGS 14
+#define ADRP_CMD_TIME_SLOT 13
+/* Per-drone command state (adrp_get_command_state), float fields then int32 fields, each a
+ * contiguous [E*N] vector like adrp_get_state's.  Floats: setpoint_t position 3, velocity 3,
+ * acceleration 3, attitudeRate 3 [deg/s], attitudeQuaternion z, w (FULLSTATE), attitude.yaw [deg]
+ * (commander); the commander's pos 3, vel 3, yaw [rad]; state_t position 3, velocity 3,
+ * attitude.yaw [deg] of the last _update_state; planner t_begin, duration, 4 x 8 polynomial
+ * coefficients (x, y, z, yaw).  Ints: planner state (0 idle, 1 flying, 2 landing),
+ * full_state_cmd_override, setpoint mode (0 never set, 1 FULLSTATE, 2 commander). */
+#define ADRP_CMD_NF 63
+#define ADRP_CMD_NI 3
+
 /* Drone constants, as BaseAviary._parseURDFParameters reads them (BaseAviary.py:989-1021). */
 typedef struct adrp_drone_params {
     double m;                  /* base mass [kg] */
@@ -198,6 +227,23 @@ int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev, void* str
  * the reset observation (SB3 VecEnv semantics). */
 int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
               uint8_t* term_dev, uint8_t* trunc_dev, float* terminal_obs_dev, void* stream);
+
+/* MultiRaceAviary only: high-level command mode.  adrp_enable_commands
+ * allocates the per-drone setpoint / commander / planner state; call it before the adrp_reset that
+ * starts the episodes (envs already running start from an idle planner and an unset setpoint).
+ * From then on adrp_step runs the step kernel that evaluates the commander's trajectory at every
+ * controller call (MellingerControl._update_setpoint, MellingerControl.py:369-374).
+ * adrp_race_command applies one command per drone (cmd_dev int32 [E,N] ADRP_CMD_*, args_dev float64
+ * [E,N,ADRP_CMD_ARGS]) as the controller processes MultiRaceAviary.step's command message before the
+ * sub-steps; eliminated drones get STOP (MultiRaceAviary.py:198-199).  Follow it with
+ * adrp_step(h, NULL, ...), which keeps the setpoints the commands left.  adrp_step with a non-NULL
+ * act_dev sends FULLSTATE (act[:3], 0, 0, act[3], 0, step_counter) first, as the ndarray path does
+ * (MultiRaceAviary.py:190-194).  Parity of the commander is unpinned. */
+int adrp_enable_commands(adrp_t* h);
+int adrp_race_command(adrp_t* h, const int32_t* cmd_dev, const double* args_dev, void* stream);
+/* float [ADRP_CMD_NF][E*N] (float32 at every precision), int32 [ADRP_CMD_NI][E*N] */
+int adrp_get_command_state(adrp_t* h, float* f_dev, int32_t* i_dev, void* stream);
+int adrp_set_command_state(adrp_t* h, const float* f_dev, const int32_t* i_dev, void* stream);
 
 /* Snapshot layout: nf float fields and ni int32 fields, each field a contiguous
  * [E*N] vector (drone-major within env: index e*N+n).  Field names: adrp_state_field. */

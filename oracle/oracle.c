@@ -844,7 +844,7 @@ int orc_step(orc_t* o, const float* act, float* obs, float* rew, uint8_t* term, 
         const size_t row = (size_t)o->N * o->D;
 #pragma omp parallel for schedule(dynamic, 4) num_threads(g_threads) if (g_threads > 1)
         for (int e = 0; e < E; ++e)
-            race_step_env(o, e, act + (size_t)e * o->N * 4, obs + e * row, rew + e, term + e, trunc + e,
+            race_step_env(o, e, act ? act + (size_t)e * o->N * 4 : NULL, obs + e * row, rew + e, term + e, trunc + e,
                           terminal_obs ? terminal_obs + e * row : NULL);
     } else {
 #pragma omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)

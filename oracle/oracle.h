@@ -15,7 +15,8 @@
  *   - parity unpinned (no runnable pybullet / pycffirmware here): the Bullet
  *     btMultiBody integration step (restated from Bullet 3.x, pybullet ^3.2.5,
  *     pyproject.toml:20), Bullet collision/ray/proximity queries, and the Crazyflie
- *     firmware Mellinger controller + lpf2p (restated from the published algorithm).
+ *     firmware Mellinger controller + lpf2p, and the firmware's high-level commander /
+ *     planner (restated from the published algorithm).
  */
 #ifndef ADRP_ORACLE_H
 #define ADRP_ORACLE_H
@@ -37,6 +38,16 @@ int orc_act_dim(const orc_t* o);
 int orc_reset(orc_t* o, const uint8_t* env_mask, float* obs);
 int orc_step(orc_t* o, const float* act, float* obs, float* rew, uint8_t* term,
              uint8_t* trunc, float* terminal_obs);
+/* MultiRace high-level commands (adrp.h ADRP_CMD_*): one command per drone, cmd [E*N], args
+   [E*N][ADRP_CMD_ARGS]; then orc_step(o, NULL, ...) keeps the setpoints.  The command state
+   snapshot has the adrp_get_command_state layout (float [ADRP_CMD_NF][E*N], int [ADRP_CMD_NI][E*N]). */
+int orc_race_command(orc_t* o, const int32_t* cmd, const double* args);
+int orc_get_command_state(const orc_t* o, float* f, int32_t* i);
+int orc_set_command_state(orc_t* o, const float* f, const int32_t* i);
+/* one poly4d_eval of the commander's trajectory (tests): coef [4][8], out = pos 3, vel 3, acc 3,
+   omega 3, yaw; poly7_nojerk coefficients */
+void orc_poly4d_eval(const float* coef, float t, float out[13]);
+void orc_poly7_nojerk(float T, float x0, float dx0, float ddx0, float xf, float dxf, float ddxf, float out[8]);
 int orc_state_layout(const orc_t* o, int* nf, int* ni);
 const char* orc_state_field(const orc_t* o, int is_int, int index);
 int orc_get_state(const orc_t* o, double* f, int32_t* i);

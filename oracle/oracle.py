@@ -16,7 +16,8 @@ LIB = os.path.join(HERE, "liboracle.so")
 def build(force=False):
     src = os.path.join(HERE, "oracle.c")
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
-            os.path.getmtime(src), os.path.getmtime(os.path.join(HERE, "oracle.h")),
+            os.path.getmtime(src), os.path.getmtime(os.path.join(HERE, "race.c")),
+            os.path.getmtime(os.path.join(HERE, "oracle.h")),
             os.path.getmtime(os.path.join(HERE, "..", "include", "adrp.h"))):
         subprocess.check_call(["make", "-s", "-C", HERE])
     return LIB
@@ -73,6 +74,11 @@ def _load():
     lib.orc_race_progress.argtypes = [I, I, P, P, P, P]
     lib.orc_race_reward.argtypes = [P, P, P, P, I, I]
     lib.orc_race_reward.restype = D
+    lib.orc_race_command.argtypes = [P, P, P]
+    lib.orc_get_command_state.argtypes = [P, P, P]
+    lib.orc_set_command_state.argtypes = [P, P, P]
+    lib.orc_poly4d_eval.argtypes = [P, ctypes.c_float, P]
+    lib.orc_poly7_nojerk.argtypes = [ctypes.c_float] * 7 + [P]
     return lib
 
 
@@ -128,7 +134,9 @@ class Oracle:
         return obs
 
     def step(self, act):
-        act = np.ascontiguousarray(act, np.float32).reshape(self.E, self.N, self.A)
+        """act None: MultiRace command mode, the setpoints the last command() left."""
+        if act is not None:
+            act = np.ascontiguousarray(act, np.float32).reshape(self.E, self.N, self.A)
         obs = np.zeros((self.E, self.N, self.D), np.float32)
         tobs = np.zeros_like(obs)
         rew = np.zeros(self.E, np.float32)
@@ -136,6 +144,27 @@ class Oracle:
         trunc = np.zeros(self.E, np.uint8)
         lib().orc_step(self.h, _ptr(act), _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(tobs))
         return obs, rew, term.astype(bool), trunc.astype(bool), tobs
+
+    CMD_NF, CMD_NI, CMD_ARGS = 63, 3, 14
+
+    def command(self, cmd, args):
+        """One high-level command per drone: cmd int32 [E, N], args float64 [E, N, 14]."""
+        c = np.ascontiguousarray(cmd, np.int32).reshape(self.E * self.N)
+        a = np.ascontiguousarray(args, np.float64).reshape(self.E * self.N, self.CMD_ARGS)
+        rc = lib().orc_race_command(self.h, _ptr(c), _ptr(a))
+        assert rc == 0, lib().orc_last_error()
+
+    def get_command_state(self):
+        f = np.zeros((self.CMD_NF, self.E * self.N), np.float32)
+        i = np.zeros((self.CMD_NI, self.E * self.N), np.int32)
+        assert lib().orc_get_command_state(self.h, _ptr(f), _ptr(i)) == 0
+        return f, i
+
+    def set_command_state(self, f, i):
+        f = np.ascontiguousarray(f, np.float32)
+        i = np.ascontiguousarray(i, np.int32)
+        assert f.shape == (self.CMD_NF, self.E * self.N) and i.shape == (self.CMD_NI, self.E * self.N)
+        assert lib().orc_set_command_state(self.h, _ptr(f), _ptr(i)) == 0
 
     def get_state(self):
         f = np.zeros((self.nf, self.E * self.N), np.float64)
@@ -162,6 +191,20 @@ class Oracle:
         trunc = np.zeros(self.E, np.uint8)
         lib().orc_hover_eval(self.h, _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc))
         return obs, rew, term.astype(bool), trunc.astype(bool)
+
+
+def poly4d_eval(coef, t):
+    """firmware poly4d_eval of a [4, 8] float32 coefficient block -> (pos, vel, acc, omega, yaw)."""
+    c = np.ascontiguousarray(coef, np.float32).reshape(4, 8)
+    o = np.zeros(13, np.float32)
+    lib().orc_poly4d_eval(_ptr(c), float(t), _ptr(o))
+    return o[0:3], o[3:6], o[6:9], o[9:12], o[12]
+
+
+def poly7_nojerk(T, x0, dx0, ddx0, xf, dxf, ddxf):
+    o = np.zeros(8, np.float32)
+    lib().orc_poly7_nojerk(T, x0, dx0, ddx0, xf, dxf, ddxf, _ptr(o))
+    return o
 
 
 def force_assembly(cfg, states, n, rpm, prev):

@@ -73,6 +73,14 @@ typedef struct rdrone_s {
     float ctl[4];                    /* control_t roll, pitch, yaw (int16 values), thrust */
     /* race progress */
     int gate, elim, fin;
+    /* command state (adrp.h ADRP_CMD_NF / ADRP_CMD_NI order): setpoint_t fields the controller
+       reads, the high-level commander's pos / vel / yaw, the firmware state_t of the last
+       _update_state, the planner's single-piece trajectory */
+    float sp_pos[3], sp_vel[3], sp_acc[3], sp_rate[3], sp_qz, sp_qw, sp_yaw;
+    float c_pos[3], c_vel[3], c_yaw;
+    float st_pos[3], st_vel[3], st_yaw;
+    float plan_t0, plan_dur, coef[4][8];
+    int plan_state, override, sp_mode;
 } rdrone_t;
 
 typedef struct renv_s {
@@ -125,15 +133,22 @@ static void mellinger_reset(rdrone_t* d) {   /* controllerMellingerReset */
     for (int k = 0; k < 3; ++k) { d->i_err[k] = 0; d->i_err_m[k] = 0; }
 }
 
-/* controllerMellinger(control, setpoint, sensors, state, tick) with the FULLSTATE setpoint
- * modes (x,y,z,quat = modeAbs; roll,pitch,yaw = modeDisable; velocity, acceleration and
- * attitude rates 0) that MellingerControl._sendFullStateCmd sets (MellingerControl.py:510-543). */
-static void mellinger_fw(rdrone_t* d, const float sp_pos[3], const float sp_quat[4], const float gyro[3],
-                         const float st_pos[3], const float st_vel[3], const float st_q[4], int tick) {
+enum { SP_UNSET = 0, SP_FULLSTATE = 1, SP_COMMANDER = 2 };   /* setpoint_t modes the controller sees */
+
+/* controllerMellinger(control, setpoint, sensors, state, tick).  Setpoint modes:
+ *   SP_FULLSTATE (MellingerControl._sendFullStateCmd, MellingerControl.py:510-543): x,y,z,quat
+ *     modeAbs, roll/pitch/yaw modeDisable -> desiredYaw from the quaternion;
+ *   SP_COMMANDER (crtpCommanderHighLevelGetSetpoint): x,y,z,yaw modeAbs, quat modeDisable ->
+ *     desiredYaw = attitude.yaw;
+ *   SP_UNSET (the zeroed setpoint_t of reset(), MellingerControl.py:121, before any command):
+ *     every mode modeDisable -> thrust direction (-sin(pitch), -sin(roll), 1) with roll = pitch = 0
+ *     and desiredYaw 0. */
+static void mellinger_fw(rdrone_t* d, const float gyro[3], const float st_pos[3], const float st_vel[3],
+                         const float st_q[4], int tick) {
     if (tick % 2 != 0) return;   /* RATE_DO_EXECUTE(ATTITUDE_RATE = 500, tick), RATE_MAIN_LOOP = 1000 */
     const float dt = (float)(1.0f / 500);
-    f3 r_error = F3(sp_pos[0] - st_pos[0], sp_pos[1] - st_pos[1], sp_pos[2] - st_pos[2]);
-    f3 v_error = F3(0.0f - st_vel[0], 0.0f - st_vel[1], 0.0f - st_vel[2]);
+    f3 r_error = F3(d->sp_pos[0] - st_pos[0], d->sp_pos[1] - st_pos[1], d->sp_pos[2] - st_pos[2]);
+    f3 v_error = F3(d->sp_vel[0] - st_vel[0], d->sp_vel[1] - st_vel[1], d->sp_vel[2] - st_vel[2]);
     d->i_err[2] += r_error.z * dt;
     d->i_err[2] = clampf_(d->i_err[2], -MEL_I_RANGE_Z, MEL_I_RANGE_Z);
     d->i_err[0] += r_error.x * dt;
@@ -141,13 +156,24 @@ static void mellinger_fw(rdrone_t* d, const float sp_pos[3], const float sp_quat
     d->i_err[1] += r_error.y * dt;
     d->i_err[1] = clampf_(d->i_err[1], -MEL_I_RANGE_XY, MEL_I_RANGE_XY);
     f3 target;
-    target.x = MEL_MASS * 0.0f + MEL_KP_XY * r_error.x + MEL_KD_XY * v_error.x + MEL_KI_XY * d->i_err[0];
-    target.y = MEL_MASS * 0.0f + MEL_KP_XY * r_error.y + MEL_KD_XY * v_error.y + MEL_KI_XY * d->i_err[1];
-    target.z = MEL_MASS * (0.0f + GRAVITY_MAGNITUDE) + MEL_KP_Z * r_error.z + MEL_KD_Z * v_error.z +
-               MEL_KI_Z * d->i_err[2];
-    /* desiredYaw from the setpoint quaternion (mode.quat == modeAbs): quat2rpy(q).z in degrees */
-    float qx = sp_quat[0], qy = sp_quat[1], qz = sp_quat[2], qw = sp_quat[3];
-    float desired_yaw = degreesf_(atan2f(2.0f * (qw * qz + qx * qy), 1 - 2 * (qy * qy + qz * qz)));
+    float desired_yaw = 0;
+    if (d->sp_mode != SP_UNSET) {
+        target.x = MEL_MASS * d->sp_acc[0] + MEL_KP_XY * r_error.x + MEL_KD_XY * v_error.x + MEL_KI_XY * d->i_err[0];
+        target.y = MEL_MASS * d->sp_acc[1] + MEL_KP_XY * r_error.y + MEL_KD_XY * v_error.y + MEL_KI_XY * d->i_err[1];
+        target.z = MEL_MASS * (d->sp_acc[2] + GRAVITY_MAGNITUDE) + MEL_KP_Z * r_error.z + MEL_KD_Z * v_error.z +
+                   MEL_KI_Z * d->i_err[2];
+    } else {
+        target.x = -sinf(radiansf_(0.0f));
+        target.y = -sinf(radiansf_(0.0f));
+        target.z = 1;
+    }
+    if (d->sp_mode == SP_COMMANDER) {
+        desired_yaw = d->sp_yaw;
+    } else if (d->sp_mode == SP_FULLSTATE) {
+        /* quat2rpy(setpoint quaternion).z in degrees (the quaternion's x = y = 0) */
+        float qx = 0.0f, qy = 0.0f, qz = d->sp_qz, qw = d->sp_qw;
+        desired_yaw = degreesf_(atan2f(2.0f * (qw * qz + qx * qy), 1 - 2 * (qy * qy + qz * qz)));
+    }
     /* state attitude quaternion -> rotation matrix (quat2rotmat) */
     float x = st_q[0], y = st_q[1], z = st_q[2], w = st_q[3];
     float R[3][3];
@@ -165,20 +191,21 @@ static void mellinger_fw(rdrone_t* d, const float sp_pos[3], const float sp_quat
     eR.x = f3dot(z_des, Ry) - f3dot(Rz, y_des);
     eR.y = -(f3dot(x_des, Rz) - f3dot(Rx, z_des));
     eR.z = f3dot(y_des, Rx) - f3dot(Ry, x_des);
-    /* ew: gyro in deg/s, pitch inverted; setpoint attitude rates are 0 */
+    /* ew: gyro in deg/s, pitch inverted; setpoint attitude rates in deg/s */
     float rate_roll = radiansf_(gyro[0]);
     float rate_pitch = -radiansf_(gyro[1]);
     float rate_yaw = radiansf_(gyro[2]);
-    f3 ew = F3(radiansf_(0.0f) - rate_roll, -radiansf_(0.0f) - rate_pitch, radiansf_(0.0f) - rate_yaw);
+    const float spr = d->sp_rate[0], spp = d->sp_rate[1], spy = d->sp_rate[2];
+    f3 ew = F3(radiansf_(spr) - rate_roll, -radiansf_(spp) - rate_pitch, radiansf_(spy) - rate_yaw);
     float err_d_roll = 0, err_d_pitch = 0;
     if (d->prev_omega_roll == d->prev_omega_roll) {   /* d part initialised (not NaN) */
-        err_d_roll = ((radiansf_(0.0f) - d->prev_sp_roll) - (rate_roll - d->prev_omega_roll)) / dt;
-        err_d_pitch = (-(radiansf_(0.0f) - d->prev_sp_pitch) - (rate_pitch - d->prev_omega_pitch)) / dt;
+        err_d_roll = ((radiansf_(spr) - d->prev_sp_roll) - (rate_roll - d->prev_omega_roll)) / dt;
+        err_d_pitch = (-(radiansf_(spp) - d->prev_sp_pitch) - (rate_pitch - d->prev_omega_pitch)) / dt;
     }
     d->prev_omega_roll = rate_roll;
     d->prev_omega_pitch = rate_pitch;
-    d->prev_sp_roll = radiansf_(0.0f);
-    d->prev_sp_pitch = radiansf_(0.0f);
+    d->prev_sp_roll = radiansf_(spr);
+    d->prev_sp_pitch = radiansf_(spp);
     d->i_err_m[0] += (-eR.x) * dt;
     d->i_err_m[0] = clampf_(d->i_err_m[0], -MEL_I_RANGE_M_XY, MEL_I_RANGE_M_XY);
     d->i_err_m[1] += (-eR.y) * dt;
@@ -216,12 +243,241 @@ static void mellinger_wrapper_reset(rdrone_t* d, const double init_rpy[3], const
     d->ctl[0] = d->ctl[1] = d->ctl[2] = d->ctl[3] = 0;
 }
 
+/* ---------------------------------------------------------------------------------- */
+/* Crazyflie high-level commander + planner: restated from the published   */
+/* firmware algorithm (crtp_commander_high_level.c, planner.c, pptraj.c, math3d.h; C float). */
+/* Not in /root/reference (pycffirmware is an un-vendored dependency): parity unpinned.      */
+/* Call sites: low_level_control (MellingerControl.py:17-61), process_command_queue         */
+/* (292-303), _update_setpoint (369-374), the send*Cmd / _send*Cmd pairs (491-699), reset's  */
+/* crtpCommanderHighLevelInit + TellState (145-150).                                        */
+/* ---------------------------------------------------------------------------------- */
+enum { PLAN_IDLE = 0, PLAN_FLYING = 1, PLAN_LANDING = 2 };
+#define HL_GRAV 9.81f                  /* pptraj.c GRAV */
+#define HL_DEFAULT_VELOCITY 0.5f       /* defaultTakeoffVelocity / defaultLandingVelocity */
+
+static f3 f3scl(float s, f3 v) { return F3(s * v.x, s * v.y, s * v.z); }
+static f3 f3normr(f3 v) {   /* math3d vnormalize = vdiv(v, vmag(v)) = vscl(1 / |v|, v) */
+    return f3scl(1.0f / sqrtf(v.x * v.x + v.y * v.y + v.z * v.z), v);
+}
+static float shortest_signed_angle_radians(float start, float goal) {
+    float diff = goal - start;
+    float signed_diff = fmodf(diff + M_PI_F, 2 * M_PI_F) - M_PI_F;
+    if (signed_diff < -M_PI_F) signed_diff += 2 * M_PI_F;
+    return signed_diff;
+}
+/* poly7_nojerk: 7th-order polynomial with x, x', x'' given and x''' = 0 at both ends */
+static void poly7_nojerk(float p[8], float T, float x0, float dx0, float ddx0, float xf, float dxf, float ddxf) {
+    if (T <= 0.0f) {
+        p[0] = xf; p[1] = dxf; p[2] = ddxf / 2;
+        for (int i = 3; i < 8; ++i) p[i] = 0;
+        return;
+    }
+    const float T2 = T * T, T3 = T2 * T, T4 = T3 * T, T5 = T4 * T, T6 = T5 * T, T7 = T6 * T;
+    p[0] = x0; p[1] = dx0; p[2] = ddx0 / 2; p[3] = 0;
+    p[4] = -(5 * (14 * x0 - 14 * xf + 8 * T * dx0 + 6 * T * dxf + 2 * T2 * ddx0 - T2 * ddxf)) / (2 * T4);
+    p[5] = (84 * x0 - 84 * xf + 45 * T * dx0 + 39 * T * dxf + 10 * T2 * ddx0 - 7 * T2 * ddxf) / T5;
+    p[6] = -(140 * x0 - 140 * xf + 72 * T * dx0 + 68 * T * dxf + 15 * T2 * ddx0 - 13 * T2 * ddxf) / (2 * T6);
+    p[7] = (2 * (10 * x0 - 10 * xf + 5 * T * dx0 + 5 * T * dxf + T2 * ddx0 - T2 * ddxf)) / T7;
+    (void)T3;
+}
+static float polyval7(const float p[8], float t) {   /* Horner from the top coefficient */
+    float x = 0.0f;
+    for (int i = 7; i >= 0; --i) x = x * t + p[i];
+    return x;
+}
+static void polyder7(float p[8]) {
+    for (int i = 1; i <= 7; ++i) p[i - 1] = i * p[i];
+    p[7] = 0;
+}
+typedef struct { f3 pos, vel, acc, omega; float yaw; } traj_eval_t;
+/* poly4d_eval: flat outputs -> pos, vel, acc, yaw and the body rates of the differential flatness map */
+static traj_eval_t poly4d_eval(const float coef[4][8], float t) {
+    float d[4][8];
+    memcpy(d, coef, sizeof d);
+    traj_eval_t o;
+    o.pos = F3(polyval7(d[0], t), polyval7(d[1], t), polyval7(d[2], t));
+    o.yaw = polyval7(d[3], t);
+    for (int k = 0; k < 4; ++k) polyder7(d[k]);
+    o.vel = F3(polyval7(d[0], t), polyval7(d[1], t), polyval7(d[2], t));
+    const float dyaw = polyval7(d[3], t);
+    for (int k = 0; k < 4; ++k) polyder7(d[k]);
+    o.acc = F3(polyval7(d[0], t), polyval7(d[1], t), polyval7(d[2], t));
+    for (int k = 0; k < 4; ++k) polyder7(d[k]);
+    const f3 jerk = F3(polyval7(d[0], t), polyval7(d[1], t), polyval7(d[2], t));
+    const f3 thrust = F3(o.acc.x + 0.0f, o.acc.y + 0.0f, o.acc.z + HL_GRAV);
+    const f3 z_body = f3normr(thrust);
+    const f3 x_world = F3(cosf(o.yaw), sinf(o.yaw), 0);
+    const f3 y_body = f3normr(f3cross(z_body, x_world));
+    const f3 x_body = f3cross(y_body, z_body);
+    const float jz = f3dot(jerk, z_body);   /* vorthunit(jerk, z_body) */
+    const f3 jerk_orth = F3(jerk.x - jz * z_body.x, jerk.y - jz * z_body.y, jerk.z - jz * z_body.z);
+    const f3 h_w = f3scl(1.0f / sqrtf(f3dot(thrust, thrust)), jerk_orth);
+    o.omega = F3(-f3dot(h_w, y_body), f3dot(h_w, x_body), z_body.z * dyaw);
+    return o;
+}
+/* piecewise_eval of the planner's one-piece trajectory (timescale 1, shift 0); past its end the
+   end point with zero derivatives.  Before t_begin the polynomial is extrapolated, as the firmware
+   does (no clamp at t < t_begin). */
+static traj_eval_t plan_eval(const rdrone_t* d, float t) {
+    const float tr = t - d->plan_t0;
+    if (tr <= d->plan_dur * 1.0f) return poly4d_eval(d->coef, tr);
+    traj_eval_t ev = poly4d_eval(d->coef, d->plan_dur);
+    ev.vel = ev.acc = ev.omega = F3(0, 0, 0);
+    return ev;
+}
+/* piecewise_plan_7th_order_no_jerk into the planner, state -> FLYING / LANDING from t */
+static void plan_7th(rdrone_t* d, int state, float t, float dur, f3 p0, float y0, f3 v0, float dy0, f3 a0,
+                     f3 p1, float y1) {
+    d->plan_dur = dur;
+    poly7_nojerk(d->coef[0], dur, p0.x, v0.x, a0.x, p1.x, 0, 0);
+    poly7_nojerk(d->coef[1], dur, p0.y, v0.y, a0.y, p1.y, 0, 0);
+    poly7_nojerk(d->coef[2], dur, p0.z, v0.z, a0.z, p1.z, 0, 0);
+    poly7_nojerk(d->coef[3], dur, y0, dy0, 0, y1, 0, 0);
+    d->plan_state = state;
+    d->plan_t0 = t;
+}
+static f3 cpos_(const rdrone_t* d) { return F3(d->c_pos[0], d->c_pos[1], d->c_pos[2]); }
+/* plan_takeoff / plan_land (planner.c): takeoff only from IDLE, land not from IDLE / LANDING */
+static void plan_takeoff(rdrone_t* d, float height, float hover_yaw, float dur, float t) {
+    if (d->plan_state != PLAN_IDLE) return;
+    const f3 p = cpos_(d), z = F3(0, 0, 0);
+    plan_7th(d, PLAN_FLYING, t, dur, p, d->c_yaw, z, 0, z, F3(p.x, p.y, height), hover_yaw);
+}
+static void plan_land(rdrone_t* d, float height, float hover_yaw, float dur, float t) {
+    if (d->plan_state == PLAN_IDLE || d->plan_state == PLAN_LANDING) return;
+    const f3 p = cpos_(d), z = F3(0, 0, 0);
+    plan_7th(d, PLAN_LANDING, t, dur, p, d->c_yaw, z, 0, z, F3(p.x, p.y, height), hover_yaw);
+}
+/* go_to from a stopped planner (the only case here: process_command_queue stops the planner
+   before every command): plan_go_to_from the commander's last pos / vel / yaw, zero acc / rates */
+static void plan_go_to(rdrone_t* d, f3 hover_pos, float hover_yaw, float dur, int relative, float t) {
+    const f3 p0 = cpos_(d), v0 = F3(d->c_vel[0], d->c_vel[1], d->c_vel[2]), z = F3(0, 0, 0);
+    const float y0 = d->c_yaw;
+    if (relative) {
+        hover_pos = F3(hover_pos.x + p0.x, hover_pos.y + p0.y, hover_pos.z + p0.z);
+        hover_yaw += y0;
+    }
+    const float end_yaw = y0 + shortest_signed_angle_radians(y0, hover_yaw);
+    plan_7th(d, PLAN_FLYING, t, dur, p0, y0, v0, 0, z, hover_pos, end_yaw);
+}
+/* crtpCommanderHighLevelTellState(state) */
+static void hl_tell_state(rdrone_t* d) {
+    for (int k = 0; k < 3; ++k) { d->c_pos[k] = d->st_pos[k]; d->c_vel[k] = d->st_vel[k]; }
+    d->c_yaw = d->st_yaw * M_PI_F / 180.0f;
+}
+/* MellingerControl._update_setpoint (369-374) while full_state_cmd_override is off:
+   TellState(state), UpdateTime(t), GetSetpoint(setpoint, state) */
+static void hl_update_setpoint(rdrone_t* d, float t) {
+    hl_tell_state(d);
+    traj_eval_t ev;
+    int valid = 0;
+    if (d->plan_state != PLAN_IDLE) {   /* plan_current_goal */
+        if (d->plan_state == PLAN_LANDING && t - d->plan_t0 >= d->plan_dur * 1.0f) d->plan_state = PLAN_IDLE;
+        ev = plan_eval(d, t);
+        valid = 1;
+    }
+    if (!valid || d->plan_state == PLAN_IDLE) {   /* plan_stop; plan_is_stopped: keep the setpoint */
+        for (int k = 0; k < 3; ++k) { d->c_pos[k] = d->st_pos[k]; d->c_vel[k] = d->st_vel[k]; }
+        d->c_yaw = radiansf_(d->st_yaw);
+        return;
+    }
+    d->sp_pos[0] = ev.pos.x; d->sp_pos[1] = ev.pos.y; d->sp_pos[2] = ev.pos.z;
+    d->sp_vel[0] = ev.vel.x; d->sp_vel[1] = ev.vel.y; d->sp_vel[2] = ev.vel.z;
+    d->sp_acc[0] = ev.acc.x; d->sp_acc[1] = ev.acc.y; d->sp_acc[2] = ev.acc.z;
+    d->sp_yaw = degreesf_(ev.yaw);
+    d->sp_rate[0] = degreesf_(ev.omega.x); d->sp_rate[1] = degreesf_(ev.omega.y); d->sp_rate[2] = degreesf_(ev.omega.z);
+    d->sp_mode = SP_COMMANDER;
+    d->c_pos[0] = ev.pos.x; d->c_pos[1] = ev.pos.y; d->c_pos[2] = ev.pos.z;
+    d->c_vel[0] = ev.vel.x; d->c_vel[1] = ev.vel.y; d->c_vel[2] = ev.vel.z;
+    d->c_yaw = ev.yaw;
+}
+/* reset (MellingerControl.py:119-150): zeroed setpoint_t, override on, crtpCommanderHighLevelInit
+   (planner IDLE), _update_state from the initial obs row, TellState */
+static void hl_reset(rdrone_t* d, const double pos[3], const double rpy[3]) {
+    for (int k = 0; k < 3; ++k) {
+        d->sp_pos[k] = d->sp_vel[k] = d->sp_acc[k] = d->sp_rate[k] = 0;
+        d->st_pos[k] = (float)pos[k];
+        d->st_vel[k] = 0.0f;
+    }
+    d->sp_qz = d->sp_qw = d->sp_yaw = 0;
+    d->st_yaw = (float)(rpy[2] * RAD_TO_DEG);
+    d->plan_t0 = d->plan_dur = 0;
+    memset(d->coef, 0, sizeof d->coef);
+    d->plan_state = PLAN_IDLE;
+    d->override = 1;
+    d->sp_mode = SP_UNSET;
+    hl_tell_state(d);
+}
+/* _sendFullStateCmd (510-543): float setpoint fields from the float64 arguments */
+static void hl_fullstate(rdrone_t* d, const double pos[3], const double vel[3], const double acc[3], double yaw,
+                         const double rate[3]) {
+    double q[4], e3[3] = {0, 0, yaw};
+    orc_quat_from_euler(e3, q);   /* get_quaternion_from_euler(0, 0, yaw) */
+    for (int k = 0; k < 3; ++k) {
+        d->sp_pos[k] = (float)pos[k];
+        d->sp_vel[k] = (float)vel[k];
+        d->sp_acc[k] = (float)acc[k];
+        d->sp_rate[k] = (float)(rate[k] * RAD_TO_DEG);
+    }
+    d->sp_qz = (float)q[2];
+    d->sp_qw = (float)q[3];
+    d->sp_mode = SP_FULLSTATE;
+    d->override = 1;
+}
+/* one command message: low_level_control (17-61) -> send*Cmd -> process_command_queue(args[-1])
+   (292-303): crtpCommanderHighLevelStop, UpdateTime(args[-1]), then the queued _send*Cmd */
+static void hl_command(rdrone_t* d, int code, const double* a, int obs_wrapper) {
+    if (code <= ADRP_CMD_NONE || code > ADRP_CMD_NOTIFY) return;
+    d->plan_state = PLAN_IDLE;
+    const float t = (float)a[ADRP_CMD_TIME_SLOT];
+    switch (code) {
+        case ADRP_CMD_FULLSTATE:   /* DroneObservationWrapper zeroes the tuple's yaw (wrapper.py:56-57) */
+            hl_fullstate(d, a, a + 3, a + 6, obs_wrapper ? 0.0 : a[9], a + 10);
+            return;
+        case ADRP_CMD_TAKEOFF:     /* takeoff2, useCurrentYaw */
+            plan_takeoff(d, (float)a[0], d->c_yaw, (float)a[1], t);
+            break;
+        case ADRP_CMD_TAKEOFFYAW:
+            plan_takeoff(d, (float)a[0], (float)a[2], (float)a[1], t);
+            break;
+        case ADRP_CMD_TAKEOFFVEL: {  /* takeoff_with_velocity */
+            float h = (float)a[0];
+            if (a[2] != 0) h += d->c_pos[2];
+            const float v = (float)a[1] > 0 ? (float)a[1] : HL_DEFAULT_VELOCITY;
+            plan_takeoff(d, h, d->c_yaw, fabsf(h - d->c_pos[2]) / v, t);
+            break;
+        }
+        case ADRP_CMD_LAND:
+            plan_land(d, (float)a[0], d->c_yaw, (float)a[1], t);
+            break;
+        case ADRP_CMD_LANDYAW:
+            plan_land(d, (float)a[0], (float)a[2], (float)a[1], t);
+            break;
+        case ADRP_CMD_LANDVEL: {   /* land_with_velocity */
+            float h = (float)a[0];
+            if (a[2] != 0) h = d->c_pos[2] - h;
+            const float v = (float)a[1] > 0 ? (float)a[1] : HL_DEFAULT_VELOCITY;
+            plan_land(d, h, d->c_yaw, fabsf(h - d->c_pos[2]) / v, t);
+            break;
+        }
+        case ADRP_CMD_STOP:
+            break;
+        case ADRP_CMD_GOTO:
+            plan_go_to(d, F3((float)a[0], (float)a[1], (float)a[2]), (float)a[3], (float)a[4], a[5] != 0, t);
+            break;
+        case ADRP_CMD_NOTIFY:
+            hl_tell_state(d);
+            break;
+    }
+    d->override = 0;
+}
+
 /* computeControl(t, pos, rpy, vel, ang_vel, disturbance) -> rpm[4] */
 static lpf_t g_gyro_lpf;   /* written once in orc_create, before any (threaded) step */
 static void race_init_consts(void) { g_gyro_lpf = lpf_coeffs(FIRMWARE_FREQ, 30); }
 
-static void mellinger_compute(rdrone_t* d, const double sp_xyz[3], double sp_yaw, const double pos[3],
-                              const double rpy[3], const double vel[3], const double noise[4], double rpm[4]) {
+static void mellinger_compute(rdrone_t* d, const double pos[3], const double rpy[3], const double vel[3],
+                              const double noise[4], double rpm[4]) {
     const lpf_t gyro_lpf = g_gyro_lpf;   /* ACCEL_LPF_CUTOFF_FREQ (swapped); set by orc_create */
     double rates[3], acc[3];
     for (int k = 0; k < 3; ++k) {
@@ -240,13 +496,12 @@ static void mellinger_compute(rdrone_t* d, const double sp_xyz[3], double sp_yaw
     float st_acc_z = (float)acc[2];
     /* _update_sensorData: gyro = lpf2p(rates in deg/s); the acc channel only feeds the
        firmware's log variable and is not modelled */
+    for (int k = 0; k < 3; ++k) { d->st_pos[k] = st_pos[k]; d->st_vel[k] = st_vel[k]; }
+    d->st_yaw = (float)(rpy[2] * RAD_TO_DEG);   /* state.attitude.yaw [deg] */
     float gyro[3];
     for (int k = 0; k < 3; ++k) gyro[k] = lpf_apply(&gyro_lpf, &d->lpf_d1[k], &d->lpf_d2[k], (float)(rates[k] * RAD_TO_DEG));
-    /* setpoint (FULLSTATE): position, attitudeQuaternion from yaw */
-    double spq[4], e3[3] = {0, 0, sp_yaw};
-    orc_quat_from_euler(e3, spq);
-    float sp_pos[3] = {(float)sp_xyz[0], (float)sp_xyz[1], (float)sp_xyz[2]};
-    float sp_quat[4] = {(float)spq[0], (float)spq[1], (float)spq[2], (float)spq[3]};
+    /* _update_setpoint(self.tick / FIRMWARE_FREQ) (369-374) */
+    if (!d->override) hl_update_setpoint(d, (float)(d->tick / (double)FIRMWARE_FREQ));
     /* _step_controller */
     double pwm[4];
     if (st_acc_z < -0.5f) d->tumble += 1; else d->tumble = 0;
@@ -264,7 +519,7 @@ static void mellinger_compute(rdrone_t* d, const double sp_xyz[3], double sp_yaw
         } else {
             t = 1;
         }
-        mellinger_fw(d, sp_pos, sp_quat, gyro, st_pos, st_vel, st_q, t);
+        mellinger_fw(d, gyro, st_pos, st_vel, st_q, t);
         d->tick += 1;
         double c[4] = {d->ctl[0], d->ctl[1], d->ctl[2], d->ctl[3]};
         orc_compute_pwms(c, pwm);
@@ -631,6 +886,8 @@ static void race_reset_env(orc_t* o, int e, float* obs_env) {
         double nom_rpy[3], zero[3] = {0, 0, 0};
         body_rpy(b, nom_rpy);
         mellinger_wrapper_reset(d, nom_rpy, zero);
+        const double nom_pos[3] = {b->pos.x, b->pos.y, b->pos.z};
+        hl_reset(d, nom_pos, nom_rpy);
         d->kin_pos = b->pos;                 /* self.pos still holds the nominal pose */
         d->mass = t->race_mass;
         d->inertia = V(t->race_inertia[0], t->race_inertia[1], t->race_inertia[2]);
@@ -807,6 +1064,20 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
     body_t* bs = &o->b[(size_t)e * N];
     rdrone_t* ds = &o->rd[(size_t)e * N];
     int touched = 0;
+    /* the command message per drone (190-210): FULLSTATE (act[:3], 0, 0, act[3], 0, step_counter)
+       from an ndarray action (act = NULL: the commands adrp_race_command / orc_race_command sent);
+       eliminated drones get STOP [step_counter] */
+    for (int i = 0; i < N; ++i) {
+        double a[ADRP_CMD_ARGS] = {0};
+        a[ADRP_CMD_TIME_SLOT] = o->step_counter[e];
+        if (ds[i].elim) {
+            hl_command(&ds[i], ADRP_CMD_STOP, a, 0);
+        } else if (act) {
+            for (int k = 0; k < 3; ++k) a[k] = act[(size_t)i * 4 + k];
+            a[9] = act[(size_t)i * 4 + 3];   /* zeroed under the DroneObservationWrapper (wrapper.py:51-57) */
+            hl_command(&ds[i], ADRP_CMD_FULLSTATE, a, t->obs_wrapper);
+        }
+    }
     for (int s = 0; s < o->S; ++s) {
         const uint32_t idx = (uint32_t)(o->step_counter[e] + s);
         if (c->physics != ADRP_PHYS_PYB)     /* KIN_PHYSICS: _updateAndStoreKinematicInformation */
@@ -848,11 +1119,8 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
             }
             double rpy[3], pos[3] = {bs[i].pos.x, bs[i].pos.y, bs[i].pos.z}, vel[3] = {bs[i].vel.x, bs[i].vel.y, bs[i].vel.z};
             body_rpy(&bs[i], rpy);
-            const float* a = act + (size_t)i * 4;
-            double sp[3] = {a[0], a[1], a[2]};
             memcpy(d->prev_rpm, d->rpm, sizeof d->rpm);
-            /* DroneObservationWrapper.step zeroes the yaw of every ndarray action (wrapper.py:51-57) */
-            mellinger_compute(d, sp, t->obs_wrapper ? 0.0 : (double)a[3], pos, rpy, vel, noise, d->rpm);
+            mellinger_compute(d, pos, rpy, vel, noise, d->rpm);
         }
     }
     o->contact[e] = (uint8_t)touched;
@@ -973,6 +1241,77 @@ static void race_set_row(orc_t* o, size_t slot, int e, int first, const double* 
     }
     d->tick = iv[2]; d->last_att_tick = iv[3]; d->last_pos_tick = iv[4]; d->tumble = iv[5]; d->gate = iv[6];
     d->elim = iv[7] & 1; d->fin = (iv[7] >> 1) & 1;
+}
+
+/* ---- high-level commands ---------------------------------------------------------------- */
+int orc_race_command(orc_t* o, const int32_t* cmd, const double* args) {
+    if (o->cfg.task != ADRP_TASK_RACE) return fail("commands: MultiRaceAviary only");
+    const size_t EN = (size_t)o->E * o->N;
+    for (size_t slot = 0; slot < EN; ++slot) {
+        rdrone_t* d = &o->rd[slot];
+        if (d->elim) {   /* MultiRaceAviary.py:198-199 */
+            double a[ADRP_CMD_ARGS] = {0};
+            a[ADRP_CMD_TIME_SLOT] = o->step_counter[slot / o->N];
+            hl_command(d, ADRP_CMD_STOP, a, 0);
+        } else {
+            hl_command(d, cmd[slot], args + slot * ADRP_CMD_ARGS, o->cfg.track.obs_wrapper);
+        }
+    }
+    return ADRP_OK;
+}
+/* float fields in adrp.h order: sp pos 3, vel 3, acc 3, rate 3, qz, qw, yaw; commander pos 3,
+   vel 3, yaw; state pos 3, vel 3, yaw; t_begin, duration, coef 32 */
+static void cmd_fields(rdrone_t* d, float* p[ADRP_CMD_NF], int* q[ADRP_CMD_NI]) {
+    int n = 0;
+    for (int k = 0; k < 3; ++k) p[n++] = &d->sp_pos[k];
+    for (int k = 0; k < 3; ++k) p[n++] = &d->sp_vel[k];
+    for (int k = 0; k < 3; ++k) p[n++] = &d->sp_acc[k];
+    for (int k = 0; k < 3; ++k) p[n++] = &d->sp_rate[k];
+    p[n++] = &d->sp_qz; p[n++] = &d->sp_qw; p[n++] = &d->sp_yaw;
+    for (int k = 0; k < 3; ++k) p[n++] = &d->c_pos[k];
+    for (int k = 0; k < 3; ++k) p[n++] = &d->c_vel[k];
+    p[n++] = &d->c_yaw;
+    for (int k = 0; k < 3; ++k) p[n++] = &d->st_pos[k];
+    for (int k = 0; k < 3; ++k) p[n++] = &d->st_vel[k];
+    p[n++] = &d->st_yaw;
+    p[n++] = &d->plan_t0; p[n++] = &d->plan_dur;
+    for (int a = 0; a < 4; ++a) for (int k = 0; k < 8; ++k) p[n++] = &d->coef[a][k];
+    q[0] = &d->plan_state; q[1] = &d->override; q[2] = &d->sp_mode;
+}
+int orc_get_command_state(const orc_t* o, float* f, int32_t* ii) {
+    if (o->cfg.task != ADRP_TASK_RACE) return fail("commands: MultiRaceAviary only");
+    const size_t EN = (size_t)o->E * o->N;
+    for (size_t slot = 0; slot < EN; ++slot) {
+        float* p[ADRP_CMD_NF];
+        int* q[ADRP_CMD_NI];
+        cmd_fields(&o->rd[slot], p, q);
+        for (int k = 0; k < ADRP_CMD_NF; ++k) f[k * EN + slot] = *p[k];
+        for (int k = 0; k < ADRP_CMD_NI; ++k) ii[k * EN + slot] = *q[k];
+    }
+    return ADRP_OK;
+}
+int orc_set_command_state(orc_t* o, const float* f, const int32_t* ii) {
+    if (o->cfg.task != ADRP_TASK_RACE) return fail("commands: MultiRaceAviary only");
+    const size_t EN = (size_t)o->E * o->N;
+    for (size_t slot = 0; slot < EN; ++slot) {
+        float* p[ADRP_CMD_NF];
+        int* q[ADRP_CMD_NI];
+        cmd_fields(&o->rd[slot], p, q);
+        for (int k = 0; k < ADRP_CMD_NF; ++k) *p[k] = f[k * EN + slot];
+        for (int k = 0; k < ADRP_CMD_NI; ++k) *q[k] = ii[k * EN + slot];
+    }
+    return ADRP_OK;
+}
+void orc_poly4d_eval(const float* coef, float t, float out[13]) {
+    float c[4][8];
+    memcpy(c, coef, sizeof c);
+    traj_eval_t ev = poly4d_eval((const float(*)[8])c, t);
+    const f3 v[4] = {ev.pos, ev.vel, ev.acc, ev.omega};
+    for (int k = 0; k < 4; ++k) { out[3 * k] = v[k].x; out[3 * k + 1] = v[k].y; out[3 * k + 2] = v[k].z; }
+    out[12] = ev.yaw;
+}
+void orc_poly7_nojerk(float T, float x0, float dx0, float ddx0, float xf, float dxf, float ddxf, float out[8]) {
+    poly7_nojerk(out, T, x0, dx0, ddx0, xf, dxf, ddxf);
 }
 
 /* ---- unit entry points for tests ------------------------------------------------------ */

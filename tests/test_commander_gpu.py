@@ -1,0 +1,145 @@
+"""High-level command mode of the race kernel vs the CPU oracle.  Needs an
+MI355X: -m gpu.
+
+Both sides restate the firmware's commander / planner (csrc/commander.h, oracle/race.c hl_*;
+parity with pycffirmware itself is unpinned).  Teacher forcing as in test_race_gpu.py: every
+step starts from the oracle's state (body + command state, float32-representable), one command
+per drone is sent to both, one env.step is compared.  Every env follows its own script mixing
+all eleven commands, so FLYING / IDLE planners, FULLSTATE / commander / unset setpoints and
+overrides on and off all occur in one launch.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from gym_pybullet_adrp_amd.commands import encode_commands  # noqa: E402
+from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary  # noqa: E402
+from gym_pybullet_adrp_amd.utils.enums import Command, Physics, RaceMode  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+from test_race_gpu import check_state, sync  # noqa: E402
+
+PLAN, OVR, MODE = 0, 1, 2
+T0, DUR, COEF = 29, 30, 31
+
+
+def script(e, k, obs0, n):
+    """command of drone n of env e at step k"""
+    p = obs0[e, n, :3].astype(float)
+    z3 = np.zeros(3)
+    v = (e + n) % 6
+    if k == 0:
+        return [(Command.TAKEOFF, [0.5, 1.0]), (Command.TAKEOFFYAW, [0.6, 0.8, 0.4]),
+                (Command.TAKEOFFVEL, [0.4, 0.5, True]), (Command.GOTO, [p + [0.2, 0.1, 0.5], 0.2, 1.5, False]),
+                (Command.FULLSTATE, [p + [0, 0, 0.5], [0.1, 0, 0.2], [0.5, 0.5, 0.5], 0.3, [0, 0, 0.2], 0.0]),
+                (Command.NONE, [])][v]
+    if k == 3:
+        return [(Command.GOTO, [np.array([0.1, -0.2, 0.2]), 0.5, 1.0, True]), (Command.NOTIFY, [0.12]),
+                (Command.LAND, [0.0, 2.0]), (Command.STOP, [0.12]),
+                (Command.LANDYAW, [0.1, 1.0, 0.2]), (Command.TAKEOFF, [0.7, 0.5])][v]
+    if k == 5:
+        return [(Command.FULLSTATE, [p + [0.3, 0, 0.6], z3, z3, -0.2, z3, 0.2]), (Command.LANDVEL, [0.2, 0.3, True]),
+                (Command.GOTO, [p + [-0.2, 0.3, 0.6], -0.5, 0.6, False]), (Command.NOTIFY, [0.2]),
+                (Command.NONE, []), (Command.GOTO, [np.array([0.0, 0.0, 0.1]), 3.0, 0.4, True])][v]
+    return (Command.NONE, [])
+
+
+def encode_step(k, obs0, E, N):
+    return encode_commands([[script(e, k, obs0, n) for n in range(N)] for e in range(E)], E, N)
+
+
+def sync_cmd(env, orc):
+    f, i = orc.get_command_state()
+    env.set_command_state(torch.from_numpy(f), torch.from_numpy(i))
+
+
+def check_cmd(env, orc, rtol):
+    fg, ig = (t.cpu().numpy() for t in env.get_command_state())
+    fo, io = orc.get_command_state()
+    np.testing.assert_array_equal(ig, io)
+    np.testing.assert_array_equal(fg[T0], fo[T0])
+    np.testing.assert_allclose(fg[DUR], fo[DUR], rtol=1e-6)
+    np.testing.assert_allclose(fg[COEF:], fo[COEF:], rtol=1e-4, atol=1e-4)
+    # setpoint / commander / firmware-state fields follow the closed-loop state
+    np.testing.assert_allclose(fg[:COEF], fo[:COEF], rtol=rtol, atol=5e-3)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+@pytest.mark.parametrize("level,N,physics,mode", [("level0", 2, Physics.PYB, RaceMode.COMPARE),
+                                                  ("level3", 3, Physics.PYB_DW, RaceMode.COMPETE)])
+def test_commands_teacher_forced(level, N, physics, mode, precision):
+    E = 48
+    env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=11,
+                          autoreset=False, precision=precision, commands=True)
+    orc = O.Oracle(env.cfg.copy())
+    env.reset()
+    obs0 = orc.reset()
+    sync(env, orc)
+    sync_cmd(env, orc)
+    for k in range(8):
+        codes, args = encode_step(k, obs0, E, N)
+        orc.command(codes, args)
+        obs_o, rew_o, te_o, tr_o, _ = orc.step(None)
+        obs_g, rew_g, te_g, tr_g, _ = env.step((codes, args))
+        check_cmd(env, orc, 2e-3)
+        check_state(env, orc, 2e-3)
+        og = obs_g.cpu().numpy()
+        np.testing.assert_allclose(og[..., :3], obs_o[..., :3], rtol=1e-3, atol=1e-3)
+        np.testing.assert_array_equal(te_g.cpu().numpy(), te_o)
+        sync(env, orc)
+        sync_cmd(env, orc)
+    env.close()
+
+
+def test_tuple_actions_through_step():
+    """the reference's list-of-tuples action (E = 1) through MultiRaceAviary.step, and ndarray
+    actions in command mode (FULLSTATE sent by the step kernel) against the oracle"""
+    N = 2
+    env = MultiRaceAviary("level0", num_drones=N, num_envs=1, seed=3, autoreset=False)
+    orc = O.Oracle(env.cfg.copy())
+    env.reset()
+    obs0 = orc.reset()
+    acts = [[(Command.TAKEOFF, [0.5, 1.0]), (Command.GOTO, [obs0[0, 1, :3] + [0, 0, 0.5], 0.0, 1.0, False])]]
+    acts += [[(Command.NONE, []), (Command.NONE, [])]] * 3
+    for a in acts:
+        codes, args = encode_commands(a, 1, N)
+        orc.command(codes, args)
+        obs_o, *_ = orc.step(None)
+        obs_g, *_ = env.step(a[0])   # the reference's format: one (Command, args) per drone
+        np.testing.assert_allclose(obs_g.cpu().numpy()[..., :12], obs_o[..., :12], rtol=2e-3, atol=2e-3)
+        sync(env, orc)
+        sync_cmd(env, orc)
+    assert env.commands
+    tgt = np.concatenate([obs0[:, :, :3] + [0.1, 0, 0.6], np.zeros((1, N, 1))], -1).astype(np.float32)
+    for _ in range(3):
+        obs_o, *_ = orc.step(tgt)
+        obs_g, *_ = env.step(torch.from_numpy(tgt).to(env.device))
+        check_cmd(env, orc, 2e-3)
+        check_state(env, orc, 2e-3)
+        sync(env, orc)
+        sync_cmd(env, orc)
+    env.close()
+
+
+def test_enable_commands_matches_reset_state():
+    """adrp_enable_commands after a reset leaves what a reset in command mode leaves"""
+    E, N = 16, 3
+    a = MultiRaceAviary("level2", num_drones=N, num_envs=E, seed=8, autoreset=False)
+    b = MultiRaceAviary("level2", num_drones=N, num_envs=E, seed=8, autoreset=False, commands=True)
+    a.reset()
+    b.reset()
+    a.enable_commands()
+    fa, ia = (t.cpu().numpy() for t in a.get_command_state())
+    fb, ib = (t.cpu().numpy() for t in b.get_command_state())
+    np.testing.assert_array_equal(ia, ib)
+    np.testing.assert_array_equal(fa, fb)
+    orc = O.Oracle(b.cfg.copy())
+    orc.reset()
+    fo, io = orc.get_command_state()
+    np.testing.assert_array_equal(ib, io)
+    np.testing.assert_allclose(fb, fo, atol=1e-6)
+    a.close()
+    b.close()
