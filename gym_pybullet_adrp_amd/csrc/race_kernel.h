@@ -1350,6 +1350,13 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     __shared__ TrackJobs tjobs;
     constexpr bool pre = PRE == 2;
     const int tl = threadIdx.x % kRaceBlock;
+    // Barrier protocol (every wave passes the same count before the helpers exit):
+    //   PRE == 2: helpers  B1 after the draws of s < S/2, B2 after the rest;
+    //             chain    B1 before the sub-step loop,  B2 at s == S/2 (reached once for every
+    //                      1 <= S <= kRacePreS: S/2 < S; S = 1 puts it on s = 0, right after B1).
+    //   PRE == 1: helpers  B2 after the track copy;  chain  B2 after the sub-step loop.
+    // Later barriers (GJK pooling, copy-out) see only the chain wave: exited waves do not count.
+    // test_helper_waves_bit_identical runs S = 20, 5 and 1 with and without the helpers.
     if (threadIdx.x >= kRaceBlock) {   // helper waves
         if constexpr (PRE) {
             const int hw = int(threadIdx.x / kRaceBlock) - 1;

@@ -317,18 +317,22 @@ def test_masked_reset():
     env.close()
 
 
+@pytest.mark.parametrize("ctrl_freq", [25, 100, 500])
 @pytest.mark.parametrize("E,N,level,physics,mode", [(300, 2, "level0", Physics.PYB, RaceMode.COMPARE),
                                                     (333, 4, "level3", Physics.PYB_DW, RaceMode.COMPETE),
                                                     (37, 3, "level2", Physics.PYB, RaceMode.COMPETE)])
-def test_helper_waves_bit_identical(monkeypatch, E, N, level, physics, mode):
-    """the fp32 kernel's helper waves (LDS track copy / pre-drawn disturbances) change who computes,
-    not what: 40 auto-reset env.steps with and without them (ADRP_RACE_HELPERS=0) agree bit for bit
-    (measured; the variants' code generation happens to contract identically)"""
+def test_helper_waves_bit_identical(monkeypatch, E, N, level, physics, mode, ctrl_freq):
+    """the one-lane fp32 kernel's helper waves (LDS track copy / pre-drawn disturbances, handed over
+    at two barriers: before the sub-step loop and at its middle, s = S / 2) change who computes, not
+    what: 40 auto-reset env.steps with and without them (ADRP_RACE_HELPERS=0) agree bit for bit, for
+    S = 20, an odd S = 5 and S = 1 (ctrl_freq 25 / 100 / 500), where the mid-loop barrier falls on the
+    first sub-step (measured; the variants' code generation happens to contract identically)"""
+    monkeypatch.setenv("ADRP_RACE_QUAD", "0")   # the helpers belong to the one-lane kernel
     outs = []
     for helpers in ("1", "0"):
         monkeypatch.setenv("ADRP_RACE_HELPERS", helpers)
         env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=3,
-                              autoreset=True, reward="wrapper")
+                              autoreset=True, reward="wrapper", ctrl_freq=ctrl_freq)
         obs, _ = env.reset()
         act = torch.from_numpy(targets(np.random.default_rng(4), obs.cpu().numpy(), E, N)).to(env.device)
         seq = []
