@@ -208,13 +208,15 @@ def time_graph(stepper, acts, K, W, world, dev):
     return float(el.item()), G
 
 
-def kernel_times(env, acts, n):
+def kernel_times(env, acts, n, stepper=None):
     """per-launch durations (ms) of the step kernel: start/stop events attached to its own
-    dispatch (hipExtLaunchKernelGGL in libadrp) on the launching stream"""
+    dispatch (hipExtLaunchKernelGGL in libadrp) on the launching stream.  stepper: what drives the
+    steps (the policy loop of a closed-loop bench), default env.step on the synthetic actions"""
+    stepper = stepper or env
     torch.cuda.synchronize()
     env.h.profile_begin(n)
     for k in range(n):
-        env.step(acts[k % acts.shape[0]])
+        stepper.step(acts[k % acts.shape[0]])
     return np.asarray(env.h.profile_end(n))
 
 
@@ -335,7 +337,7 @@ def bench_race(level, drones, physics, racemode, precision, E, K, W, world, rank
                 return env.step(pact)
         stepper = _Loop()
     elapsed, G = time_graph(stepper, acts, K, W, world, dev)
-    kern = kernel_times(env, acts, min(K, 512))
+    kern = kernel_times(env, acts, min(K, 512), stepper)   # closed loop: the actor-driven steps
     key = race_key(level, drones, physics, precision, E)
     rec = {"workload": f"MultiRaceAviary {racemode} {level}, {drones} drones x {E} envs per GPU, Physics.{physics} "
                        f"500/25 Hz (20 sub-steps, Mellinger 500 Hz), {precision}",

@@ -264,7 +264,8 @@ static RaceConst<Real> race_const(const adrp_config& c) {
 
 template <typename Real>
 static int upload_race_const(adrp_t* h) {
-    const RaceConst<Real> k = race_const<Real>(h->cfg);
+    RaceConst<Real> k = race_const<Real>(h->cfg);
+    k.refine = h->race_refine ? 1 : 0;
     // [RaceConst | tick-schedule tables (att, pos)] (race_args)
     std::vector<uint32_t> ticks(2 * kTickWords);
     race_tick_tables(ticks.data(), ticks.data() + kTickWords);
@@ -372,6 +373,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     if (const char* env = getenv("ADRP_RESET_HELPER")) h->reset_helper = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RACE_HELPERS")) h->race_helpers = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RACE_QUAD")) h->race_quad = atoi(env) != 0;
+    if (const char* env = getenv("ADRP_RACE_REFINE")) h->race_refine = atoi(env) != 0;
     const int rc = race ? (h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h))
                         : (h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h));
     if (rc != ADRP_OK) return cleanup(seterr(h, rc, "constant block upload failed"));
@@ -674,10 +676,11 @@ extern "C" int adrp_set_diagnostics(adrp_t* h, int enable) {
 // timing build only (not declared in include/adrp.h): per-phase s_memtime sums of the step
 // kernels -- race: [setup, physics, controller, rays, obs, contacts, tail, total, waves, -]
 // sums over waves, the same phases' max over waves at [10..17], GJK calls/iterations at
-// 9/18/19; hover: tools/hover_phases.py.  Summed over the four kernel code objects.
+// 9/18/19; hover: tools/hover_phases.py.  Summed over the kernel code objects.
 extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
-    int (*readers[4])(unsigned long long*, int) = {phase_read_hover_f32, phase_read_hover_f64, phase_read_race_f32,
-                                                  phase_read_race_f64};
+    int (*readers[7])(unsigned long long*, int) = {phase_read_hover_f32, phase_read_hover_f64, phase_read_race_f32,
+                                                  phase_read_race_f32b, phase_read_race_f32c, phase_read_race_f64,
+                                                  phase_read_race_f64b};
     for (int k = 0; k < 32; ++k) out[k] = 0;
     for (auto rd : readers) {
         unsigned long long v[32];

@@ -1,6 +1,15 @@
-// race_f32.hip — race kernels and launchers for Real = float (own translation unit so
-// the kernel instantiations compile in parallel)
+// race_f32.hip — race kernels and launchers for Real = float.  The step kernels of the physics
+// modes are split over three translation units (race_f32.hip: PYB, PYB_DW — the benched ones and
+// the dispatch; race_f32b.hip: DYN, PYB_GND; race_f32c.hip: PYB_DRAG, PYB_GND_DRAG_DW), so
+// they compile in parallel.
 #include "race_launch.h"
+
+extern template ADRP_RACE_STEP_PH(float, ADRP_PHYS_DYN);
+extern template ADRP_RACE_STEP_PH(float, ADRP_PHYS_PYB_GND);
+extern template ADRP_RACE_STEP_PH(float, ADRP_PHYS_PYB_DRAG);
+extern template ADRP_RACE_STEP_PH(float, ADRP_PHYS_PYB_GND_DRAG_DW);
+template ADRP_RACE_STEP_PH(float, ADRP_PHYS_PYB);
+template ADRP_RACE_STEP_PH(float, ADRP_PHYS_PYB_DW);
 
 template int race_step<float>(adrp_t*, const float*, float*, float*, uint8_t*, uint8_t*, float*, hipStream_t);
 template int race_reset<float>(adrp_t*, const uint8_t*, float*, hipStream_t);

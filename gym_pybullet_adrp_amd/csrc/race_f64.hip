@@ -1,6 +1,15 @@
-// race_f64.hip — race kernels and launchers for Real = double (own translation unit so
-// the kernel instantiations compile in parallel)
+// race_f64.hip — race kernels and launchers for Real = double.  PYB, PYB_DW and DYN here, the
+// other physics modes in race_f64b.hip (parallel build).
 #include "race_launch.h"
+
+extern template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_GND);
+extern template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_DRAG);
+extern template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_GND_DRAG_DW);
+#ifndef ADRP_DEV_FAST
+template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB);
+template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_DW);
+template ADRP_RACE_STEP_PH(double, ADRP_PHYS_DYN);
+#endif
 
 template int race_step<double>(adrp_t*, const float*, float*, float*, uint8_t*, uint8_t*, float*, hipStream_t);
 template int race_reset<double>(adrp_t*, const uint8_t*, float*, hipStream_t);

@@ -49,6 +49,7 @@ template <typename Real>
 struct RaceConst {
     int N, S, physics, link_lag, compete, num_gates, num_obstacles, trunc_steps;
     int disturbances, reward_wrapper, obs_wrapper, random_gates, random_state, random_inertia, D, autoreset;
+    int refine;   // support-function bounds for the pairs the centre-distance bounds leave open (ADRP_RACE_REFINE)
     Real dt, gravity, kf, km, hover_unused;
     Real px[4], py[4], pz[4];
     Real gnd_kf, prop_r4, gnd_clip, drag[3], dw1, dw2, dw3, prop_r;
@@ -866,6 +867,42 @@ __device__ __forceinline__ Real point_part_dist(V3<Real> lp, V3<Real> h, Real r,
     return hsqrt_(dx * dx + dy * dy + dz * dz);
 }
 
+// Support-function bounds of one (drone cylinder, part) pair in the part's frame: lp = the centre of
+// the drone's collision cylinder, ax = its axis (unit), dr / dhh = its radius / half height.  With q
+// the part point closest to lp and n = (q - lp) / |q - lp|, the (convex) part lies beyond the plane
+// through q normal to n, so every cylinder point x is at least |q - lp| - (x - lp).n from it:
+//   lo = |q - lp| - (dr |n - (n.a) a| + dhh |n.a|)          (the cylinder's support in direction n),
+// and the cylinder's support point x* in direction n is a point of the drone:  up = dist(x*, part).
+// For a flat face both are the exact distance; near edges the band is second order.  The centre
+// bounds (|q - lp| - sqrt(dr^2 + dhh^2), |q - lp|) leave every pair within 6 cm of a cut open.
+template <typename Real>
+__device__ __forceinline__ void part_bounds_refined(V3<Real> lp, V3<Real> ax, V3<Real> h, Real r, int cyl, Real dr,
+                                                    Real dhh, Real& lo, Real& up) {
+    V3<Real> q;
+    if (cyl) {
+        const Real rho = hsqrt_(lp.x * lp.x + lp.y * lp.y);
+        const Real k = rho > r ? r * rcp_(rho) : Real(1);
+        q = v3(lp.x * k, lp.y * k, clampr_(lp.z, -h.z, h.z));
+    } else {
+        q = v3(clampr_(lp.x, -h.x, h.x), clampr_(lp.y, -h.y, h.y), clampr_(lp.z, -h.z, h.z));
+    }
+    const V3<Real> d = q - lp;
+    const Real pd = hsqrt_(dot(d, d));
+    if (!(pd > Real(1e-6))) {   // the drone's centre is (almost) in the part: only up = 0 is known
+        lo = Real(-1);
+        up = Real(0);
+        return;
+    }
+    const V3<Real> n = rcp_(pd) * d;
+    const Real c = dot(n, ax);
+    const V3<Real> sp = n - c * ax;
+    const Real sn = hsqrt_(dot(sp, sp));
+    lo = pd - (dr * sn + dhh * fabs_(c));
+    const Real k = sn > Real(1e-6) ? dr * rcp_(sn) : Real(0);
+    const V3<Real> x = lp + (c >= Real(0) ? dhh : -dhh) * ax + k * sp;
+    up = point_part_dist(x, h, r, cyl);
+}
+
 constexpr int kGateParts = 5, kObstParts = 2, kObstBit0 = ADRP_MAX_GATES * kGateParts;
 constexpr int kRaceMaxD = 49 + 6 * (ADRP_MAX_DRONES - 1);   // obs row floats (COMPETE, 8 drones)
 constexpr int kTrackFields = RF_WR_TARGET - RF_GATE;   // the env's actual gates (16) + obstacles (12)
@@ -925,7 +962,7 @@ __device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS&
                                              uint32_t& amb, uint32_t& camb_all) {
     const Real tol = sizeof(Real) == 4 ? Real(1e-5) : Real(1e-10);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
-    const V3<Real> p = ds.c;
+    const V3<Real> p = ds.c, ax = col2(ds.R);
     amb = 0; camb_all = 0;
     gin = 0; oin = 0;
 #pragma unroll
@@ -935,6 +972,7 @@ __device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS&
             Real sn, cs;
             sincos_(T(RF_GATE + 4 * g + 3), &sn, &cs);
             const V3<Real> lg = v3(cs * dp.x + sn * dp.y, -sn * dp.x + cs * dp.y, dp.z);   // Rz(yaw)^T dp
+            const V3<Real> ag = v3(cs * ax.x + sn * ax.y, -sn * ax.x + cs * ax.y, ax.z);
             const int low = C.gate_type[g] > 0;
             bool in = false;
             uint32_t gamb = 0, camb = 0;
@@ -945,10 +983,18 @@ __device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS&
                 Real r;
                 int cyl;
                 gate_part(k, low, off, R, h, r, cyl);
-                const Real pd = point_part_dist(mulT(R, lg - off), h, r, cyl);
-                in |= pd < cut - tol;
-                if (pd - dr < cut + tol) gamb |= 1u << k;
-                if (want_contact && pd - dr < ccut + tol) camb |= 1u << k;
+                const V3<Real> lp = mulT(R, lg - off);
+                const Real pd = point_part_dist(lp, h, r, cyl);
+                Real lo = pd - dr, up = pd;
+                if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || (want_contact && lo < ccut + tol))) {
+                    Real lo2, up2;
+                    part_bounds_refined(lp, mulT(R, ag), h, r, cyl, ds.r, ds.h.z, lo2, up2);
+                    lo = fmaxr_(lo, lo2);
+                    up = up2 < up ? up2 : up;
+                }
+                in |= up < cut - tol;
+                if (lo < cut + tol) gamb |= 1u << k;
+                if (want_contact && lo < ccut + tol) camb |= 1u << k;
             }
             if (in) gin |= 1u << g;
             amb |= ((in ? 0u : gamb) | camb) << (g * kGateParts);
@@ -968,9 +1014,16 @@ __device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS&
                 int cyl;
                 obst_part(k, off, h, r, cyl);
                 const Real pd = point_part_dist(dp - off, h, r, cyl);
-                in |= pd < cut - tol;
-                if (pd - dr < cut + tol) gamb |= 1u << k;
-                if (want_contact && pd - dr < ccut + tol) camb |= 1u << k;
+                Real lo = pd - dr, up = pd;
+                if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || (want_contact && lo < ccut + tol))) {
+                    Real lo2, up2;
+                    part_bounds_refined(dp - off, ax, h, r, cyl, ds.r, ds.h.z, lo2, up2);
+                    lo = fmaxr_(lo, lo2);
+                    up = up2 < up ? up2 : up;
+                }
+                in |= up < cut - tol;
+                if (lo < cut + tol) gamb |= 1u << k;
+                if (want_contact && lo < ccut + tol) camb |= 1u << k;
             }
             if (in) oin |= 1u << o;
             amb |= ((in ? 0u : gamb) | camb) << (kObstBit0 + o * kObstParts);

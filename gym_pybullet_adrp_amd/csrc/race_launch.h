@@ -83,6 +83,16 @@ static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t*
     else by_g(std::integral_constant<int, 0>{});
 }
 
+// one physics mode's step kernels; explicitly instantiated in race_f32*.hip / race_f64*.hip so the
+// physics modes compile in parallel translation units (the dispatching unit declares the others
+// extern)
+template <typename Real, int PH>
+int race_step_ph(adrp_t* h, const RaceArgs<Real>& a, int G, hipStream_t s) {
+    launch_race_g<Real, PH>(a, G, s, h);
+    return ADRP_OK;
+}
+#define ADRP_RACE_STEP_PH(R, PH) int race_step_ph<R, PH>(adrp_t*, const RaceArgs<R>&, int, hipStream_t)
+
 template <typename Real>
 int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
                      float* tobs, hipStream_t s) {
@@ -93,17 +103,17 @@ int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term
     if (sizeof(Real) != 4 || (h->cfg.physics != ADRP_PHYS_PYB && h->cfg.physics != ADRP_PHYS_PYB_DW) || (G != 2 && G != 4))
         return seterr(h, ADRP_ERR_INVALID, "dev build: race config not instantiated");
     if constexpr (sizeof(Real) == 4) {
-        if (h->cfg.physics == ADRP_PHYS_PYB) launch_race_g<Real, ADRP_PHYS_PYB>(a, G, s, h);
-        else launch_race_g<Real, ADRP_PHYS_PYB_DW>(a, G, s, h);
+        if (h->cfg.physics == ADRP_PHYS_PYB) race_step_ph<Real, ADRP_PHYS_PYB>(h, a, G, s);
+        else race_step_ph<Real, ADRP_PHYS_PYB_DW>(h, a, G, s);
     }
 #else
     switch (h->cfg.physics) {
-        case ADRP_PHYS_PYB: launch_race_g<Real, ADRP_PHYS_PYB>(a, G, s, h); break;
-        case ADRP_PHYS_DYN: launch_race_g<Real, ADRP_PHYS_DYN>(a, G, s, h); break;
-        case ADRP_PHYS_PYB_GND: launch_race_g<Real, ADRP_PHYS_PYB_GND>(a, G, s, h); break;
-        case ADRP_PHYS_PYB_DRAG: launch_race_g<Real, ADRP_PHYS_PYB_DRAG>(a, G, s, h); break;
-        case ADRP_PHYS_PYB_DW: launch_race_g<Real, ADRP_PHYS_PYB_DW>(a, G, s, h); break;
-        default: launch_race_g<Real, ADRP_PHYS_PYB_GND_DRAG_DW>(a, G, s, h); break;
+        case ADRP_PHYS_PYB: race_step_ph<Real, ADRP_PHYS_PYB>(h, a, G, s); break;
+        case ADRP_PHYS_DYN: race_step_ph<Real, ADRP_PHYS_DYN>(h, a, G, s); break;
+        case ADRP_PHYS_PYB_GND: race_step_ph<Real, ADRP_PHYS_PYB_GND>(h, a, G, s); break;
+        case ADRP_PHYS_PYB_DRAG: race_step_ph<Real, ADRP_PHYS_PYB_DRAG>(h, a, G, s); break;
+        case ADRP_PHYS_PYB_DW: race_step_ph<Real, ADRP_PHYS_PYB_DW>(h, a, G, s); break;
+        default: race_step_ph<Real, ADRP_PHYS_PYB_GND_DRAG_DW>(h, a, G, s); break;
     }
 #endif
     HIPCHK(h, hipGetLastError());

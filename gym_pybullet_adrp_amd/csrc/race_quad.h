@@ -175,7 +175,7 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
     using Real = float;
     const Real tol = Real(1e-5);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
-    const V3<Real> p = ds.c;
+    const V3<Real> p = ds.c, ax = col2(ds.R);
     amb = 0; camb_all = 0;
     gin = 0; oin = 0;
     const int g = ql;
@@ -184,6 +184,7 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
         Real sn, cs;
         sincos_(T(RF_GATE + 4 * g + 3), &sn, &cs);
         const V3<Real> lg = v3(cs * dp.x + sn * dp.y, -sn * dp.x + cs * dp.y, dp.z);
+        const V3<Real> ag = v3(cs * ax.x + sn * ax.y, -sn * ax.x + cs * ax.y, ax.z);
         const int low = C.gate_type[g] > 0;
         bool in = false;
         uint32_t gamb = 0, camb = 0;
@@ -194,10 +195,18 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
             Real r;
             int cyl;
             gate_part(k, low, off, R, h, r, cyl);
-            const Real pd = point_part_dist(mulT(R, lg - off), h, r, cyl);
-            in |= pd < cut - tol;
-            if (pd - dr < cut + tol) gamb |= 1u << k;
-            if (pd - dr < ccut + tol) camb |= 1u << k;
+            const V3<Real> lp = mulT(R, lg - off);
+            const Real pd = point_part_dist(lp, h, r, cyl);
+            Real lo = pd - dr, up = pd;
+            if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || lo < ccut + tol)) {   // support bounds
+                Real lo2, up2;
+                part_bounds_refined(lp, mulT(R, ag), h, r, cyl, ds.r, ds.h.z, lo2, up2);
+                lo = fmaxr_(lo, lo2);
+                up = up2 < up ? up2 : up;
+            }
+            in |= up < cut - tol;
+            if (lo < cut + tol) gamb |= 1u << k;
+            if (lo < ccut + tol) camb |= 1u << k;
         }
         if (in) gin |= 1u << g;
         amb |= ((in ? 0u : gamb) | camb) << (g * kGateParts);
@@ -215,9 +224,16 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
             int cyl;
             obst_part(k, off, h, r, cyl);
             const Real pd = point_part_dist(dp - off, h, r, cyl);
-            in |= pd < cut - tol;
-            if (pd - dr < cut + tol) gamb |= 1u << k;
-            if (pd - dr < ccut + tol) camb |= 1u << k;
+            Real lo = pd - dr, up = pd;
+            if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || lo < ccut + tol)) {
+                Real lo2, up2;
+                part_bounds_refined(dp - off, ax, h, r, cyl, ds.r, ds.h.z, lo2, up2);
+                lo = fmaxr_(lo, lo2);
+                up = up2 < up ? up2 : up;
+            }
+            in |= up < cut - tol;
+            if (lo < cut + tol) gamb |= 1u << k;
+            if (lo < ccut + tol) camb |= 1u << k;
         }
         if (in) oin |= 1u << o;
         amb |= ((in ? 0u : gamb) | camb) << (kObstBit0 + o * kObstParts);
@@ -552,13 +568,6 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
         if (owner)
             for (int k = 0; k < 3; ++k) { st(a.f, RF_WR_TARGET + k, EN, slot, tgt[k]); st(a.f, RF_WR_PREV + k, EN, slot, row0[k]); }
     }
-#ifdef ADRP_RACE_TIMING
-    RACE_MARK(t6);
-    if (threadIdx.x == 0) {
-        RACE_WAVE(0, t1 - t0); RACE_WAVE(1, acc_phys); RACE_WAVE(2, (t2 - t1) - acc_phys); RACE_WAVE(3, t3 - t2);
-        RACE_WAVE(4, t4 - t3); RACE_WAVE(5, t5 - t4); RACE_WAVE(6, t6 - t5); RACE_WAVE(7, t6 - t0);
-    }
-#endif
     if (owner) {
         if (dn == 0) {
             a.rew[e] = reward;
@@ -577,6 +586,13 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
         }
     }
+#ifdef ADRP_RACE_TIMING
+    RACE_MARK(t6);   // tail: reward, flags, stores and the auto-reset of done envs
+    if (threadIdx.x == 0) {
+        RACE_WAVE(0, t1 - t0); RACE_WAVE(1, acc_phys); RACE_WAVE(2, (t2 - t1) - acc_phys); RACE_WAVE(3, t3 - t2);
+        RACE_WAVE(4, t4 - t3); RACE_WAVE(5, t5 - t4); RACE_WAVE(6, t6 - t5); RACE_WAVE(7, t6 - t0);
+    }
+#endif
     // ---- coalesced copy-out of the block's rows ----
     __syncthreads();
     const int e0 = blockIdx.x * (kQuadDrones / G);

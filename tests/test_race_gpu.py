@@ -508,3 +508,38 @@ def test_reset_seed_rekeys():
         b.reset(seed=5, mask=torch.ones(E, dtype=torch.uint8))
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("variant", ["quad", "lane", "fp64"])
+@pytest.mark.parametrize("level,N,physics,mode,E", [("level0", 2, Physics.PYB, RaceMode.COMPARE, 512),
+                                                    ("level3", 4, Physics.PYB_DW, RaceMode.COMPETE, 256)])
+def test_support_bounds_bit_identical(monkeypatch, variant, level, N, physics, mode, E):
+    """the support-function bounds (part_bounds_refined) only decide pairs the centre bounds left to
+    GJK, with the same rounding guard: a closed loop driven by the reference's PPO actor (which flies
+    the drones through the gates, where the GJK work is) gives bit-identical outputs with them on and
+    off (ADRP_RACE_REFINE=0), in both fp32 layouts and the fp64 kernel"""
+    import os
+    from gym_pybullet_adrp_amd.policy import ACTOR_KEYS, DevicePolicy
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "policy_golden.npz"))
+    w = {k: g[f"example_RL_model_w{i}"] for i, k in enumerate(ACTOR_KEYS)}
+    monkeypatch.setenv("ADRP_RACE_QUAD", "0" if variant == "lane" else "1")
+    outs = []
+    for refine in ("1", "0"):
+        monkeypatch.setenv("ADRP_RACE_REFINE", refine)
+        env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=21,
+                              autoreset=True, reward="wrapper", precision="fp64" if variant == "fp64" else "fp32")
+        pol = DevicePolicy(w, "relu" if bool(g["example_RL_model_relu"]) else "tanh", 0, "relative")
+        obs, _ = env.reset()
+        act = torch.empty((E, N, 4), device=env.device)
+        seq = []
+        for _ in range(80):
+            pol.act(obs, out=act)
+            obs, rew, te, tr, _ = env.step(act)
+            seq.append(torch.cat([obs.reshape(E, -1), rew.reshape(E, 1).float(), te.reshape(E, 1).float(),
+                                  tr.reshape(E, 1).float()], 1).cpu())
+        outs.append(torch.stack(seq))
+        pol.close()
+        env.close()
+    gates = outs[0][..., [k * env.h.D + 48 for k in range(N)]]
+    assert gates.max() >= 1, "the actor passed no gate: the test would not reach the gate parts"
+    assert torch.equal(outs[0], outs[1])

@@ -45,7 +45,7 @@ for level, n, phys, mode, E in CONFIGS:
     if pol:
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)) + "/..")
         from bench import make_policy
-        policy = make_policy(pol, env.device.index or 0, mode)
+        policy = make_policy(pol, env.device)
         pact = torch.empty((E, n, 4), device=env.device)
 
         def step(_a):
@@ -63,10 +63,12 @@ for level, n, phys, mode, E in CONFIGS:
         nb = (E * G * 4 + 63) // 64
         wbuf = (ctypes.c_ulonglong * (nb * 8))()
         means, maxs = [], []
+        done = 0.0
         env.h.profile_begin(nk)
         for k in range(nk):
-            step(acts[k % 16])
+            _, _, te, tr, _ = step(acts[k % 16])
             torch.cuda.synchronize()
+            done += float((te | tr).float().mean())
             assert lib.adrp_race_wave_read(wbuf, nb) == 0
             w = np.array(list(wbuf), dtype=np.float64).reshape(nb, 8)
             means.append(w.mean(0))
@@ -74,6 +76,8 @@ for level, n, phys, mode, E in CONFIGS:
         ms = env.h.profile_end(nk)
         print(json.dumps({"config": f"{level} N={n} {phys} {mode} E={E}", "kernel": _lib.kernel_name(env.cfg),
                           "kernel_us_timing_build": float(np.mean(ms)) * 1e3,
+                          "kernel_us_median": float(np.median(ms)) * 1e3,
+                          "reset_env_fraction_per_step": done / nk,
                           "mean_cycles_per_wave": {p: round(x) for p, x in zip(PHASES, np.mean(means, 0))},
                           "max_cycles_per_launch": {p: round(x) for p, x in zip(PHASES, np.mean(maxs, 0))}}),
               flush=True)
