@@ -687,7 +687,7 @@ extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
         const int rc = rd(v, reset);
         if (rc != ADRP_OK) return rc;
         for (int k = 0; k < 32; ++k) {
-            const bool is_max = (k >= 10 && k <= 17) || k == 19;
+            const bool is_max = (k >= 10 && k <= 17) || k == 19 || k == 21;
             out[k] = is_max ? std::max(out[k], v[k]) : out[k] + v[k];
         }
     }

@@ -30,7 +30,9 @@ constexpr int kRacePreS = 32;       // sub-steps per env.step whose draws fit th
 // they are a separate opt-in of the timing build)
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
 #define GJK_STAT(n) do { atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
-        atomicMax(&g_race_phase[19], (unsigned long long)(n)); } while (0)
+        atomicMax(&g_race_phase[19], (unsigned long long)(n)); \
+        if (cut < Real(1e-3)) { atomicAdd(&g_race_phase[20], 1ull); atomicMax(&g_race_phase[21], (unsigned long long)(n)); } \
+        if ((n) >= 48) atomicAdd(&g_race_phase[22], 1ull); } while (0)
 #else
 #define GJK_STAT(n)
 #endif
@@ -867,6 +869,17 @@ __device__ __forceinline__ Real point_part_dist(V3<Real> lp, V3<Real> h, Real r,
     return hsqrt_(dx * dx + dy * dy + dz * dz);
 }
 
+// closest point of a part (own frame: box half extents h / z-axis cylinder radius r, half height h.z)
+template <typename Real>
+__device__ __forceinline__ V3<Real> part_closest(V3<Real> x, V3<Real> h, Real r, int cyl) {
+    if (cyl) {
+        const Real rho = hsqrt_(x.x * x.x + x.y * x.y);
+        const Real k = rho > r ? r * rcp_(rho) : Real(1);
+        return v3(x.x * k, x.y * k, clampr_(x.z, -h.z, h.z));
+    }
+    return v3(clampr_(x.x, -h.x, h.x), clampr_(x.y, -h.y, h.y), clampr_(x.z, -h.z, h.z));
+}
+
 // Support-function bounds of one (drone cylinder, part) pair in the part's frame: lp = the centre of
 // the drone's collision cylinder, ax = its axis (unit), dr / dhh = its radius / half height.  With q
 // the part point closest to lp and n = (q - lp) / |q - lp|, the (convex) part lies beyond the plane
@@ -878,29 +891,30 @@ __device__ __forceinline__ Real point_part_dist(V3<Real> lp, V3<Real> h, Real r,
 template <typename Real>
 __device__ __forceinline__ void part_bounds_refined(V3<Real> lp, V3<Real> ax, V3<Real> h, Real r, int cyl, Real dr,
                                                     Real dhh, Real& lo, Real& up) {
-    V3<Real> q;
-    if (cyl) {
-        const Real rho = hsqrt_(lp.x * lp.x + lp.y * lp.y);
-        const Real k = rho > r ? r * rcp_(rho) : Real(1);
-        q = v3(lp.x * k, lp.y * k, clampr_(lp.z, -h.z, h.z));
-    } else {
-        q = v3(clampr_(lp.x, -h.x, h.x), clampr_(lp.y, -h.y, h.y), clampr_(lp.z, -h.z, h.z));
+    // y: a point of the drone's cylinder (its centre first, then its support points); q = the part
+    // point closest to y.  For every such y, n = (q - y) / |q - y| gives the lower bound
+    // (q - lp).n - support(n) and the cylinder's support point in n the upper bound.  Three rounds
+    // (alternating projections) narrow the band near edges and curved parts.
+    V3<Real> y = lp;
+    lo = Real(-1);
+    up = Real(3.0e38);
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+        const V3<Real> q = part_closest(y, h, r, cyl);
+        const V3<Real> d = q - y;
+        const Real pd = hsqrt_(dot(d, d));
+        up = pd < up ? pd : up;
+        if (!(pd > Real(1e-6))) return;   // y in (or at) the part: only the upper bound is known
+        const V3<Real> n = rcp_(pd) * d;
+        const Real c = dot(n, ax);
+        const V3<Real> sp = n - c * ax;
+        const Real sn = hsqrt_(dot(sp, sp));
+        lo = fmaxr_(lo, dot(q - lp, n) - (dr * sn + dhh * fabs_(c)));
+        const Real k = sn > Real(1e-6) ? dr * rcp_(sn) : Real(0);
+        y = lp + (c >= Real(0) ? dhh : -dhh) * ax + k * sp;
     }
-    const V3<Real> d = q - lp;
-    const Real pd = hsqrt_(dot(d, d));
-    if (!(pd > Real(1e-6))) {   // the drone's centre is (almost) in the part: only up = 0 is known
-        lo = Real(-1);
-        up = Real(0);
-        return;
-    }
-    const V3<Real> n = rcp_(pd) * d;
-    const Real c = dot(n, ax);
-    const V3<Real> sp = n - c * ax;
-    const Real sn = hsqrt_(dot(sp, sp));
-    lo = pd - (dr * sn + dhh * fabs_(c));
-    const Real k = sn > Real(1e-6) ? dr * rcp_(sn) : Real(0);
-    const V3<Real> x = lp + (c >= Real(0) ? dhh : -dhh) * ax + k * sp;
-    up = point_part_dist(x, h, r, cyl);
+    const Real fd = point_part_dist(y, h, r, cyl);
+    up = fd < up ? fd : up;
 }
 
 constexpr int kGateParts = 5, kObstParts = 2, kObstBit0 = ADRP_MAX_GATES * kGateParts;
@@ -959,7 +973,7 @@ __device__ __forceinline__ Shape<Real> track_part_shape(const RaceConst<Real>& C
 template <typename Real, class TS>
 __device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds, Real cut,
                                              bool want_contact, Real ccut, uint32_t& gin, uint32_t& oin,
-                                             uint32_t& amb, uint32_t& camb_all) {
+                                             uint32_t& amb, uint32_t& camb_all, bool* ccert = nullptr) {
     const Real tol = sizeof(Real) == 4 ? Real(1e-5) : Real(1e-10);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
     const V3<Real> p = ds.c, ax = col2(ds.R);
@@ -994,7 +1008,13 @@ __device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS&
                 }
                 in |= up < cut - tol;
                 if (lo < cut + tol) gamb |= 1u << k;
-                if (want_contact && lo < ccut + tol) camb |= 1u << k;
+                // a drone point inside the part (up == 0: the clamps are the identity; the centre or
+                // a support point of part_bounds_refined) is a contact without GJK (an
+                // intersecting pair is GJK's slowest case)
+                if (want_contact && lo < ccut + tol) {
+                    if (ccert && up == Real(0)) *ccert = true;   // a drone point in the part
+                    else camb |= 1u << k;
+                }
             }
             if (in) gin |= 1u << g;
             amb |= ((in ? 0u : gamb) | camb) << (g * kGateParts);
@@ -1023,7 +1043,10 @@ __device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS&
                 }
                 in |= up < cut - tol;
                 if (lo < cut + tol) gamb |= 1u << k;
-                if (want_contact && lo < ccut + tol) camb |= 1u << k;
+                if (want_contact && lo < ccut + tol) {
+                    if (ccert && up == Real(0)) *ccert = true;   // a drone point in the part
+                    else camb |= 1u << k;
+                }
             }
             if (in) oin |= 1u << o;
             amb |= ((in ? 0u : gamb) | camb) << (kObstBit0 + o * kObstParts);
@@ -1116,13 +1139,17 @@ __device__ __forceinline__ bool track_gjk_pool(const RaceConst<Real>& C, const T
     oin |= (r >> 4) & 15u;
     return (r >> 8) & 1u;
 }
+// want_contact: false for a drone already eliminated (its contact cannot change anything,
+// _computeTerminated 684-692 ORs it into drones_eliminated)
 template <typename Real, class TS>
 __device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds,
-                                                 bool live, Real cut, Real ccut, uint32_t& gin, uint32_t& oin,
-                                                 TrackJobs& q, int tl, int G, int N, int E) {
+                                                 bool live, bool want_contact, Real cut, Real ccut, uint32_t& gin,
+                                                 uint32_t& oin, TrackJobs& q, int tl, int G, int N, int E) {
     uint32_t amb, camb_all;
-    track_bounds(C, T, ds, cut, true, ccut, gin, oin, amb, camb_all);
-    return track_gjk_pool<Real, TS, 0>(C, T, ds, live, cut, ccut, gin, oin, amb, camb_all, q, tl, G, N, E);
+    bool ccert = false;
+    track_bounds(C, T, ds, cut, want_contact, ccut, gin, oin, amb, camb_all, &ccert);
+    const bool c = track_gjk_pool<Real, TS, 0>(C, T, ds, live, cut, ccut, gin, oin, amb, camb_all, q, tl, G, N, E);
+    return c || ccert;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1642,7 +1669,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     Real row0[15];
     const Shape<Real> ds = drone_shape(C, d.pos, d.q);
     uint32_t gin, oin;
-    bool crashed = track_query_wave(C, T, ds, active, Real(0.45), Real(1e-6), gin, oin, tjobs, tl, G, N, a.E);
+    bool crashed = track_query_wave(C, T, ds, active, !(d.flags & 1), Real(0.45), Real(1e-6), gin, oin, tjobs, tl, G, N, a.E);
     V3<Real> rpy;
     race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, active, row0, gin, oin, &rpy);
     if (C.compete) {   // other drones' pos + rpy (653-659): the rpy of their own obs rows
@@ -1669,7 +1696,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         if (C.compete) {
 #pragma unroll
             for (int k = 0; k < G; ++k) {
-                if (k < N && k != dn && !crashed) {
+                if (k < N && k != dn && !crashed && !(d.flags & 1)) {
                     // bounding spheres first: GJK only for drones closer than 2 dr
                     const V3<Real> dc = gpos[k] - d.pos;
                     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);

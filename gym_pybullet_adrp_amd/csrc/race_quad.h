@@ -170,14 +170,15 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {   // OR over the quad 
 // per-part arithmetic), the bit masks are OR-ed over the quad
 template <class TS>
 __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const TS& T, const Shape<float>& ds,
-                                                float cut, float ccut, int ql, uint32_t& gin, uint32_t& oin,
-                                                uint32_t& amb, uint32_t& camb_all) {
+                                                float cut, float ccut, int ql, bool want_contact, uint32_t& gin,
+                                                uint32_t& oin, uint32_t& amb, uint32_t& camb_all, bool& ccert) {
     using Real = float;
     const Real tol = Real(1e-5);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
     const V3<Real> p = ds.c, ax = col2(ds.R);
     amb = 0; camb_all = 0;
     gin = 0; oin = 0;
+    ccert = false;
     const int g = ql;
     if (g < C.num_gates) {
         const V3<Real> dp = p - v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
@@ -198,7 +199,7 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
             const V3<Real> lp = mulT(R, lg - off);
             const Real pd = point_part_dist(lp, h, r, cyl);
             Real lo = pd - dr, up = pd;
-            if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || lo < ccut + tol)) {   // support bounds
+            if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || (want_contact && lo < ccut + tol))) {   // support bounds
                 Real lo2, up2;
                 part_bounds_refined(lp, mulT(R, ag), h, r, cyl, ds.r, ds.h.z, lo2, up2);
                 lo = fmaxr_(lo, lo2);
@@ -206,7 +207,10 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
             }
             in |= up < cut - tol;
             if (lo < cut + tol) gamb |= 1u << k;
-            if (lo < ccut + tol) camb |= 1u << k;
+            if (want_contact && lo < ccut + tol) {   // centre inside the part: contact (race_kernel.h)
+                if (up == Real(0)) ccert = true;
+                else camb |= 1u << k;
+            }
         }
         if (in) gin |= 1u << g;
         amb |= ((in ? 0u : gamb) | camb) << (g * kGateParts);
@@ -225,7 +229,7 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
             obst_part(k, off, h, r, cyl);
             const Real pd = point_part_dist(dp - off, h, r, cyl);
             Real lo = pd - dr, up = pd;
-            if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || lo < ccut + tol)) {
+            if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || (want_contact && lo < ccut + tol))) {
                 Real lo2, up2;
                 part_bounds_refined(dp - off, ax, h, r, cyl, ds.r, ds.h.z, lo2, up2);
                 lo = fmaxr_(lo, lo2);
@@ -233,13 +237,17 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
             }
             in |= up < cut - tol;
             if (lo < cut + tol) gamb |= 1u << k;
-            if (lo < ccut + tol) camb |= 1u << k;
+            if (want_contact && lo < ccut + tol) {   // centre inside the part: contact (race_kernel.h)
+                if (up == Real(0)) ccert = true;
+                else camb |= 1u << k;
+            }
         }
         if (in) oin |= 1u << o;
         amb |= ((in ? 0u : gamb) | camb) << (kObstBit0 + o * kObstParts);
         camb_all |= camb << (kObstBit0 + o * kObstParts);
     }
     gin = quad_or(gin); oin = quad_or(oin); amb = quad_or(amb); camb_all = quad_or(camb_all);
+    ccert = quad_or(ccert ? 1u : 0u) != 0;
 }
 
 template <typename T3>
@@ -483,9 +491,10 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
     const Shape<Real> ds = drone_shape(C, d.pos, d.q);
     uint32_t gin, oin;
     uint32_t amb, camb_all;
-    track_bounds_q4(C, T, ds, Real(0.45), Real(1e-6), ql, gin, oin, amb, camb_all);
+    bool ccert;
+    track_bounds_q4(C, T, ds, Real(0.45), Real(1e-6), ql, !(d.flags & 1), gin, oin, amb, camb_all, ccert);
     bool crashed = track_gjk_pool<Real, TrackSrcQ, 2>(C, T, ds, owner, Real(0.45), Real(1e-6), gin, oin, amb, camb_all,
-                                                     tjobs, tl, G, N, a.E);
+                                                     tjobs, tl, G, N, a.E) || ccert;
     V3<Real> rpy;
     race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, owner, row0, gin, oin, &rpy);
     if (C.compete) {   // other drones' pos + rpy (653-659): the rpy of their own obs rows
@@ -512,7 +521,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
         if (C.compete) {
 #pragma unroll
             for (int k = 0; k < G; ++k) {
-                if (k < N && k != dn && !crashed) {
+                if (k < N && k != dn && !crashed && !(d.flags & 1)) {   // eliminated: contacts change nothing
                     const V3<Real> dc = gpos[k] - d.pos;
                     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
                     if (dot(dc, dc) < (Real(2) * dr + Real(1e-4)) * (Real(2) * dr + Real(1e-4))) {

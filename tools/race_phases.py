@@ -45,7 +45,7 @@ for level, n, phys, mode, E in CONFIGS:
     if pol:
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)) + "/..")
         from bench import make_policy
-        policy = make_policy(pol, env.device)
+        policy = make_policy(pol, env.device.index or 0)
         pact = torch.empty((E, n, 4), device=env.device)
 
         def step(_a):
@@ -74,7 +74,12 @@ for level, n, phys, mode, E in CONFIGS:
             means.append(w.mean(0))
             maxs.append(w.max(0))
         ms = env.h.profile_end(nk)
+        lib.adrp_race_phase_read(buf, 1)   # GJK counters (timing build with -DADRP_RACE_GJK_STATS)
+        gv = np.array(list(buf), dtype=np.float64)
         print(json.dumps({"config": f"{level} N={n} {phys} {mode} E={E}", "kernel": _lib.kernel_name(env.cfg),
+                          "gjk": {"calls_per_launch": gv[9] / nk, "mean_iters": gv[18] / max(gv[9], 1),
+                                  "max_iters": gv[19], "contact_calls_per_launch": gv[20] / nk,
+                                  "contact_max_iters": gv[21], "capped_calls": gv[22]},
                           "kernel_us_timing_build": float(np.mean(ms)) * 1e3,
                           "kernel_us_median": float(np.median(ms)) * 1e3,
                           "reset_env_fraction_per_step": done / nk,
