@@ -253,6 +253,192 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
 template <typename T3>
 __device__ __forceinline__ float sel3(const T3& v, int a) { return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]); }
 
+// ---- auto-reset of a done drone by its quad ----
+// race_reset_lane's arithmetic (MultiRaceAviary.reset 127-167, _addObstacles 347-403, _drone_init
+// 407-467) with the work dealt over the quad: lane ql draws gate ql, obstacle ql and drone draw ql;
+// the track reaches every lane by DPP broadcasts and stays in registers (the one-lane reset reads it
+// back from HBM after storing it); lane ql tests gate ql / obstacle ql at the nominal pose.  A wave
+// that resets an env waits for it after its sub-steps, and the kernel for its slowest wave.
+
+// this lane's own gate ql / obstacle ql, addressed like the track fields (the bounds pass and the
+// part shapes of lane ql only ask for gate ql and obstacle ql)
+struct TrackOne {
+    float g[4], o[3];
+    int ql;
+    __device__ __forceinline__ float operator()(int field) const {
+        if (field < RF_OBST) {
+            const int c = field - RF_GATE - 4 * ql;
+            return c == 0 ? g[0] : c == 1 ? g[1] : c == 2 ? g[2] : g[3];
+        }
+        const int c = field - RF_OBST - 3 * ql;
+        return c == 0 ? o[0] : c == 1 ? o[1] : o[2];
+    }
+};
+// the whole track in registers (field indices fold to constants in the unrolled obs-row loops)
+struct TrackRegs {
+    float v[kTrackFields];
+    __device__ __forceinline__ float operator()(int field) const { return v[field - RF_GATE]; }
+};
+
+template <int G>
+__device__ __forceinline__ void race_reset_q4(const RaceArgs<float>& a, const RaceConst<float>& C, int e, int dn, int ql,
+                                              bool active, size_t EN, size_t slot, int episode, float* obs_row) {
+    using Real = float;
+    const bool owner = active && ql == 0;
+    const uint64_t gid = uint64_t(a.env_offset + e);
+    const uint32_t ep = uint32_t(episode);
+    Real* f = a.f;
+    TrackOne own;
+    own.ql = ql;
+    {   // gate ql, obstacle ql of the next track
+        const int g = ql;
+        Real gx = C.gate_nom[g][0], gy = C.gate_nom[g][1], gyaw = C.gate_nom[g][3];
+        if (C.random_gates && g < C.num_gates) {
+            const U4 u = draw(a.seed, gid, ep, TAG_RACE_TRACK, uint32_t(g));
+            const Real lo = C.gate_off[0], hi = C.gate_off[1];
+            gx += lo + (hi - lo) * Real(u01(u.a));
+            gy += lo + (hi - lo) * Real(u01(u.b));
+            gyaw += lo + (hi - lo) * Real(u01(u.c));
+        }
+        own.g[0] = gx; own.g[1] = gy; own.g[2] = C.gate_nom[g][2]; own.g[3] = gyaw;
+        const int o = ql;
+        Real ox = C.obst_nom[o][0], oy = C.obst_nom[o][1];
+        if (C.random_gates && o < C.num_obstacles) {
+            const U4 u = draw(a.seed, gid, ep, TAG_RACE_TRACK, uint32_t(4 + o));
+            const Real lo = C.obst_off[0], hi = C.obst_off[1];
+            ox += lo + (hi - lo) * Real(u01(u.a));
+            oy += lo + (hi - lo) * Real(u01(u.b));
+        }
+        own.o[0] = ox; own.o[1] = oy; own.o[2] = C.obst_nom[o][2];
+        if (active) {   // the quad stores the drone slot's replicated track, a gate and an obstacle per lane
+#pragma unroll
+            for (int k = 0; k < 4; ++k) st(f, RF_GATE + 4 * g + k, EN, slot, own.g[k]);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) st(f, RF_OBST + 3 * o + k, EN, slot, own.o[k]);
+        }
+    }
+    TrackRegs T;
+#pragma unroll
+    for (int g = 0; g < ADRP_MAX_GATES; ++g)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) T.v[4 * g + k] = qbc(own.g[k], g);
+#pragma unroll
+    for (int o = 0; o < ADRP_MAX_OBSTACLES; ++o)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) T.v[RF_OBST - RF_GATE + 3 * o + k] = qbc(own.o[k], o);
+    // initial obs at the nominal (loadURDF) pose, at rest; lane ql tests gate ql / obstacle ql
+    const Real d2r = Real(0.017453292519943295);
+    const V3<Real> npos = v3(C.init_pos[dn][0], C.init_pos[dn][1], C.init_pos[dn][2]);
+    const Q4<Real> nq = quat_from_euler_fast(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
+    const Shape<Real> ds = drone_shape(C, npos, nq);
+    uint32_t gin, oin, amb, camb_all;
+    bool ccert;
+    track_bounds_q4(C, own, ds, Real(0.45), Real(0), ql, false, gin, oin, amb, camb_all, ccert);
+    uint32_t mine = amb & ((0x1fu << (kGateParts * ql)) | (0x3u << (kObstBit0 + kObstParts * ql)));
+    uint32_t g2 = 0, o2 = 0;
+    while (mine) {   // this lane's undecided parts (track_query)
+        const int b = __builtin_ctz(mine);
+        mine &= mine - 1;
+        if (gjk_within(ds, track_part_shape(C, own, b), Real(0.45))) {
+            if (b < kObstBit0) g2 |= 1u << (b / kGateParts);
+            else o2 |= 1u << ((b - kObstBit0) / kObstParts);
+        }
+    }
+    gin |= quad_or(g2);
+    oin |= quad_or(o2);
+    Real row0[15];
+    const V3<Real> zero = v3(Real(0), Real(0), Real(0));
+    race_obs_row(C, T, npos, nq, zero, zero, 0, obs_row, owner, row0, gin, oin);
+    // the nominal Euler angles of drone k (lane k % 4 computes drones ql, ql + 4)
+    V3<Real> nrpy_j[(G + 3) / 4];
+#pragma unroll
+    for (int j = 0; j < (G + 3) / 4; ++j) {
+        const int k = ql + 4 * j < C.N ? ql + 4 * j : 0;
+        nrpy_j[j] = euler_xyz_fast(quat_from_euler_fast(C.init_rpy[k][0] * d2r, C.init_rpy[k][1] * d2r, C.init_rpy[k][2] * d2r));
+    }
+    V3<Real> nrpy_k[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+        nrpy_k[k] = v3(qbc(nrpy_j[k / 4].x, k % 4), qbc(nrpy_j[k / 4].y, k % 4), qbc(nrpy_j[k / 4].z, k % 4));
+    V3<Real> nrpy = nrpy_k[0];
+#pragma unroll
+    for (int k = 1; k < G; ++k) nrpy = dn == k ? nrpy_k[k] : nrpy;
+    if (C.compete && owner) {   // other drones' nominal pos + rpy
+        int idx = 0;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            if (k < C.N && k != dn) {
+                float* p = obs_row + 49 + 6 * idx;
+                p[0] = C.init_pos[k][0]; p[1] = C.init_pos[k][1]; p[2] = C.init_pos[k][2];
+                p[3] = nrpy_k[k].x; p[4] = nrpy_k[k].y; p[5] = nrpy_k[k].z;
+                ++idx;
+            }
+        }
+    }
+    // _drone_init draws: lane 0 position offsets, lane 1 rotation offsets, lane 2 mass / inertia
+    // (the uniforms travel; the ranges are applied as race_reset_lane does)
+    const uint32_t dtag = TAG_RACE_DRONE | uint32_t(dn);
+    Real u[4] = {Real(0), Real(0), Real(0), Real(0)};
+    if (ql < 2 ? C.random_state != 0 : (ql == 2 && C.random_inertia != 0)) {
+        const U4 w = draw(a.seed, gid, ep, dtag, uint32_t(ql));
+        u[0] = Real(u01(w.a)); u[1] = Real(u01(w.b)); u[2] = Real(u01(w.c)); u[3] = Real(u01(w.d));
+    }
+    Real uq[3][4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) uq[j][k] = qbc(u[k], j);
+    if (!owner) return;
+    for (int k = 0; k < 3; ++k) {   // RewardWrapper.reset: current_target = obs[0, 12:15], previous_pos = obs[0, :3]
+        st(f, RF_WR_TARGET + k, EN, slot, dn == 0 && C.num_gates > 0 ? row0[3 + k] : Real(0));
+        st(f, RF_WR_PREV + k, EN, slot, dn == 0 ? row0[k] : Real(0));
+    }
+    RDrone<Real> d;
+    d.prev_rpy[0] = nrpy.x; d.prev_rpy[1] = nrpy.y; d.prev_rpy[2] = nrpy.z;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        d.prev_vel[k] = Real(0); d.lpf1[k] = d.lpf2[k] = 0.0f; d.ierr[k] = d.ierrm[k] = 0.0f;
+    }
+    d.tick = d.last_att = d.last_pos = d.tumble = 0;
+    d.pw_roll = d.pw_pitch = __builtin_nanf("");
+    d.psp_roll = d.psp_pitch = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d.ctl[k] = 0.0f; d.rpm[k] = d.prev[k] = Real(0); }
+    d.gate = 0; d.flags = 0;
+    d.mass = C.race_mass;
+    d.inertia[0] = C.race_inertia[0]; d.inertia[1] = C.race_inertia[1]; d.inertia[2] = C.race_inertia[2];
+    if (C.random_inertia) {
+        Real v[4] = {d.mass, d.inertia[0], d.inertia[1], d.inertia[2]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const Real lo = C.inertia_off[k][0], hi = C.inertia_off[k][1];
+            v[k] = clampr_(v[k] + lo + (hi - lo) * uq[2][k], Real(0), Real(100));
+        }
+        d.mass = v[0]; d.inertia[0] = v[1]; d.inertia[1] = v[2]; d.inertia[2] = v[3];
+    }
+    Real po[3] = {0, 0, 0}, ro[3] = {0, 0, 0};
+    if (C.random_state) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            po[k] = C.pos_off[k][0] + (C.pos_off[k][1] - C.pos_off[k][0]) * uq[0][k];
+            ro[k] = C.rot_off[k][0] + (C.rot_off[k][1] - C.rot_off[k][0]) * uq[1][k];
+        }
+    }
+    d.pos = v3(npos.x + po[0], npos.y + po[1], npos.z + po[2]);
+    d.q = quat_from_euler_fast(C.init_rpy[dn][0] + ro[0], C.init_rpy[dn][1] + ro[1], C.init_rpy[dn][2] + ro[2]);
+    d.vel = v3(C.init_vel[dn][0], C.init_vel[dn][1], C.init_vel[dn][2]);
+    d.w = v3(C.init_pqr[dn][0], C.init_pqr[dn][1], C.init_pqr[dn][2]);
+    d.angv = d.w;
+    if (C.physics == ADRP_PHYS_DYN) d.w = v3(Real(0), Real(0), Real(0));   // rpy_rates zeroed by _housekeeping
+    d.ql = d.q;
+    d.lpos = d.pos;
+    d.kpos = C.physics == ADRP_PHYS_PYB ? npos : d.pos;   // self.pos: nominal until the first read
+    store_drone(a, EN, slot, d, true);
+    a.ist[RI_STEP * EN + slot] = 0;
+    a.ist[RI_EPISODE * EN + slot] = episode + 1;
+    a.ist[RI_WR_GATE * EN + slot] = 0;
+}
+
 // Block = 64 lanes = 16 drones (kQuadDrones); one wave.  DRAWS: the disturbance draws of the
 // step's S <= kRacePreS sub-steps go through LDS (disturbances on); else none are needed, or (S
 // larger) each lane draws in the loop.
@@ -577,24 +763,24 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
         if (owner)
             for (int k = 0; k < 3; ++k) { st(a.f, RF_WR_TARGET + k, EN, slot, tgt[k]); st(a.f, RF_WR_PREV + k, EN, slot, row0[k]); }
     }
+    const bool reset = C.autoreset && (te || tr);   // env-uniform: every lane of the env's quads agrees
     if (owner) {
         if (dn == 0) {
             a.rew[e] = reward;
             a.term[e] = te;
             a.trunc[e] = tr;
         }
-        if (C.autoreset && (te || tr)) {
-            if (a.tobs) {
-                float* trow = a.tobs + slot * size_t(C.D);
-                for (int k = 0; k < C.D; ++k) trow[k] = row[k];
-            }
-            race_reset_lane(a, C, e, dn, EN, slot, episode, row);
-        } else {
+        if (reset && a.tobs) {
+            float* trow = a.tobs + slot * size_t(C.D);
+            for (int k = 0; k < C.D; ++k) trow[k] = row[k];
+        }
+        if (!reset) {
             store_drone(a, EN, slot, d, false);
             a.ist[RI_STEP * EN + slot] = sc0 + C.S;
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
         }
     }
+    if (reset) race_reset_q4<G>(a, C, e, dn, ql, active, EN, slot, episode, row);
 #ifdef ADRP_RACE_TIMING
     RACE_MARK(t6);   // tail: reward, flags, stores and the auto-reset of done envs
     if (threadIdx.x == 0) {
