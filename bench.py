@@ -285,9 +285,10 @@ def hbm_roofline(bytes_per_launch, kern_ms, traffic_key):
 
 
 def valu_roofline(env, kern_ms, key, precision):
-    """race kernel: PMC-counted flops per launch (profiles/pmc_valu.json, tools/pmc_summary.py valu mode:
-    64 x (ADD + MUL + TRANS + 2 FMA) VALU instruction counts) over the kernel time, vs the vector peak.
-    HBM fraction kept alongside for information."""
+    """race kernel: flops per launch over the kernel time, vs the vector peak.  Flop model: the PMC
+    FLOPS counters of the one-lane kernel per drone-step (profiles/pmc_valu.json
+    algorithmic_flops_per_drone_step; tools/pmc_summary.py valu mode); the four-lane kernel's own
+    counters (executed, redundant lanes included) and VALU busy beside it.  HBM fraction for information."""
     avg_s = float(np.mean(kern_ms)) / 1e3
     hbm = hbm_roofline(env.step_bytes(), kern_ms, key)
     pmc = pmc_record("pmc_valu.json", key)
@@ -298,9 +299,15 @@ def valu_roofline(env, kern_ms, key, precision):
            "timed_launches": hbm["timed_launches"],
            "hbm": {"achieved_GBps": hbm["achieved"], "frac": hbm["frac"], "bytes_per_launch": hbm["bytes_per_launch"]}}
     if pmc is not None:
-        flops = pmc["flops_per_launch"]
+        # achieved = ALGORITHMIC flops (per drone-step, counted on the one-lane kernel) x drones per
+        # launch / kernel time; the four-lane kernel's executed flops (redundant quad lanes included)
+        # are reported beside it
+        exe = pmc["flops_per_launch"]
+        per_drone = pmc.get("algorithmic_flops_per_drone_step", exe / drones)
+        flops = per_drone * drones
         rec.update({"achieved": flops / avg_s / 1e12, "frac": flops / avg_s / 1e12 / peak,
-                    "flops_per_launch": flops, "flops_per_drone_step": flops / drones,
+                    "flops_per_launch": flops, "flops_per_drone_step": per_drone,
+                    "executed_flops_per_launch": exe, "executed_frac": exe / avg_s / 1e12 / peak,
                     "valu_busy": pmc.get("valu_busy"), "source": f"profiles/pmc_valu.json[{key}]"})
     return rec
 

@@ -14,7 +14,7 @@ VALU instruction was executing.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is
-taken as is.  Keys starting with ``race_`` select race_step_kernel, the others
+taken as is.  Keys starting with ``race_`` select the race step kernels (race_step_q4 / race_step_kernel), the others
 hover_step_kernel.  The first 8 dispatches (cold caches, first-touch) are skipped; the median of
 the rest is reported.
 """
@@ -48,7 +48,7 @@ def valu(out_path, rest):
         rec = {}
     for i in range(0, len(rest), 3):
         key, fdir, bdir = rest[i:i + 3]
-        kernel = "race_step_kernel" if key.startswith("race_") else "hover_step_kernel"
+        kernel = "race_step" if key.startswith("race_") else "hover_step_kernel"   # race_step_q4 / race_step_kernel
         c = {n: counter(fdir, n, kernel)[0] for n in ("SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS",
                                                       "SQ_INSTS_VALU_FLOPS_FP64", "SQ_INSTS_VALU")}
         c.update({n: counter(bdir, n, kernel)[0] for n in (
@@ -78,7 +78,7 @@ def main():
         rec = {}
     for i in range(0, len(rest), 3):
         key, fdir, wdir = rest[i:i + 3]
-        kernel = "race_step_kernel" if key.startswith("race_") else "hover_step_kernel"
+        kernel = "race_step" if key.startswith("race_") else "hover_step_kernel"   # race_step_q4 / race_step_kernel
         fetch_kib, nf = counter(fdir, "FETCH_SIZE", kernel)
         write_kib, nw = counter(wdir, "WRITE_SIZE", kernel)
         rd = fetch_kib * 1024 * 2
