@@ -333,7 +333,11 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<float>& a, const Ra
     const Shape<Real> ds = drone_shape(C, npos, nq);
     uint32_t gin, oin, amb, camb_all;
     bool ccert;
+#ifdef ADRP_EXP_RESET_NOQ
+    gin = oin = amb = camb_all = 0; ccert = false;
+#else
     track_bounds_q4(C, own, ds, Real(0.45), Real(0), ql, false, gin, oin, amb, camb_all, ccert);
+#endif
     uint32_t mine = amb & ((0x1fu << (kGateParts * ql)) | (0x3u << (kObstBit0 + kObstParts * ql)));
     uint32_t g2 = 0, o2 = 0;
     while (mine) {   // this lane's undecided parts (track_query)
@@ -348,7 +352,11 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<float>& a, const Ra
     oin |= quad_or(o2);
     Real row0[15];
     const V3<Real> zero = v3(Real(0), Real(0), Real(0));
+#ifdef ADRP_EXP_RESET_NOROW
+    for (int k = 0; k < 15; ++k) row0[k] = T.v[k];
+#else
     race_obs_row(C, T, npos, nq, zero, zero, 0, obs_row, owner, row0, gin, oin);
+#endif
     // the nominal Euler angles of drone k (lane k % 4 computes drones ql, ql + 4)
     V3<Real> nrpy_j[(G + 3) / 4];
 #pragma unroll
