@@ -79,6 +79,8 @@ def load():
     lib.adrp_policy_act.restype = I
     lib.adrp_policy_destroy.argtypes = [P]
     lib.adrp_policy_destroy.restype = None
+    lib.adrp_math_probe.argtypes = [I, P, P, I, P]
+    lib.adrp_math_probe.restype = I
     if lib.adrp_abi_version() != abi.ABI_VERSION:
         raise AdrpError(f"libadrp ABI {lib.adrp_abi_version()} != python mirror {abi.ABI_VERSION}")
     _lib = lib

@@ -81,40 +81,157 @@ __device__ __forceinline__ V3<Real> cross(V3<Real> a, V3<Real> b) {
     return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
 
+// ---- fp64 fast transcendentals -------------------------------------------------------------
+// The fp64 kernels compute at the reference's precision (float64), but CDNA has no correctly
+// rounded fp64 division / sqrt / sin instruction: IEEE 1/x is a ~10-instruction scale / fixup
+// sequence, libm sqrt / sincos / atan2 / exp add range checks and branches, and the fp64 step is
+// one wave's dependent chain at E = 4096.  These are the hardware approximations (v_rcp_f64,
+// v_rsq_f64) refined by Newton-Raphson to <= 2 ulp, and polynomials on the reduced ranges the
+// kernels use (coefficients and their error: tools/fit_f64_poly.py; device check against
+// longdouble references: tests/test_math_gpu.py through adrp_math_probe).
+namespace f64 {
+__device__ __forceinline__ double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
+// 1/x: v_rcp_f64 + 2 Newton steps (quadratic convergence); 0 / inf / NaN keep the hardware result
+__device__ __forceinline__ double rcp(double x) {
+    const double y0 = __builtin_amdgcn_rcp(x);
+    double e = fma_(-x, y0, 1.0);
+    double y = fma_(y0, e, y0);
+    e = fma_(-x, y, 1.0);
+    y = fma_(y, e, y);
+    return __builtin_isfinite(y) ? y : y0;
+}
+// 1/sqrt(x): v_rsq_f64 + 2 Newton steps
+__device__ __forceinline__ double rsq(double x) {
+    const double y0 = __builtin_amdgcn_rsq(x);
+    double y = y0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double e = fma_(-x * y, y, 1.0);
+        y = fma_(0.5 * y, e, y);
+    }
+    return __builtin_isfinite(y) ? y : y0;
+}
+// sqrt(x), x >= 0: Goldschmidt on v_rsq_f64 (g -> sqrt x, h -> 1/(2 sqrt x)) + a final residual step
+__device__ __forceinline__ double sqrt(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double r = fma_(-g, h, 0.5);
+        g = fma_(g, r, g);
+        h = fma_(h, r, h);
+    }
+    const double d = fma_(-g, g, x);
+    g = fma_(d, h, g);
+    return x > 0.0 ? g : (x == 0.0 ? x : __builtin_nan(""));
+}
+// sin / cos for |x| <= pi/8: Taylor to x^13 / x^14 (relative error <= 1.7e-16 before rounding)
+__device__ __forceinline__ void sincos_small(double x, double* s, double* c) {
+    const double x2 = x * x;
+    double ps = 1.6059043836821613e-10;
+    ps = fma_(ps, x2, -2.505210838544172e-08);
+    ps = fma_(ps, x2, 2.7557319223985893e-06);
+    ps = fma_(ps, x2, -0.0001984126984126984);
+    ps = fma_(ps, x2, 0.008333333333333333);
+    ps = fma_(ps, x2, -0.16666666666666666);
+    double pc = -1.1470745597729725e-11;
+    pc = fma_(pc, x2, 2.08767569878681e-09);
+    pc = fma_(pc, x2, -2.755731922398589e-07);
+    pc = fma_(pc, x2, 2.48015873015873e-05);
+    pc = fma_(pc, x2, -0.001388888888888889);
+    pc = fma_(pc, x2, 0.041666666666666664);
+    pc = fma_(pc, x2, -0.5);
+    *s = fma_(x * x2, ps, x);
+    *c = fma_(x2, pc, 1.0);
+}
+// atan2(y, x): octant reduction to a = min/max in [0, 1], then t = a or (a - 1)/(a + 1) (one
+// division either way: (min - max)/(min + max)) so |t| <= tan(pi/8), atan t = t + t^3 P(t^2)
+// with a degree-9 near-minimax P (1.7e-16 relative).  atan2(0, 0) = 0 (as the fp32 fatan2_).
+__device__ __forceinline__ double atan2(double y, double x) {
+    const double ax = __builtin_fabs(x), ay = __builtin_fabs(y);
+    const double mx = __builtin_fmax(ax, ay), mn = __builtin_fmin(ax, ay);
+    const bool big = mn > 0.41421356237309504880 * mx;
+    const double num = big ? mn - mx : mn, den = big ? mn + mx : mx;
+    const double t = mx > 0.0 ? num * rcp(den) : 0.0;
+    const double s = t * t;
+    double p = 0.021428368220326288;
+    p = fma_(p, s, -0.04375458729368037);
+    p = fma_(p, s, 0.05699267039194693);
+    p = fma_(p, s, -0.06642647883966969);
+    p = fma_(p, s, 0.07690277001250925);
+    p = fma_(p, s, -0.09090800003785938);
+    p = fma_(p, s, 0.11111107550967636);
+    p = fma_(p, s, -0.14285714221246087);
+    p = fma_(p, s, 0.19999999999459742);
+    p = fma_(p, s, -0.3333333333333199);
+    double r = fma_(t * s, p, t);
+    if (big) r += 0.78539816339744830962;
+    if (ay > ax) r = 1.57079632679489661923 - r;
+    if (x < 0.0) r = 3.14159265358979323846 - r;
+    return __builtin_copysign(r, y);
+}
+// asin(s), |s| < 1: atan2(s, sqrt((1 - s)(1 + s)))
+__device__ __forceinline__ double asin(double s) { return atan2(s, sqrt((1.0 - s) * (1.0 + s))); }
+// exp(x): k = rint(x log2 e), r = x - k ln2 (two-part ln2), Taylor to r^13 on |r| <= ln2/2, 2^k by
+// v_ldexp_f64 (underflows to 0 below -745; the kernels call it with x <= 0)
+__device__ __forceinline__ double exp(double x) {
+    x = __builtin_fmax(x, -1000.0);
+    const double k = __builtin_rint(x * 1.4426950408889634);
+    const double r = fma_(-k, 1.9082149292705877e-10, fma_(-k, 0.6931471803691238, x));
+    double p = 1.6059043836821613e-10;
+    p = fma_(p, r, 2.08767569878681e-09);
+    p = fma_(p, r, 2.505210838544172e-08);
+    p = fma_(p, r, 2.755731922398589e-07);
+    p = fma_(p, r, 2.7557319223985893e-06);
+    p = fma_(p, r, 2.48015873015873e-05);
+    p = fma_(p, r, 0.0001984126984126984);
+    p = fma_(p, r, 0.001388888888888889);
+    p = fma_(p, r, 0.008333333333333333);
+    p = fma_(p, r, 0.041666666666666664);
+    p = fma_(p, r, 0.16666666666666666);
+    p = fma_(p, r, 0.5);
+    p = fma_(p, r, 1.0);
+    p = fma_(p, r, 1.0);
+    return __builtin_amdgcn_ldexp(p, int(k));
+}
+}  // namespace f64
+
 __device__ __forceinline__ float rsqrt_(float x) { return __frsqrt_rn(x); }
-__device__ __forceinline__ double rsqrt_(double x) { return 1.0 / sqrt(x); }
+__device__ __forceinline__ double rsqrt_(double x) { return 1.0 / ::sqrt(x); }
 __device__ __forceinline__ float sqrt_(float x) { return __fsqrt_rn(x); }
-__device__ __forceinline__ double sqrt_(double x) { return sqrt(x); }
+__device__ __forceinline__ double sqrt_(double x) { return ::sqrt(x); }
 __device__ __forceinline__ void sincos_(float x, float* s, float* c) { sincosf(x, s, c); }
-__device__ __forceinline__ void sincos_(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ void sincos_(double x, double* s, double* c) { ::sincos(x, s, c); }
 __device__ __forceinline__ float atan2_(float y, float x) { return atan2f(y, x); }
-__device__ __forceinline__ double atan2_(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ double atan2_(double y, double x) { return ::atan2(y, x); }
 __device__ __forceinline__ float asin_(float x) { return asinf(x); }
-__device__ __forceinline__ double asin_(double x) { return asin(x); }
+__device__ __forceinline__ double asin_(double x) { return ::asin(x); }
 __device__ __forceinline__ float exp_(float x) { return expf(x); }
-__device__ __forceinline__ double exp_(double x) { return exp(x); }
+__device__ __forceinline__ double exp_(double x) { return ::exp(x); }
 __device__ __forceinline__ float fabs_(float x) { return fabsf(x); }
 __device__ __forceinline__ double fabs_(double x) { return fabs(x); }
 
-// latency-oriented fp32 primitives (1-ulp hardware ops); fp64 keeps IEEE-exact ones
+// latency-oriented primitives of the step loops: 1-ulp hardware ops in fp32, the refined
+// hardware approximations above in fp64 (sqrt_ / rsqrt_ / atan2_ / asin_ / exp_ / sincos_ keep
+// the correctly rounded / libm forms for code outside the loops)
 __device__ __forceinline__ float rcp_(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ double rcp_(double x) { return 1.0 / x; }
+__device__ __forceinline__ double rcp_(double x) { return f64::rcp(x); }
 __device__ __forceinline__ float hsqrt_(float x) { return __builtin_amdgcn_sqrtf(x); }
-__device__ __forceinline__ double hsqrt_(double x) { return sqrt(x); }
+__device__ __forceinline__ double hsqrt_(double x) { return f64::sqrt(x); }
 __device__ __forceinline__ float hrsqrt_(float x) { return __builtin_amdgcn_rsqf(x); }
-__device__ __forceinline__ double hrsqrt_(double x) { return 1.0 / sqrt(x); }
+__device__ __forceinline__ double hrsqrt_(double x) { return f64::rsq(x); }
 
 // sin/cos for |x| <= pi/8 (the exp-map half angle is clamped there): Taylor to x^7 / x^8,
-// truncation error < 2e-9 relative, i.e. exact in fp32; fp64 uses the libm call.
+// truncation error < 2e-9 relative, i.e. exact in fp32; fp64 to x^13 / x^14 (f64::sincos_small).
 __device__ __forceinline__ void small_sincos(float x, float* s, float* c) {
     const float x2 = x * x;
     *s = x * (1.0f + x2 * (-1.0f / 6.0f + x2 * (1.0f / 120.0f + x2 * (-1.0f / 5040.0f))));
     *c = 1.0f + x2 * (-0.5f + x2 * (1.0f / 24.0f + x2 * (-1.0f / 720.0f + x2 * (1.0f / 40320.0f))));
 }
-__device__ __forceinline__ void small_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ void small_sincos(double x, double* s, double* c) { f64::sincos_small(x, s, c); }
 
-// fast fp32 transcendentals for the latency-bound sub-step loop (the fp64 overloads keep
-// libm). atan on [0,1] is an odd minimax polynomial (|err| <= 1.1e-7 rad, fitted by IRLS on
+// fast fp32 transcendentals for the latency-bound sub-step loop (fp64: the f64 forms above).
+// atan on [0,1] is an odd minimax polynomial (|err| <= 1.1e-7 rad, fitted by IRLS on
 // Chebyshev nodes, checked in fp32 Horner), after octant reduction with a hardware reciprocal.
 __device__ __forceinline__ float fatan2_(float y, float x) {
     const float ax = fabsf(x), ay = fabsf(y);
@@ -135,11 +252,11 @@ __device__ __forceinline__ float fatan2_(float y, float x) {
     if (x < 0.0f) r = 3.14159265358979323846f - r;
     return copysignf(r, y);
 }
-__device__ __forceinline__ double fatan2_(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ double fatan2_(double y, double x) { return f64::atan2(y, x); }
 __device__ __forceinline__ float fasin_(float s) { return fatan2_(s, __builtin_amdgcn_sqrtf((1.0f - s) * (1.0f + s))); }
-__device__ __forceinline__ double fasin_(double s) { return asin(s); }
+__device__ __forceinline__ double fasin_(double s) { return f64::asin(s); }
 __device__ __forceinline__ float fexp_(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
-__device__ __forceinline__ double fexp_(double x) { return exp(x); }
+__device__ __forceinline__ double fexp_(double x) { return f64::exp(x); }
 
 // rotation matrix of a unit quaternion (body->world)
 template <typename Real>

@@ -1,0 +1,36 @@
+// math_probe.hip — adrp_math_probe: evaluates the fp64 fast transcendentals of adrp_device.h
+// (namespace f64) over a device array, so tests/test_math_gpu.py can check them against
+// extended-precision references (the step kernels inline the same functions).
+#include <hip/hip_runtime.h>
+
+#include "adrp_device.h"
+#include "../../include/adrp.h"
+
+namespace {
+__global__ void __launch_bounds__(256) math_probe_kernel(int fn, const double* __restrict__ in, double* __restrict__ out,
+                                                         int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = in[i];
+    double r = 0.0, c = 0.0;
+    switch (fn) {
+        case ADRP_MATH_RCP: r = adrp::f64::rcp(x); break;
+        case ADRP_MATH_RSQ: r = adrp::f64::rsq(x); break;
+        case ADRP_MATH_SQRT: r = adrp::f64::sqrt(x); break;
+        case ADRP_MATH_SIN_SMALL: adrp::f64::sincos_small(x, &r, &c); break;
+        case ADRP_MATH_COS_SMALL: adrp::f64::sincos_small(x, &c, &r); break;
+        case ADRP_MATH_ATAN2: r = adrp::f64::atan2(x, in[n + i]); break;
+        case ADRP_MATH_ASIN: r = adrp::f64::asin(x); break;
+        case ADRP_MATH_EXP: r = adrp::f64::exp(x); break;
+        default: r = __builtin_nan(""); break;
+    }
+    out[i] = r;
+}
+}  // namespace
+
+extern "C" int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream) {
+    if (fn < ADRP_MATH_RCP || fn > ADRP_MATH_EXP || n < 0 || (n > 0 && (!in_dev || !out_dev))) return ADRP_ERR_INVALID;
+    if (n == 0) return ADRP_OK;
+    hipLaunchKernelGGL(math_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, in_dev, out_dev, n);
+    return hipGetLastError() == hipSuccess ? ADRP_OK : ADRP_ERR_DEVICE;
+}

@@ -169,6 +169,16 @@ class MultiRaceAviary:
     def close(self):
         self.h.close()
 
+    def bind_outputs(self, obs, rew, term, trunc):
+        """Write step / reset outputs into caller-owned device tensors from now on (e.g. views of a
+        collective's send buffer, sharding.ShardedAviary(packed=True)): obs [E,N,D] float32, reward
+        [E] float32, terminated / truncated [E] bool, all contiguous on this env's device."""
+        want = ((self._obs, obs), (self._rew, rew), (self._term, term), (self._trunc, trunc))
+        for old, new in want:
+            if new.shape != old.shape or new.dtype != old.dtype or new.device != old.device or not new.is_contiguous():
+                raise ValueError(f"bind_outputs: need a contiguous {old.dtype} {tuple(old.shape)} tensor on {old.device}")
+        self._obs, self._rew, self._term, self._trunc = obs, rew, term, trunc
+
     # ---- fused wrappers (utils/wrapper.py; gym_pybullet_adrp_amd.utils.wrapper) ----
     @property
     def reward_wrapper(self):

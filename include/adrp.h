@@ -301,6 +301,22 @@ int adrp_policy_act(adrp_policy_t* p, const float* obs_dev, int rows, int obs_st
                     float* act_dev, void* stream);
 void adrp_policy_destroy(adrp_policy_t* p);
 
+/* ---------------------------------------------------------------------------------------
+ * Numerics probe (no reference counterpart: test support).  Evaluates one of the fp64
+ * fast transcendentals the fp64 step kernels inline (csrc/adrp_device.h namespace f64:
+ * refined v_rcp_f64 / v_rsq_f64, range-reduced polynomials) on n device doubles:
+ * out[i] = f(in[i]); ATAN2 reads y = in[i], x = in[n + i].  Stream-ordered.
+ * --------------------------------------------------------------------------------------- */
+#define ADRP_MATH_RCP 0
+#define ADRP_MATH_RSQ 1
+#define ADRP_MATH_SQRT 2
+#define ADRP_MATH_SIN_SMALL 3      /* |x| <= pi/8 */
+#define ADRP_MATH_COS_SMALL 4      /* |x| <= pi/8 */
+#define ADRP_MATH_ATAN2 5
+#define ADRP_MATH_ASIN 6           /* |x| < 1 */
+#define ADRP_MATH_EXP 7            /* x <= 0 in the kernels */
+int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

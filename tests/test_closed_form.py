@@ -14,12 +14,16 @@ velocity 100; reference call site envs/BaseAviary.py:373-374, forces :683-718):
   * torque-free spin about any axis: in the body frame of step n,
       |J w'_b|^2 = (1 - dt kw)^2 |J w_b|^2 + dt^2 |w_b x J w_b|^2,  kw = 0.04 (1 + |w_b|)
     (the gyroscopic term only turns J w; damping shrinks it);
-  * |q| = 1 over 10^4 sub-steps.
+  * |q| = 1 over 10^4 sub-steps;
+  * Newton's first law for a spinning, translating body with no force and no gravity: v keeps
+    its direction and its speed follows s' = s - dt 0.04 (1 + s) s; x' = x + dt v'.  This pins
+    the spatial -> classical "+ w x v" conversion of the base acceleration (oracle.c bullet_step):
+    without it (orc_set_bullet_variant(1)) the body's velocity would precess about w by dt |w x v|
+    per sub-step (test_newton_first_law_oracle shows that reading fails the law).
 
 The oracle is held to ~1e-12 (float64), the fp64 kernels to 1e-11 and the fp32 kernels to
-float32 rounding (-m gpu).  test_unpinned_wxv_residual quantifies the one unpinned choice these
-forms do not decide: whether the base's spatial acceleration is converted to a classical one
-(+ w x v); DESIGN.md §6 records the number.
+float32 rounding (-m gpu).  test_wxv_reading_residual measures how far the rejected reading
+(no "+ w x v") would move config-2 states; DESIGN.md §6 records the numbers.
 """
 import numpy as np
 import pytest
@@ -110,6 +114,27 @@ def free_fall_reference(p0, v0, dt, n):
     return out
 
 
+def newton_state(names, E, rng, z=50.0):
+    """no thrust (gravity 0 => HOVER_RPM 0, zero action), random attitude, spinning (world w) and
+    translating (world v), high above the plane"""
+    v = spin_state(names, E, rng.uniform(-8, 8, (E, 3)), rng)
+    v0 = rng.uniform(-3, 3, (E, 3))
+    for k, ax in enumerate("xyz"):
+        v[f"vel_{ax}"] = v0[:, k]
+    v["pos_z"] = np.full(E, z)
+    return v, v0
+
+
+def newton_reference(p0, v0, dt, n):
+    """x' = x + dt v', v' = v (1 - dt 0.04 (1 + |v|)): the damped straight line, float64"""
+    p, v, out = p0.copy(), v0.copy(), []
+    for _ in range(n):
+        v = v - dt * DAMP * (1 + np.linalg.norm(v, axis=1, keepdims=True)) * v
+        p = p + dt * v
+        out.append((p.copy(), v.copy()))
+    return out
+
+
 def spin_z_reference(w0, dt, n):
     w, th, out = w0.copy(), np.zeros_like(w0), []
     for _ in range(n):
@@ -178,7 +203,10 @@ def test_constant_thrust_vertical_oracle(a):
     assert np.abs(field(f, names[0], "omega_", "xyz")).max() == 0.0
 
 
-def test_free_fall_oracle():
+@pytest.mark.parametrize("spin", [False, True])
+def test_free_fall_oracle(spin):
+    """race path, motors off (eliminated drones): the damped free fall; with spin the same
+    recurrence holds (Newton: w does not turn v)"""
     E, N = 6, 2
     cfg = race_cfg(E)
     orc = O.Oracle(cfg)
@@ -191,7 +219,7 @@ def test_free_fall_oracle():
     for k, ax in enumerate("xyz"):
         vals[f"pos_{ax}"] = p0[:, k]
         vals[f"vel_{ax}"] = v0[:, k]
-        vals[f"omega_{ax}"] = np.zeros(E * N)
+        vals[f"omega_{ax}"] = rng.uniform(-8, 8, E * N) if spin else np.zeros(E * N)
     for m in range(4):
         vals[f"rpm_{m}"] = np.zeros(E * N)
         vals[f"prev_rpm_{m}"] = np.zeros(E * N)
@@ -264,10 +292,44 @@ def test_quaternion_norm_oracle():
     assert np.abs(np.linalg.norm(q, axis=1) - 1).max() < 1e-13
 
 
-def test_unpinned_wxv_residual():
-    """The one A.2 choice the closed forms above do not decide: whether btMultiBody's spatial
-    base acceleration gets the "+ w x v" conversion to a classical one (oracle.c bullet_step).
-    On BASELINE config-2 states (airborne around (0,0,1), |v|, |w| ~ U(+-0.1) per axis, RPM
+@pytest.mark.parametrize("variant", [0, 1])
+def test_newton_first_law_oracle(variant):
+    """force-free, gravity-free, spinning and translating: the restatement (variant 0, with the
+    spatial -> classical "+ w x v" conversion) keeps v on its damped straight line to 1e-12; the
+    other reading of btMultiBody (variant 1) turns v by ~dt |w x v| per sub-step and fails the law"""
+    E = 16
+    cfg = hover_cfg(E, gravity=0.0, pyb=240, ctrl=240)
+    rng = np.random.default_rng(8)
+    O.set_bullet_variant(variant)
+    try:
+        orc = O.Oracle(cfg)
+        names = orc.field_names()
+        vals, v0 = newton_state(names, E, rng)
+        f0, _ = set_fields(orc.get_state, orc.set_state, vals)
+        n = names[0]
+        ref = newton_reference(field(f0, n, "pos_", "xyz"), v0, 1.0 / 240, 240)
+        act = np.zeros((E, 1, 4), np.float32)
+        for _ in range(240):
+            orc.step(act)
+    finally:
+        O.set_bullet_variant(0)
+    f, _ = orc.get_state()
+    p, v = ref[-1]
+    vg = field(f, n, "vel_", "xyz")
+    # direction: sin of the angle between v(t) and v(0)
+    turn = np.linalg.norm(np.cross(vg, v0), axis=1) / (np.linalg.norm(vg, axis=1) * np.linalg.norm(v0, axis=1))
+    if variant == 0:
+        assert turn.max() < 1e-13, turn.max()
+        np.testing.assert_allclose(vg, v, rtol=1e-12, atol=1e-13)
+        np.testing.assert_allclose(field(f, n, "pos_", "xyz"), p, rtol=1e-12, atol=1e-12)
+    else:
+        assert turn.max() > 0.1, turn.max()      # 1 s at |w| ~ 8 rad/s: the velocity precesses
+
+
+def test_wxv_reading_residual():
+    """How much the rejected reading of btMultiBody (no spatial -> classical "+ w x v" conversion,
+    which test_newton_first_law_oracle shows violates Newton's first law) would change config-2
+    states: DESIGN.md §6 records the numbers.  On BASELINE config-2 states (airborne around (0,0,1), |v|, |w| ~ U(+-0.1) per axis, RPM
     actions) the per-env.step difference between the two readings is measured here and bounded;
     DESIGN.md §6 records it.  Worst case: O(dt |w| |v|) per sub-step."""
     E = 4096

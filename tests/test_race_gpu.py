@@ -219,6 +219,51 @@ def test_physics_substep_identical_rpm(level, N, physics, mode, reward, precisio
     env.close()
 
 
+@pytest.mark.parametrize("physics", [Physics.PYB_DW, Physics.PYB_GND_DRAG_DW])
+def test_physics_substep_identical_rpm_config4_size(physics):
+    """BASELINE config 4 at full size (4,096 envs x 4 drones, level3, COMPETE, disturbance force and
+    action noise on; also PYB_GND_DRAG_DW): one 500 Hz sub-step per env.step.  The GPU flies 0.4 s,
+    then EVERY drone is teacher-forced against the (OpenMP) oracle from the identical state for 4
+    sub-steps: pos / quat / vel / omega within the north-star 1e-4 bar (the physics consumes the
+    synced RPMs and the same Philox disturbance draws)."""
+    import os
+    E, N = 4096, 4
+    rng = np.random.default_rng(41)
+    env = MultiRaceAviary("level3", num_drones=N, physics=physics, racemode=RaceMode.COMPETE, num_envs=E, seed=7,
+                          autoreset=False, ctrl_freq=500)
+    orc = O.Oracle(env.cfg.copy())
+    obs, _ = env.reset()
+    orc.reset()
+    act = targets(rng, obs.cpu().numpy(), E, N)
+    at = torch.from_numpy(act).to(env.device)
+    for _ in range(200):
+        env.step(at)
+    f, i = env.get_state()
+    f, i = f.double().cpu().numpy(), i.cpu().numpy()
+    names, _ = orc.field_names()
+    idx = {n: k for k, n in enumerate(names)}
+    O.set_threads(min(16, os.cpu_count() or 1))
+    try:
+        worst = {}
+        for k in range(4):
+            orc.set_state(f, i)
+            env.set_state(torch.from_numpy(f.astype(np.float32)), torch.from_numpy(i))
+            orc.step(act)
+            env.step(at)
+            fg = env.get_state()[0].double().cpu().numpy()
+            fo, io = orc.get_state()
+            for g in ("pos", "quat", "vel", "omega"):
+                rows = [idx[n] for n in GROUPS[g]]
+                err = np.linalg.norm(fg[rows] - fo[rows], axis=0) / np.maximum(np.linalg.norm(fo[rows], axis=0), FLOORS[g])
+                worst[g] = max(worst.get(g, 0.0), float(err.max()))
+                assert err.max() <= 1e-4, f"sub-step {k} {g}: {err.max():.3e} at drone slot {err.argmax()}"
+            f, i = fo.astype(np.float32).astype(np.float64), io
+        print(physics, "worst relative error over 16,384 drones x 4 sub-steps:", worst)
+    finally:
+        O.set_threads(1)
+    env.close()
+
+
 def test_autoreset_and_truncation():
     """drive envs to their time limit: truncation at the same step, auto-reset obs == oracle's"""
     E, N = 32, 2
@@ -389,7 +434,8 @@ def test_obs_wrapper_autoreset(mode):
 
 
 @pytest.mark.parametrize("E,N,level,physics,mode", [(2048, 2, "level0", Physics.PYB, RaceMode.COMPARE),
-                                                    (4096, 4, "level3", Physics.PYB_DW, RaceMode.COMPETE)])
+                                                    (4096, 4, "level3", Physics.PYB_DW, RaceMode.COMPETE),
+                                                    (4096, 4, "level3", Physics.PYB_GND_DRAG_DW, RaceMode.COMPETE)])
 def test_full_size_subset_vs_oracle(E, N, level, physics, mode):
     """BASELINE configs 3 / 4 at full size: after 0.8 s of flight on the GPU, 48 random envs are
     teacher-forced one env.step against the oracle (one single-env oracle per sampled env, keyed by

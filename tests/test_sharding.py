@@ -75,13 +75,26 @@ class OracleShard:
         c.num_envs = num_envs
         c.env_offset = env_offset
         self.o = O.Oracle(c)
+        E = num_envs
+        self._obs = torch.zeros((E, self.o.N, self.o.D), dtype=torch.float32)
+        self._rew = torch.zeros(E, dtype=torch.float32)
+        self._term = torch.zeros(E, dtype=torch.bool)
+        self._trunc = torch.zeros(E, dtype=torch.bool)
+
+    def bind_outputs(self, obs, rew, term, trunc):    # the envs' packed-output contract
+        for old, new in ((self._obs, obs), (self._rew, rew), (self._term, term), (self._trunc, trunc)):
+            assert new.shape == old.shape and new.dtype == old.dtype and new.is_contiguous()
+        self._obs, self._rew, self._term, self._trunc = obs, rew, term, trunc
 
     def reset(self):
-        return torch.from_numpy(self.o.reset()), {}
+        self._obs.copy_(torch.from_numpy(self.o.reset()))
+        return self._obs, {}
 
     def step(self, act):
         obs, rew, te, tr, _ = self.o.step(act.numpy())
-        return torch.from_numpy(obs), torch.from_numpy(rew), torch.from_numpy(te), torch.from_numpy(tr), {}
+        for dst, src in ((self._obs, obs), (self._rew, rew), (self._term, te), (self._trunc, tr)):
+            dst.copy_(torch.from_numpy(src))
+        return self._obs, self._rew, self._term, self._trunc, {}
 
 
 def _actions(kind="hover"):
@@ -94,23 +107,38 @@ def _actions(kind="hover"):
     return np.repeat(t, 10, axis=0).astype(np.float32)
 
 
-def _worker(rank, world, port, out_dir, kind="hover"):
+def _unpack(g):
+    """packed Gathered views (per-rank row blocks, padded) -> global batches"""
+    cat = lambda x: torch.cat([x[r, :c] for r, c in enumerate(g.counts)])
+    return cat(g.obs).clone(), cat(g.rew).clone(), cat(g.term).clone(), cat(g.trunc).clone()
+
+
+def _worker(rank, world, port, out_dir, kind="hover", packed=False):
     import functools
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        env = ShardedAviary(E_GLOBAL, functools.partial(OracleShard, kind=kind))
+        env = ShardedAviary(E_GLOBAL, functools.partial(OracleShard, kind=kind), packed=packed)
         assert (env.offset, env.count) == shard_range(E_GLOBAL, world, rank)
         obs, _ = env.reset()
-        g_obs = env.gather(obs, torch.zeros(env.count), torch.zeros(env.count, dtype=torch.bool),
-                           torch.zeros(env.count, dtype=torch.bool))[0]
+        if packed:
+            g_obs = _unpack(env.gather_packed())[0]
+        else:
+            g_obs = env.gather(obs, torch.zeros(env.count), torch.zeros(env.count, dtype=torch.bool),
+                               torch.zeros(env.count, dtype=torch.bool))[0]
         traj = [g_obs.numpy()]
         rews, terms, truncs = [], [], []
         for a in _actions(kind):
-            obs, rew, te, tr, _ = env.step(torch.from_numpy(a))      # global batch in, own slice used
-            go, gr, gte, gtr = env.gather(obs, rew, te, tr)
-            traj.append(go.numpy()); rews.append(gr.numpy()); terms.append(gte.numpy()); truncs.append(gtr.numpy())
+            if packed:     # env.step + one all-gather of the packed send buffer, no per-step allocation
+                send = env._send.data_ptr()
+                go, gr, gte, gtr = _unpack(env.step_gather(torch.from_numpy(a)))
+                assert env._send.data_ptr() == send and env.env._obs.data_ptr() == send
+            else:
+                obs, rew, te, tr, _ = env.step(torch.from_numpy(a))      # global batch in, own slice used
+                go, gr, gte, gtr = env.gather(obs, rew, te, tr)
+            traj.append(go.numpy().copy()); rews.append(gr.numpy().copy()); terms.append(gte.numpy().copy())
+            truncs.append(gtr.numpy().copy())
         if rank == 0:
             np.savez(os.path.join(out_dir, f"sharded_{kind}.npz"), obs=np.stack(traj), rew=np.stack(rews),
                      term=np.stack(terms), trunc=np.stack(truncs))
@@ -125,16 +153,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
+@pytest.mark.parametrize("packed", [False, True])
 @pytest.mark.parametrize("kind", ["hover", "race"])
-def test_two_rank_gloo_matches_single_batch(tmp_path, kind):
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), kind), nprocs=2, join=True)
+def test_two_rank_gloo_matches_single_batch(tmp_path, kind, packed):
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), kind, packed), nprocs=2, join=True)
     got = np.load(tmp_path / f"sharded_{kind}.npz")
     one = OracleShard(E_GLOBAL, 0, kind)
     obs, _ = one.reset()
-    traj, rews, terms, truncs = [obs.numpy()], [], [], []
+    traj, rews, terms, truncs = [obs.numpy().copy()], [], [], []
     for a in _actions(kind):
-        obs, rew, te, tr, _ = one.step(torch.from_numpy(a))
-        traj.append(obs.numpy()); rews.append(rew.numpy()); terms.append(te.numpy()); truncs.append(tr.numpy())
+        obs, rew, te, tr, _ = one.step(torch.from_numpy(a))    # persistent buffers: copy
+        traj.append(obs.numpy().copy()); rews.append(rew.numpy().copy()); terms.append(te.numpy().copy())
+        truncs.append(tr.numpy().copy())
     np.testing.assert_array_equal(got["obs"], np.stack(traj))
     np.testing.assert_array_equal(got["rew"], np.stack(rews))
     np.testing.assert_array_equal(got["term"], np.stack(terms))

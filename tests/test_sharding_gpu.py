@@ -1,0 +1,127 @@
+"""BASELINE config 5 on the HIP path (one GPU): the 32,768-env level3 / COMPETE / 4-drone / PYB_DW /
+disturbed race sharded as 8 handles of 4,096 envs with env_offset = r * 4096 (what rank r of an
+8-GPU job builds, gym_pybullet_adrp_amd/sharding.py) against ONE 32,768-env handle.  Reset and
+sub-step draws are Philox-keyed by the global env id, so the shards must reproduce the single batch
+bit for bit: obs, reward, terminated, truncated, terminal obs and the full SoA state, 40 env.steps
+with auto-resets (reference step: envs/MultiRaceAviary.py:171-270).
+The packed-buffer gather of ShardedAviary (the learner-side reassembly) is checked on the same
+tensors with a one-rank gloo group.  Needs an MI355X: -m gpu."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary  # noqa: E402
+from gym_pybullet_adrp_amd.utils.enums import Physics, RaceMode  # noqa: E402
+
+SHARDS, E_SHARD, N = 8, 4096, 4
+E_GLOBAL = SHARDS * E_SHARD
+STEPS = 40
+
+
+def _make(num_envs, env_offset):
+    return MultiRaceAviary("level3", num_drones=N, physics=Physics.PYB_DW, racemode=RaceMode.COMPETE,
+                           num_envs=num_envs, env_offset=env_offset, seed=2024, autoreset=True, reward="wrapper")
+
+
+def _actions(obs0, dev):
+    """FULLSTATE targets: start + U(+-0.3) m for 3/4 of the envs (config 3/4's synthetic actions);
+    the rest outside the level3 bounds or at the ground, so drones are eliminated, envs terminate
+    and auto-reset inside the run.  Re-drawn every 10 steps."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(55)
+    out = []
+    for k in range(STEPS // 10):
+        tgt = obs0[..., :3] + torch.rand(obs0.shape[:2] + (3,), generator=g, device=dev) * 0.6 - 0.3
+        tgt[..., 2] = tgt[..., 2].clamp(0.2, 1.5)
+        wild = torch.rand(obs0.shape[:2] + (3,), generator=g, device=dev) * torch.tensor([8.0, 8.0, 2.6], device=dev) \
+            - torch.tensor([4.0, 4.0, 0.0], device=dev)
+        sel = (torch.arange(obs0.shape[0], device=dev) % 4 == k % 4)[:, None, None]
+        tgt = torch.where(sel, wild, tgt)
+        a = torch.cat([tgt, torch.zeros(obs0.shape[:2] + (1,), device=dev)], -1).contiguous()
+        out += [a] * 10
+    return out
+
+
+def test_config5_shards_bit_identical_to_one_batch():
+    one = _make(E_GLOBAL, 0)
+    shards = [_make(E_SHARD, r * E_SHARD) for r in range(SHARDS)]
+    dev = one.device
+    obs1, _ = one.reset()
+    obs_s = torch.cat([s.reset()[0] for s in shards])
+    assert torch.equal(obs1, obs_s)
+    # the reset states differ per env (global-id keyed draws), not per shard-local index
+    assert not torch.equal(obs_s[:E_SHARD], obs_s[E_SHARD:2 * E_SHARD])
+    acts = _actions(obs1.clone(), dev)
+    ep_field = one.state_field_names()[1].index("episode")
+    ep_prev = one.get_state()[1][ep_field].reshape(E_GLOBAL, N)[:, 0].clone()
+    done_total = 0
+    for k in range(STEPS):
+        o1, r1, te1, tr1, info1 = one.step(acts[k])
+        outs = [s.step(acts[k][r * E_SHARD:(r + 1) * E_SHARD]) for r, s in enumerate(shards)]
+        assert torch.equal(o1, torch.cat([o[0] for o in outs])), f"obs differ at step {k}"
+        assert torch.equal(r1, torch.cat([o[1] for o in outs])), f"reward differs at step {k}"
+        assert torch.equal(te1, torch.cat([o[2] for o in outs])), f"terminated differs at step {k}"
+        assert torch.equal(tr1, torch.cat([o[3] for o in outs])), f"truncated differs at step {k}"
+        done = te1 | tr1
+        tob1 = info1["terminal_observation"][done]
+        tobs = torch.cat([o[4]["terminal_observation"] for o in outs])[done]
+        assert torch.equal(tob1, tobs), f"terminal obs differ at step {k}"
+        # full-size property: exactly the done envs start a new episode in the same launch
+        ep = one.get_state()[1][ep_field].reshape(E_GLOBAL, N)[:, 0].clone()
+        assert torch.equal(ep - ep_prev, done.to(ep.dtype)), f"episode counters vs done flags at step {k}"
+        ep_prev = ep
+        done_total += int(done.sum())
+        assert torch.isfinite(o1).all()
+    assert done_total > 0, "the run should exercise termination + auto-reset"
+    f1, i1 = one.get_state()
+    fs = torch.cat([s.get_state()[0] for s in shards], 1)
+    is_ = torch.cat([s.get_state()[1] for s in shards], 1)
+    assert torch.equal(i1, is_)
+    np.testing.assert_array_equal(f1.cpu().numpy(), fs.cpu().numpy())    # NaN == NaN (D-term memory)
+    for s in shards:
+        s.close()
+    one.close()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_packed_gather_one_rank():
+    """ShardedAviary(packed=True): the env writes obs / reward / flags straight into the rank's slot
+    of the preallocated send buffer; step_gather() is env.step + one all-gather with no allocation,
+    and its global views equal the env's own outputs (world 1, gloo)."""
+    import functools
+    import torch.distributed as dist
+    from gym_pybullet_adrp_amd.sharding import ShardedAviary
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        E = 256
+        sh = ShardedAviary(E, functools.partial(MultiRaceAviary, "level3", num_drones=N, physics=Physics.PYB_DW,
+                                                racemode=RaceMode.COMPETE, seed=5), packed=True)
+        ref = MultiRaceAviary("level3", num_drones=N, physics=Physics.PYB_DW, racemode=RaceMode.COMPETE, seed=5,
+                              num_envs=E)
+        obs, _ = sh.reset()
+        obs_r, _ = ref.reset()
+        assert torch.equal(obs, obs_r)
+        act = torch.cat([obs_r[..., :3] + 0.1, torch.zeros_like(obs_r[..., :1])], -1).contiguous()
+        for _ in range(5):
+            g = sh.step_gather(act)
+            o, r, te, tr, _ = ref.step(act)
+            assert torch.equal(g.obs.reshape(E, N, -1), o)
+            assert torch.equal(g.rew.reshape(E), r)
+            assert torch.equal(g.term.reshape(E), te) and torch.equal(g.trunc.reshape(E), tr)
+        sh.close()
+        ref.close()
+    finally:
+        dist.destroy_process_group()
