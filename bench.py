@@ -5,24 +5,30 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 `value` is BASELINE.json configs[1] (HoverAviary, 4096 envs x 1 drone per GPU, PYB, 240/30 Hz =
-8 sub-steps, RPM actions, auto-reset): one "step" = one env.step() of every env on every GPU,
-one fused HIP launch per GPU, envs sharded across ranks (weak scaling, no collective on the
-step path).  Inputs are resident in HBM before the timed region.  `--gpus N` without a launcher
+8 sub-steps, RPM actions, auto-reset) at the reference's precision (float64 kernel; the
+reference integrates in float64): one "step" = one env.step() of every env on every GPU, one
+fused HIP launch per GPU, envs sharded across ranks (weak scaling, no collective on the step
+path).  Inputs are resident in HBM before the timed region.  `--gpus N` without a launcher
 starts N ranks itself (a child `torch.distributed.run`), before anything touches the GPU.
 
 The same JSON line carries sub-records (`configs`), each timed the same way:
   config5      every N: MultiRaceAviary COMPETE level3, 4 drones x 4096 envs per GPU, PYB_DW,
-               disturbances on (at N = 1 this is configs[3]); kernel-only and step + RCCL
-               all-gather of the packed obs/reward/flags (N > 1)
-  config3      N = 1: MultiRaceAviary COMPARE level0, 2 drones x 2048 envs, PYB
-  config3_policy  N = 1: config 3 driven by the reference's PPO actor on the device
-  config2_f64  N = 1: the `value` workload with the float64 kernel (reference precision)
+               disturbances on (at N = 1 this is configs[3]), float64 physics + wrapper and
+               float32 firmware as the reference; kernel-only, and (N > 1) step + RCCL
+               all-gather of the packed obs/reward/flags captured in the same HIP graph;
+               `strong`: 32,768 envs in total over the N GPUs
+  config5_f32  every N: the same with the float32 kernel
+  config3 / config3_f32  N = 1: MultiRaceAviary COMPARE level0, 2 drones x 2048 envs, PYB
+  config3_policy  N = 1: config 3 (float64) driven by the reference's PPO actor on the device
+  config4_gnd_drag_dw  N = 1: config 4 with Physics.PYB_GND_DRAG_DW (float64)
+  config2_f32  N = 1: the `value` workload with the float32 kernel
   config1      N = 1: one HoverAviary env (E = 1), per-step latency, GPU and CPU oracle
 Rooflines: the hover kernel is HBM-bound (bytes per launch / kernel time vs 8 TB/s); the race
-kernel is VALU/issue-bound (PMC-counted flops per launch / kernel time vs the fp32 vector peak;
-HBM fraction kept as information).  Kernel times are HIP events attached to each step kernel's
-own dispatch on its launching stream.  CPU baseline: the float64 oracle (test infrastructure)
-on the host, one thread and all of the job's cores (OpenMP over envs), bounded samples.
+kernel is VALU/issue-bound (PMC-counted flops per launch / kernel time vs the vector peak;
+HBM fraction kept as information).  Kernel time = HIP events on the launching stream around
+the timed region (K graph-replayed launches, one per step) / K; the per-dispatch events of
+eager launches are kept beside it.  CPU baseline: the float64 oracle (test infrastructure)
+on the host, one thread and the job's CPU share (OpenMP over envs), bounded samples.
 """
 import argparse
 import functools
@@ -54,7 +60,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=200)
     p.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
     p.add_argument("--physics", default="PYB")
-    p.add_argument("--precision", default="fp32")
+    p.add_argument("--precision", default="fp64", choices=["fp64", "fp32"],
+                   help="main line kernel precision (fp64 = the reference's float64)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU-baseline leg")
     p.add_argument("--no-allgather", action="store_true", help="N>1: skip the obs all-gather variant")
@@ -69,6 +76,9 @@ def parse():
     p.add_argument("--policy", default=None,
                    help="race main line: closed loop with the on-device PPO actor: 'example' / 'twogates' "
                         "(weights from tests/golden/policy_golden.npz) or a SB3 zip path")
+    p.add_argument("--graph-only", action="store_true",
+                   help="profiling runs (rocprofv3): no eager event-timed launches after the timed region, so "
+                        "the kernel statistics are those of the graph-replayed launches")
     p.add_argument("--launch-check", action="store_true",
                    help="CPU-only check of the rank launch: every rank joins a gloo group, rank 0 prints the "
                         "record of the world it saw, no GPU work")
@@ -164,7 +174,8 @@ def cpu_baseline(cfg, seconds, race=False):
     vN, nN, dN = _oracle_leg(cfg, max(E, 8 * thr), fn, seconds, thr)
     return {"value": vN, "unit": "env-steps/s", "cores": thr, "kind": "port",
             "sample": f"{max(E, 8 * thr)} envs x {nN} env.steps, float64 oracle, {dN:.1f} s, OpenMP {thr} threads "
-                      f"over envs; {info['model']}",
+                      f"over envs (the job's CPU share: OMP_NUM_THREADS / affinity cap {thr} of {info['nproc']} "
+                      f"host threads); {info['model']}",
             "one_core": {"value": v1, "cores": 1, "sample": f"{E} envs x {n1} env.steps, {d1:.1f} s, 1 thread"},
             "host": info}
 
@@ -194,9 +205,12 @@ def time_graph(stepper, acts, K, W, world, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(K // G):
         graph.replay()
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -205,6 +219,7 @@ def time_graph(stepper, acts, K, W, world, dev):
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     del graph
+    time_graph.last_event_ms = ev0.elapsed_time(ev1) / K     # device time per replayed step (this rank)
     return float(el.item()), G
 
 
@@ -273,42 +288,57 @@ def make_policy(spec, device):
     return DevicePolicy.from_zip(spec, device, mode)
 
 
-def hbm_roofline(bytes_per_launch, kern_ms, traffic_key):
-    avg_s = float(np.mean(kern_ms)) / 1e3
-    ach = bytes_per_launch / avg_s / 1e9
+def _kernel_time(step_ms, eager_ms):
+    """per-launch kernel time: the timed region's HIP events / K (graph replay, one launch per
+    step; what rocprofv3 of the same graph replays averages, plus the graph's inter-launch gaps),
+    and the eager per-dispatch events beside it"""
+    rec = {"kernel_us": step_ms * 1e3,
+           "kernel_time": "HIP events around the timed region (graph replay) / K on the launching stream"}
+    if eager_ms is not None and len(eager_ms):
+        rec.update({"eager_dispatch_us": float(np.mean(eager_ms)) * 1e3,
+                    "eager_dispatch_us_median": float(np.median(eager_ms)) * 1e3, "eager_launches": int(len(eager_ms))})
+    return rec
+
+
+def hbm_roofline(bytes_per_launch, step_ms, eager_ms, traffic_key):
+    rec = _kernel_time(step_ms, eager_ms)
+    ach = bytes_per_launch / (rec["kernel_us"] * 1e-6) / 1e9
     pmc = pmc_record("pmc_traffic.json", traffic_key)
-    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
-            "traffic": None if pmc is None else pmc["hbm_bytes_per_launch"],
-            "traffic_source": None if pmc is None else f"profiles/pmc_traffic.json[{traffic_key}]",
-            "bytes_per_launch": bytes_per_launch, "kernel_us": avg_s * 1e6,
-            "kernel_us_median": float(np.median(kern_ms)) * 1e3, "timed_launches": int(len(kern_ms))}
+    out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
+           "traffic": None if pmc is None else pmc["hbm_bytes_per_launch"],
+           "traffic_source": None if pmc is None else f"profiles/pmc_traffic.json[{traffic_key}]",
+           "bytes_per_launch": bytes_per_launch}
+    out.update(rec)
+    return out
 
 
-def valu_roofline(env, kern_ms, key, precision):
-    """race kernel: flops per launch over the kernel time, vs the vector peak.  Flop model: the PMC
-    FLOPS counters of the one-lane kernel per drone-step (profiles/pmc_valu.json
-    algorithmic_flops_per_drone_step; tools/pmc_summary.py valu mode); the four-lane kernel's own
-    counters (executed, redundant lanes included) and VALU busy beside it.  HBM fraction for information."""
-    avg_s = float(np.mean(kern_ms)) / 1e3
-    hbm = hbm_roofline(env.step_bytes(), kern_ms, key)
+def valu_roofline(env, step_ms, eager_ms, key, precision):
+    """race kernel: flops per launch over the kernel time, vs the vector peak (fp64 kernel: the
+    fp64 peak, although its firmware part is fp32 as in the reference).  Flop model: the PMC FLOPS
+    counters of the one-lane fp32 kernel per drone-step (profiles/pmc_valu.json
+    algorithmic_flops_per_drone_step; tools/pmc_summary.py valu mode): the same algorithm in either
+    precision; the kernel's own counters (executed flops, redundant quad lanes included) and VALU
+    busy beside it.  HBM fraction for information."""
+    hbm = hbm_roofline(env.step_bytes(), step_ms, eager_ms, key)
+    kt = _kernel_time(step_ms, eager_ms)
+    avg_s = kt["kernel_us"] * 1e-6
     pmc = pmc_record("pmc_valu.json", key)
     peak = VALU_F32_PEAK_TFLOPS if precision == "fp32" else VALU_F64_PEAK_TFLOPS
     drones = env.num_envs * env.NUM_DRONES
-    rec = {"bound": "valu", "achieved": None, "peak": peak, "unit": "TFLOP/s", "frac": None,
-           "traffic": hbm["traffic"], "kernel_us": hbm["kernel_us"], "kernel_us_median": hbm["kernel_us_median"],
-           "timed_launches": hbm["timed_launches"],
+    rec = {"bound": "valu", "achieved": None, "peak": peak, "unit": "TFLOP/s", "frac": None, "traffic": hbm["traffic"],
            "hbm": {"achieved_GBps": hbm["achieved"], "frac": hbm["frac"], "bytes_per_launch": hbm["bytes_per_launch"]}}
-    if pmc is not None:
-        # achieved = ALGORITHMIC flops (per drone-step, counted on the one-lane kernel) x drones per
-        # launch / kernel time; the four-lane kernel's executed flops (redundant quad lanes included)
-        # are reported beside it
-        exe = pmc["flops_per_launch"]
-        per_drone = pmc.get("algorithmic_flops_per_drone_step", exe / drones)
+    rec.update(kt)
+    alg = pmc_record("pmc_valu.json", key.replace("_fp64_", "_fp32_")) if pmc is None or "algorithmic_flops_per_drone_step" not in pmc else pmc
+    if alg is not None and "algorithmic_flops_per_drone_step" in alg:
+        per_drone = alg["algorithmic_flops_per_drone_step"]
         flops = per_drone * drones
         rec.update({"achieved": flops / avg_s / 1e12, "frac": flops / avg_s / 1e12 / peak,
                     "flops_per_launch": flops, "flops_per_drone_step": per_drone,
-                    "executed_flops_per_launch": exe, "executed_frac": exe / avg_s / 1e12 / peak,
-                    "valu_busy": pmc.get("valu_busy"), "source": f"profiles/pmc_valu.json[{key}]"})
+                    "source": f"profiles/pmc_valu.json[{key if pmc is alg else key.replace('_fp64_', '_fp32_')}]"})
+    if pmc is not None:
+        exe = pmc["flops_per_launch"]
+        rec.update({"executed_flops_per_launch": exe, "executed_frac": exe / avg_s / 1e12 / peak,
+                    "valu_busy": pmc.get("valu_busy"), "executed_source": f"profiles/pmc_valu.json[{key}]"})
     return rec
 
 
@@ -319,17 +349,53 @@ def race_key(level, drones, physics, precision, E):
 # ----------------------------------------------------------------------------------------------
 # workloads
 # ----------------------------------------------------------------------------------------------
+def _gather_record(sharded, acts, K, W, world, dev, E_rank, row_floats):
+    """step + packed all-gather (sharding.ShardedAviary(packed=True).step_gather): env.step and one
+    all_gather_into_tensor of the preallocated send buffer, captured together in the HIP graph;
+    eager (one launch + one collective per step) if the capture is refused"""
+
+    class _SG:
+        def step(self, a):
+            return sharded.step_gather(a)
+    rec = {"collective": "all_gather_into_tensor (RCCL over xGMI) of the packed obs/reward/flags send buffer "
+                         "(preallocated; the env writes its outputs into it)",
+           "bytes_per_rank_per_step": sharded._seg, "obs_floats_per_env": row_floats}
+    try:
+        el, G = time_graph(_SG(), acts, K, W, world, dev)
+        rec["timed_region"] = f"{K // G} replays of a {G}-step HIP graph (step kernel + RCCL all-gather per step)"
+    except Exception as exc:   # capture of the collective refused: time it eagerly instead
+        torch.cuda.synchronize()
+        rec["graph_capture_error"] = repr(exc)[:300]
+        for k in range(W):
+            sharded.step_gather(acts[k % acts.shape[0]])
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(K):
+            sharded.step_gather(acts[k % acts.shape[0]])
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        rec["timed_region"] = f"{K} eager steps (step kernel + RCCL all-gather each)"
+    rec.update({"value": E_rank * world * K / el, "unit": "env-steps/s", "ms_per_step": el / K * 1e3, "steps": K})
+    return rec
+
+
 def bench_race(level, drones, physics, racemode, precision, E, K, W, world, rank, dev, seed,
-               sharded_gather=False, policy_spec=None):
+               sharded_gather=False, policy_spec=None, graph_only=False, global_envs=None):
+    """one MultiRaceAviary workload; E envs per GPU, or global_envs in total (strong scaling)"""
     from gym_pybullet_adrp_amd import _lib
     make = race_make(level, drones, physics, racemode, precision, dev)
     sharded = None
     if world > 1:
         from gym_pybullet_adrp_amd.sharding import ShardedAviary
-        sharded = ShardedAviary(E * world, make)
+        sharded = ShardedAviary(global_envs or E * world, make, packed=sharded_gather)
         env = sharded.env
     else:
-        env = make(num_envs=E, env_offset=0)
+        env = make(num_envs=global_envs or E, env_offset=0)
+    E = env.num_envs
     obs0, _ = env.reset()
     acts = race_actions(obs0.clone(), dev, seed + rank)
     policy = None
@@ -344,14 +410,22 @@ def bench_race(level, drones, physics, racemode, precision, E, K, W, world, rank
                 return env.step(pact)
         stepper = _Loop()
     elapsed, G = time_graph(stepper, acts, K, W, world, dev)
-    kern = kernel_times(env, acts, min(K, 512), stepper)   # closed loop: the actor-driven steps
+    step_ms = time_graph.last_event_ms
+    # closed loop: the timed region holds the policy launch too, so the step kernel's own time comes
+    # from its dispatch events on the actor-driven steps
+    eager = None if graph_only else kernel_times(env, acts, min(K, 512), stepper)
+    if policy is not None and eager is not None:
+        step_ms = float(np.mean(eager))
     key = race_key(level, drones, physics, precision, E)
-    rec = {"workload": f"MultiRaceAviary {racemode} {level}, {drones} drones x {E} envs per GPU, Physics.{physics} "
-                       f"500/25 Hz (20 sub-steps, Mellinger 500 Hz), {precision}",
-           "value": E * world * K / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
-           "ms_per_step": elapsed / K * 1e3, "drone_steps_per_s": E * world * K / elapsed * drones,
-           "kernel": _lib.kernel_name(env.cfg),
-           "roofline": valu_roofline(env, kern, key, precision),
+    total = E * world
+    rec = {"workload": f"MultiRaceAviary {racemode} {level}, {drones} drones x {E} envs per GPU ({total} in total), "
+                       f"Physics.{physics} 500/25 Hz (20 sub-steps, Mellinger 500 Hz), {precision}"
+                       + (" (float64 physics / wrapper, float32 firmware: the reference's precision)"
+                          if precision == "fp64" else " (narrower than the reference's float64)"),
+           "value": total * K / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
+           "ms_per_step": elapsed / K * 1e3, "drone_steps_per_s": total * K / elapsed * drones,
+           "envs_per_gpu": E, "global_envs": total, "kernel": env.kernel_name,
+           "roofline": valu_roofline(env, step_ms, eager, key, precision),
            "timed_region": f"{K // G} replays of a {G}-step HIP graph"}
     if policy is not None:
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(200)]
@@ -373,22 +447,7 @@ def bench_race(level, drones, physics, racemode, precision, E, K, W, world, rank
         rec["world"] = dist.get_world_size()
         rec["backend"] = dist.get_backend()
         if sharded_gather:
-            ng = min(K, 300)
-            for k in range(10):
-                sharded.gather(*env.step(acts[k % acts.shape[0]])[:4])
-            torch.cuda.synchronize()
-            dist.barrier()
-            tg0 = time.perf_counter()
-            for k in range(ng):
-                sharded.gather(*env.step(acts[k % acts.shape[0]])[:4])
-            torch.cuda.synchronize()
-            tg = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64, device=dev)
-            dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-            tg = float(tg.item())
-            rec["with_obs_allgather"] = {
-                "value": E * world * ng / tg, "unit": "env-steps/s", "ms_per_step": tg / ng * 1e3, "steps": ng,
-                "collective": "all_gather_into_tensor (RCCL over xGMI) of packed fp32 obs+reward+flags, eager",
-                "bytes_per_rank_per_step": E * (drones * env.h.D + 3) * 4}
+            rec["with_obs_allgather"] = _gather_record(sharded, acts, K, W, world, dev, E, drones * env.h.D)
     env.close()
     return rec
 
@@ -399,44 +458,31 @@ def bench_hover(args, precision, E, K, W, world, rank, dev, sweep=False, sharded
     sharded = None
     if world > 1:
         from gym_pybullet_adrp_amd.sharding import ShardedAviary
-        sharded = ShardedAviary(E * world, make)     # rank r owns global envs [r*E, (r+1)*E)
+        sharded = ShardedAviary(E * world, make, packed=sharded_gather)   # rank r owns global envs [r*E, (r+1)*E)
         env = sharded.env
     else:
         env = make(num_envs=E, env_offset=0)
     env.reset()
     acts = hover_actions(E, dev, 1 + rank)
     elapsed, G = time_graph(env, acts, K, W, world, dev)
-    kern = kernel_times(env, acts, min(K, 512))
-    # eager (no graph) end-to-end rate, for reference
-    torch.cuda.synchronize()
-    ne = min(K, 1000)
-    te0 = time.perf_counter()
-    for k in range(ne):
-        env.step(acts[k % acts.shape[0]])
-    torch.cuda.synchronize()
-    te = time.perf_counter() - te0
+    step_ms = time_graph.last_event_ms
+    eager = None if args.graph_only else kernel_times(env, acts, min(K, 512))
     rec = {"value": E * world * K / elapsed, "ms_per_step": elapsed / K * 1e3,
-           "kernel": _lib.kernel_name(env.cfg),
-           "roofline": hbm_roofline(env.step_bytes(), kern, f"{args.physics}_{precision}_{E}"),
-           "timing": {"timed_region": f"{K // G} replays of a {G}-step HIP graph (one fused launch per env.step)",
-                      "eager": {"env_steps_per_s_per_gpu": E * ne / te, "ms_per_step": te / ne * 1e3}}}
+           "kernel": env.kernel_name,
+           "roofline": hbm_roofline(env.step_bytes(), step_ms, eager, f"{args.physics}_{precision}_{E}"),
+           "timing": {"timed_region": f"{K // G} replays of a {G}-step HIP graph (one fused launch per env.step)"}}
+    if not args.graph_only:
+        # eager (no graph) end-to-end rate, for reference
+        torch.cuda.synchronize()
+        ne = min(K, 1000)
+        te0 = time.perf_counter()
+        for k in range(ne):
+            env.step(acts[k % acts.shape[0]])
+        torch.cuda.synchronize()
+        te = time.perf_counter() - te0
+        rec["timing"]["eager"] = {"env_steps_per_s_per_gpu": E * ne / te, "ms_per_step": te / ne * 1e3}
     if sharded is not None and sharded_gather:
-        ng = min(K, 500)
-        for k in range(10):
-            sharded.gather(*env.step(acts[k % acts.shape[0]])[:4])
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg0 = time.perf_counter()
-        for k in range(ng):
-            sharded.gather(*env.step(acts[k % acts.shape[0]])[:4])
-        torch.cuda.synchronize()
-        tg = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64, device=dev)
-        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-        tg = float(tg.item())
-        rec["with_obs_allgather"] = {"value": E * world * ng / tg, "unit": "env-steps/s",
-                                     "ms_per_step": tg / ng * 1e3, "steps": ng,
-                                     "collective": "all_gather_into_tensor (RCCL) of packed fp32 obs+reward+flags",
-                                     "bytes_per_rank_per_step": E * (env.h.D + 3) * 4}
+        rec["with_obs_allgather"] = _gather_record(sharded, acts, K, W, world, dev, E, env.h.D)
     if sweep:
         rec["roofline"]["sweep"] = roofline_sweep(make, [65536, 262144, 1048576])
     cfg = env.cfg.copy()
@@ -467,7 +513,7 @@ def bench_config1(args, dev, cpu_seconds, with_cpu):
     """BASELINE configs[0]: one HoverAviary env (E = 1, PYB, 240/30 Hz) stepped from Python like
     examples/pid.py: per-step latency on the GPU (synchronised each step, and graph-replayed)
     and the float64 oracle for one env on one host core."""
-    make = hover_make("fp32", "PYB", dev)
+    make = hover_make(args.precision, "PYB", dev)
     env = make(num_envs=1, env_offset=0)
     env.reset()
     acts = hover_actions(1, dev, 3)
@@ -482,16 +528,46 @@ def bench_config1(args, dev, cpu_seconds, with_cpu):
     sync_s = (time.perf_counter() - t0) / n
     elapsed, G = time_graph(env, acts, 1000, 10, 1, dev)
     kern = kernel_times(env, acts, 200)
-    rec = {"workload": "HoverAviary 1 env x 1 drone, Physics.PYB 240/30 Hz (8 sub-steps), RPM actions, fp32",
+    graph_kernel_us = time_graph.last_event_ms * 1e3
+    rec = {"workload": f"HoverAviary 1 env x 1 drone, Physics.PYB 240/30 Hz (8 sub-steps), RPM actions, {args.precision}",
            "gpu_sync_per_step": {"value": 1 / sync_s, "unit": "env-steps/s", "us_per_step": sync_s * 1e6,
                                  "note": "Python env.step + torch.cuda.synchronize each step"},
            "gpu_graph": {"value": 1000 / elapsed, "unit": "env-steps/s", "us_per_step": elapsed / 1000 * 1e6},
-           "kernel_us": float(np.mean(kern)) * 1e3}
+           "kernel_us": graph_kernel_us, "eager_dispatch_us": float(np.mean(kern)) * 1e3}
     if with_cpu:
         v, steps, dt = _oracle_leg(env.cfg, 1, _hover_acts, min(cpu_seconds, 3.0), 1)
         rec["cpu_oracle_1env"] = {"value": v, "unit": "env-steps/s", "cores": 1,
                                   "sample": f"1 env x {steps} env.steps, {dt:.1f} s"}
     env.close()
+    return rec
+
+
+def bench_sb3_loop(args, dev, E=ENVS_PER_GPU, K=200, W=20):
+    """SB3's side of the boundary (examples/learn.py:53-57 make_vec_env + PPO.collect_rollouts):
+    numpy actions in, numpy obs / rewards / dones / infos out, through vec_env.AviaryVecEnv, on
+    the `value` workload.  packed = one packed device buffer, one async copy into pinned memory,
+    one wait, lazy infos; legacy = per-tensor .cpu() copies and a dict per env."""
+    from gym_pybullet_adrp_amd.vec_env import AviaryVecEnv
+    make = hover_make(args.precision, args.physics, dev)
+    rng = np.random.default_rng(1)
+    acts = rng.uniform(-1, 1, (16, E, 1, 4)).astype(np.float32)
+    rec = {"workload": f"HoverAviary {E} envs ({args.precision}) stepped through the SB3 VecEnv protocol "
+                       "(numpy actions in, numpy obs / rewards / dones / infos out, auto-reset infos)"}
+    for name, packed in (("packed", True), ("legacy", False)):
+        env = make(num_envs=E, env_offset=0)
+        v = AviaryVecEnv(env, packed=packed)
+        v.reset()
+        for k in range(W):
+            v.step(acts[k % 16])
+        t0 = time.perf_counter()
+        done = 0
+        for k in range(K):
+            _, _, d, _ = v.step(acts[k % 16])
+            done += int(d.sum())
+        dt = time.perf_counter() - t0
+        rec[name] = {"value": E * K / dt, "unit": "env-steps/s", "us_per_step": dt / K * 1e6, "steps": K,
+                     "done_envs": done}
+        v.close()
     return rec
 
 
@@ -546,17 +622,32 @@ def main():
 
     if not args.no_configs and args.task == "hover":
         cf = {}
-        # config 5 at every N (at N = 1 it is BASELINE configs[3])
-        cf["config5"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp32", 4096, RK, RW, world, rank, local, 4,
-                                   sharded_gather=world > 1 and not args.no_allgather)
+        gather = world > 1 and not args.no_allgather
+        go = args.graph_only
+        # config 5 at every N (at N = 1 it is BASELINE configs[3]): reference precision, then fp32;
+        # `strong`: the 32,768 envs of config 5 in total over the N GPUs
+        cf["config5"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp64", 4096, RK, RW, world, rank, local, 4,
+                                   sharded_gather=gather, graph_only=go)
+        cf["config5"]["strong"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp64", None, RK, RW, world, rank,
+                                             local, 4, graph_only=go, global_envs=8 * 4096)
+        cf["config5_f32"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp32", 4096, RK, RW, world, rank, local, 4,
+                                       sharded_gather=gather, graph_only=go)
         if world == 1:
-            cf["config3"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2)
-            cf["config3_policy"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
-                                              policy_spec="example")
-            r64, _ = bench_hover(args, "fp64", E, min(K, 1000), min(W, 100), 1, 0, local)
-            r64.update({"workload": "the `value` workload with the float64 kernel", "unit": "env-steps/s"})
-            cf["config2_f64"] = r64
-            cf["config1"] = bench_config1(args, local, args.cpu_seconds, not args.no_cpu_baseline)
+            cf["config4_gnd_drag_dw"] = bench_race("level3", 4, "PYB_GND_DRAG_DW", "COMPETE", "fp64", 4096, RK, RW, 1,
+                                                   0, local, 4, graph_only=go)
+            cf["config3"] = bench_race("level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2, graph_only=go)
+            cf["config3_f32"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
+                                           graph_only=go)
+            cf["config3_policy"] = bench_race("level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2,
+                                              policy_spec="example", graph_only=go)
+            other = "fp32" if args.precision == "fp64" else "fp64"
+            r2, _ = bench_hover(args, other, E, min(K, 1000), min(W, 100), 1, 0, local)
+            r2.update({"workload": f"the `value` workload with the {other} kernel", "unit": "env-steps/s",
+                       "dtype": "f32" if other == "fp32" else "f64"})
+            cf[f"config2_{'f32' if other == 'fp32' else 'f64'}"] = r2
+            if not go:
+                cf["config1"] = bench_config1(args, local, args.cpu_seconds, not args.no_cpu_baseline)
+                cf["config2_sb3_vecenv"] = bench_sb3_loop(args, local)
         result["configs"] = cf
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -567,7 +658,8 @@ def main():
             if "configs" in result:
                 from gym_pybullet_adrp_amd.envs.race import race_config
                 for name, lv, n, ph, md in (("config5", "level3", 4, "PYB_DW", "COMPETE"),
-                                            ("config3", "level0", 2, "PYB", "COMPARE")):
+                                            ("config3", "level0", 2, "PYB", "COMPARE"),
+                                            ("config4_gnd_drag_dw", "level3", 4, "PYB_GND_DRAG_DW", "COMPETE")):
                     c = race_config(lv, n, ph, md)
                     result["configs"][name]["cpu_baseline"] = cpu_baseline(c, args.cpu_seconds / 2, race=True)
     elif rank == 0:

@@ -55,6 +55,9 @@ def load():
     lib.adrp_set_state.argtypes = [P, P, P, P]
     lib.adrp_kernel_name.argtypes = [P]
     lib.adrp_kernel_name.restype = ctypes.c_char_p
+    if hasattr(lib, "adrp_handle_kernel_name"):   # (A/B runs may load an older build without it)
+        lib.adrp_handle_kernel_name.argtypes = [P]
+        lib.adrp_handle_kernel_name.restype = ctypes.c_char_p
     lib.adrp_step_bytes.argtypes = [P]
     lib.adrp_step_bytes.restype = ctypes.c_int64
     lib.adrp_profile_begin.argtypes = [P, I]
@@ -79,8 +82,9 @@ def load():
     lib.adrp_policy_act.restype = I
     lib.adrp_policy_destroy.argtypes = [P]
     lib.adrp_policy_destroy.restype = None
-    lib.adrp_math_probe.argtypes = [I, P, P, I, P]
-    lib.adrp_math_probe.restype = I
+    if hasattr(lib, "adrp_math_probe"):      # (A/B runs may load an older build without it)
+        lib.adrp_math_probe.argtypes = [I, P, P, I, P]
+        lib.adrp_math_probe.restype = I
     if lib.adrp_abi_version() != abi.ABI_VERSION:
         raise AdrpError(f"libadrp ABI {lib.adrp_abi_version()} != python mirror {abi.ABI_VERSION}")
     _lib = lib
@@ -176,6 +180,12 @@ class Handle:
 
     def step_bytes(self):
         return self.lib.adrp_step_bytes(self.h)
+
+    def kernel_name(self):
+        """the step-kernel instantiation this handle launches now"""
+        if not hasattr(self.lib, "adrp_handle_kernel_name"):
+            return kernel_name(self.cfg)
+        return self.lib.adrp_handle_kernel_name(self.h).decode()
 
     # ---- high-level command mode (include/adrp.h adrp_enable_commands) ----
     CMD_NF, CMD_NI, CMD_ARGS = 63, 3, 14

@@ -285,7 +285,7 @@ extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
     const int p = cfg->physics >= 0 && cfg->physics <= 5 ? cfg->physics : 0;
     if (cfg->task == ADRP_TASK_RACE) {
         const char* q = getenv("ADRP_RACE_QUAD");
-        const bool quad = !cfg->precision && !(q && atoi(q) == 0);
+        const bool quad = !(q && atoi(q) == 0);
         snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s>", cfg->precision ? "f64" : "f32", ph[p],
                  race_group(cfg->num_drones), quad ? ",Q4" : "");
         return buf;
@@ -299,6 +299,21 @@ extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
     }
     snprintf(buf, sizeof buf, "hover_step<%s,%s,A%d,B%s,%s>", cfg->precision ? "f64" : "f32", ph[p], A,
              cfg->action_buffer_size == 15 ? "15" : "n", config_is_cf2x(*cfg) ? "cf2x" : "generic");
+    return buf;
+}
+
+// the instantiation a live handle launches: command mode (adrp_enable_commands) switches a race
+// handle to the one-lane G = 8 command kernel, ADRP_RACE_QUAD is read at create
+extern "C" const char* adrp_handle_kernel_name(const adrp_t* h) {
+    static thread_local char buf[96];
+    if (!h) return nullptr;
+    if (h->cfg.task != ADRP_TASK_RACE) return adrp_kernel_name(&h->cfg);
+    static const char* ph[] = {"PYB", "DYN", "PYB_GND", "PYB_DRAG", "PYB_DW", "PYB_GND_DRAG_DW"};
+    const int p = h->cfg.physics >= 0 && h->cfg.physics <= 5 ? h->cfg.physics : 0;
+    const char* prec = h->real_size == 8 ? "f64" : "f32";
+    if (h->cmdf) snprintf(buf, sizeof buf, "race_step<%s,%s,G8,CMD>", prec, ph[p]);
+    else snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s>", prec, ph[p], race_group(h->N),
+                  h->race_quad ? ",Q4" : "");
     return buf;
 }
 
@@ -678,9 +693,9 @@ extern "C" int adrp_set_diagnostics(adrp_t* h, int enable) {
 // sums over waves, the same phases' max over waves at [10..17], GJK calls/iterations at
 // 9/18/19; hover: tools/hover_phases.py.  Summed over the kernel code objects.
 extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
-    int (*readers[7])(unsigned long long*, int) = {phase_read_hover_f32, phase_read_hover_f64, phase_read_race_f32,
+    int (*readers[8])(unsigned long long*, int) = {phase_read_hover_f32, phase_read_hover_f64, phase_read_race_f32,
                                                   phase_read_race_f32b, phase_read_race_f32c, phase_read_race_f64,
-                                                  phase_read_race_f64b};
+                                                  phase_read_race_f64b, phase_read_race_f64c};
     for (int k = 0; k < 32; ++k) out[k] = 0;
     for (auto rd : readers) {
         unsigned long long v[32];
@@ -696,6 +711,7 @@ extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
 // per-workgroup phases of the fp32 four-lane race kernel: n slots of [setup, physics, controller,
 // rays, obs, contacts, tail, total] s_memtime cycles (RACE_WAVE), written by the last launch
 extern "C" int adrp_race_wave_read(unsigned long long* out, int n) { return wave_read_race_f32(out, n); }
+extern "C" int adrp_race_wave_read_f64(unsigned long long* out, int n) { return wave_read_race_f64(out, n); }
 #endif
 
 extern "C" int adrp_diagnostic_contact_count(adrp_t* h, int reset) {

@@ -36,7 +36,7 @@ struct adrp_handle {
     bool stage_rows = true;       // LDS-staged obs rows when E % 64 == 0 (ADRP_STAGE_ROWS=0 disables)
     bool reset_helper = true;     // staged kernels: reset states from a helper wave (ADRP_RESET_HELPER=0)
     bool race_helpers = true;     // race fp32: helper waves (track copy, draws) (ADRP_RACE_HELPERS=0)
-    bool race_quad = true;        // race fp32: four lanes per drone (race_quad.h) (ADRP_RACE_QUAD=0: one lane)
+    bool race_quad = true;        // race: four lanes per drone (race_quad.h) (ADRP_RACE_QUAD=0: one lane)
     bool race_refine = true;      // race: support-function bounds before GJK (ADRP_RACE_REFINE=0: centre bounds only)
     float* cmdf = nullptr;        // race command mode (adrp_enable_commands): [ADRP_CMD_NF][E*N]
     int32_t* cmdi = nullptr;      // [ADRP_CMD_NI][E*N]
@@ -129,7 +129,9 @@ int phase_read_race_f64(unsigned long long* out, int reset);
 int phase_read_race_f32b(unsigned long long* out, int reset);
 int phase_read_race_f32c(unsigned long long* out, int reset);
 int phase_read_race_f64b(unsigned long long* out, int reset);
+int phase_read_race_f64c(unsigned long long* out, int reset);
 int wave_read_race_f32(unsigned long long* out, int n);
+int wave_read_race_f64(unsigned long long* out, int n);
 #define ADRP_PHASE_READER(name)                                                                  \
     int name(unsigned long long* out, int reset) {                                               \
         if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_race_phase), 32 * sizeof(unsigned long long)) != hipSuccess) \

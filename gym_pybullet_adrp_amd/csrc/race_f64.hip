@@ -1,15 +1,14 @@
-// race_f64.hip — race kernels and launchers for Real = double.  PYB, PYB_DW and DYN here, the
-// other physics modes in race_f64b.hip (parallel build).
+// race_f64.hip — race kernels and launchers for Real = double.  The step kernels of the physics
+// modes are split over three translation units as in fp32 (race_f64.hip: PYB, PYB_DW — the benched
+// ones and the dispatch; race_f64b.hip: DYN, PYB_GND; race_f64c.hip: PYB_DRAG, PYB_GND_DRAG_DW).
 #include "race_launch.h"
 
+extern template ADRP_RACE_STEP_PH(double, ADRP_PHYS_DYN);
 extern template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_GND);
 extern template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_DRAG);
 extern template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_GND_DRAG_DW);
-#ifndef ADRP_DEV_FAST
 template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB);
 template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_DW);
-template ADRP_RACE_STEP_PH(double, ADRP_PHYS_DYN);
-#endif
 
 template int race_step<double>(adrp_t*, const float*, float*, float*, uint8_t*, uint8_t*, float*, hipStream_t);
 template int race_reset<double>(adrp_t*, const uint8_t*, float*, hipStream_t);
@@ -18,4 +17,5 @@ template int race_cmd_init<double>(adrp_t*, hipStream_t);
 
 #ifdef ADRP_RACE_TIMING
 ADRP_PHASE_READER(phase_read_race_f64)
+ADRP_WAVE_READER(wave_read_race_f64)
 #endif

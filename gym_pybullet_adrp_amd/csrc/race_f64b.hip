@@ -1,10 +1,9 @@
-// race_f64b.hip — fp64 race step kernels of PYB_GND, PYB_DRAG and PYB_GND_DRAG_DW (see race_f64.hip)
+// race_f64b.hip — fp64 race step kernels of DYN and PYB_GND (see race_f64.hip)
 #include "race_launch.h"
 
 #ifndef ADRP_DEV_FAST
+template ADRP_RACE_STEP_PH(double, ADRP_PHYS_DYN);
 template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_GND);
-template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_DRAG);
-template ADRP_RACE_STEP_PH(double, ADRP_PHYS_PYB_GND_DRAG_DW);
 #endif
 
 #ifdef ADRP_RACE_TIMING

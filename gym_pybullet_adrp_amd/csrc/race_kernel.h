@@ -1378,6 +1378,26 @@ __global__ void __launch_bounds__(kRaceBlock) race_command_kernel(RaceArgs<Real>
 // ---------------------------------------------------------------------------------------
 // The 7 disturbance values of one drone and sub-step (MultiRaceAviary.py:222-228, 532-544): the
 // world force U(lo, hi) on link 4 and the N(0, std) thrust noise per motor (Box-Muller pairs).
+// The Gaussian samples come from the hardware log2 / sin / cos (float) in both precisions: they
+// are random numbers of a documented Philox stream (DESIGN.md §6 deviation 5), not a computation
+// of the reference's; the fp64 kernel widens them (its force draws stay in Real).
+template <typename Real>
+__device__ __forceinline__ void race_noise_draws(const RaceConst<Real>& H, uint64_t seed, uint64_t gid, uint32_t ep,
+                                                 int dn, uint32_t idx, Real noise[4]) {
+    const U4 v = draw(seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
+    const uint32_t x[4] = {v.a, v.b, v.c, v.d};
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const float u1 = (float(x[2 * p] >> 8) + 1.0f) * float(1.0 / 16777216.0);
+        const float u2 = float(x[2 * p + 1] >> 8) * float(1.0 / 16777216.0);
+        // v_log_f32 is log2; v_sin / v_cos take turns
+        const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+        const float sn = __builtin_amdgcn_sinf(u2), cs = __builtin_amdgcn_cosf(u2);
+        noise[2 * p] = Real(r * cs) * H.noise_std;
+        noise[2 * p + 1] = Real(r * sn) * H.noise_std;
+    }
+}
+
 template <typename Real>
 __device__ __forceinline__ void race_substep_draws(const RaceConst<Real>& H, uint64_t seed, uint64_t gid, uint32_t ep,
                                                    int dn, uint32_t idx, Real fd[3], Real noise[4]) {
@@ -1385,26 +1405,8 @@ __device__ __forceinline__ void race_substep_draws(const RaceConst<Real>& H, uin
     fd[0] = H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * u01r<Real>(u.a);
     fd[1] = H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * u01r<Real>(u.b);
     fd[2] = H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * u01r<Real>(u.c);
-    const U4 v = draw(seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
-    const uint32_t x[4] = {v.a, v.b, v.c, v.d};
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        const Real u1 = (Real(x[2 * p] >> 8) + Real(1)) * Real(1.0 / 16777216.0);
-        const Real u2 = Real(x[2 * p + 1] >> 8) * Real(1.0 / 16777216.0);
-        Real r, sn, cs;
-        if constexpr (sizeof(Real) == 4) {   // v_log_f32 is log2; v_sin/v_cos take turns
-            r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-            sn = __builtin_amdgcn_sinf(u2);
-            cs = __builtin_amdgcn_cosf(u2);
-        } else {
-            r = sqrt_(Real(-2) * log(u1));
-            sincos_(Real(6.283185307179586) * u2, &sn, &cs);
-        }
-        noise[2 * p] = r * cs * H.noise_std;
-        noise[2 * p + 1] = r * sn * H.noise_std;
-    }
+    race_noise_draws(H, seed, gid, ep, dn, idx, noise);
 }
-
 // Block = kRaceBlock drone lanes.  Wave 0 runs the serial sub-step chain (physics -> controller ->
 // physics ...; one wave per CU at the race batch sizes, one instruction per 4 cycles).  With
 // disturbances on, kRaceHelpers more waves, on the CU's otherwise idle SIMDs, pre-compute every

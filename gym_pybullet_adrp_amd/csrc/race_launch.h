@@ -3,9 +3,9 @@
 
 #include "adrp_internal.h"
 
-// fp32, four lanes per drone (race_quad.h): 16 drones per 64-lane block
-template <int PH>
-static void launch_race_q4(const RaceArgs<float>& a, int G, hipStream_t s, adrp_t* h) {
+// four lanes per drone (race_quad.h): 16 drones per 64-lane block
+template <typename Real, int PH>
+static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
     const bool draws = h->cfg.track.disturbances && h->S <= kRacePreS;
     const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G * 4 + kRaceBlock - 1) / kRaceBlock));
     auto go = [&](auto kernel) {
@@ -20,11 +20,11 @@ static void launch_race_q4(const RaceArgs<float>& a, int G, hipStream_t s, adrp_
         constexpr bool D = decltype(dr)::value;
         switch (G) {
 #ifndef ADRP_DEV_FAST
-            case 1: go(race_step_q4<PH, 1, D>); break;
-            case 8: go(race_step_q4<PH, 8, D>); break;
+            case 1: go(race_step_q4<Real, PH, 1, D>); break;
+            case 8: go(race_step_q4<Real, PH, 8, D>); break;
 #endif
-            case 2: go(race_step_q4<PH, 2, D>); break;
-            default: go(race_step_q4<PH, 4, D>); break;
+            case 2: go(race_step_q4<Real, PH, 2, D>); break;
+            default: go(race_step_q4<Real, PH, 4, D>); break;
         }
     };
     if (draws) by_g(std::true_type{});
@@ -49,9 +49,7 @@ static void launch_race_cmd(const RaceArgs<Real>& a, hipStream_t s, adrp_t* h) {
 template <typename Real, int PH>
 static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
     if (h->cmdf) return launch_race_cmd<Real, PH>(a, s, h);
-    if constexpr (sizeof(Real) == 4) {
-        if (h->race_quad) return launch_race_q4<PH>(a, G, s, h);
-    }
+    if (h->race_quad) return launch_race_q4<Real, PH>(a, G, s, h);
     // kRaceBlock drone lanes, + kRaceHelpers helper waves per block in the fp32 kernel (the track
     // copy into LDS, and the sub-step draws with disturbances on; race_kernel.h)
     const int helpers = sizeof(Real) != 4 || !h->race_helpers ? 0

@@ -1,4 +1,4 @@
-// race_quad.h — MultiRaceAviary env.step, fp32, four lanes per drone (gfx950).
+// race_quad.h — MultiRaceAviary env.step, four lanes per drone (gfx950), fp32 and fp64.
 //
 // The one-lane kernel (race_kernel.h) puts a drone on a lane, so config 4 (16,384 drones) is 256
 // waves: one per CU, on one of its four SIMDs, each issuing one VALU instruction per 4 cycles
@@ -19,7 +19,9 @@
 // reward, reset) runs redundantly on the quad's four lanes; lane ql = 0 owns the stores.  The
 // per-element arithmetic is the one-lane kernel's, operation for operation (the same functions
 // with the same contraction scopes), so the two layouts agree (tests/test_race_gpu.py
-// test_quad_matches_lane).
+// test_quad_matches_lane).  Real = double is the reference-precision kernel: float64 physics and
+// MellingerControl wrapper (numpy's divisions), float firmware, as in the one-lane fp64 kernel;
+// cross-lane moves of doubles are two 32-bit DPP / swizzle moves.
 #pragma once
 
 #include "race_kernel.h"
@@ -39,8 +41,15 @@ __device__ __forceinline__ int qbc_i(int v, int k) {
     }
 }
 __device__ __forceinline__ float qbc(float v, int k) { return __int_as_float(qbc_i(__float_as_int(v), k)); }
+__device__ __forceinline__ double qbc(double v, int k) {
+    return __hiloint2double(qbc_i(__double2hiint(v), k), qbc_i(__double2loint(v), k));
+}
 __device__ __forceinline__ float qmirror(float v) {   // quad_perm [3, 2, 1, 0]
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x1b, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double qmirror(double v) {
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x1b, 0xf, 0xf, false),
+                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x1b, 0xf, 0xf, false));
 }
 
 // value of drone k of this lane's env (its quad lane ql): the env's G quads are 4G <= 32 aligned
@@ -66,41 +75,50 @@ __device__ __forceinline__ int grpq_i(int v, int k) {
 }
 template <int G>
 __device__ __forceinline__ float grpq(float v, int k) { return __int_as_float(grpq_i<G>(__float_as_int(v), k)); }
+template <int G>
+__device__ __forceinline__ double grpq(double v, int k) {
+    return __hiloint2double(grpq_i<G>(__double2hiint(v), k), grpq_i<G>(__double2loint(v), k));
+}
 
 // this lane's controller Euler angle (axis a = min(ql, 2)) of euler_xyz_fast_u(q): the same
 // atan2 / asin expressions, one per lane; the rare gimbal-lock branch evaluates all three
-__device__ __forceinline__ float euler_axis_q4(Q4<float> q, int a) {
-    const float sarg = -2.0f * (q.x * q.z - q.w * q.y);
-    if (__builtin_expect(__any(fabs_(sarg) >= 0.99999f), 0)) {
-        const V3<float> r = euler_xyz_fast(q);
+template <typename Real>
+__device__ __forceinline__ Real euler_axis_q4(Q4<Real> q, int a) {
+    const Real sarg = Real(-2) * (q.x * q.z - q.w * q.y);
+    if (__builtin_expect(__any(fabs_(sarg) >= Real(0.99999)), 0)) {
+        const V3<Real> r = euler_xyz_fast(q);
         return a == 0 ? r.x : (a == 1 ? r.y : r.z);
     }
-    const float sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
-    const float y0 = 2.0f * (q.y * q.z + q.w * q.x), x0 = squ - sqx - sqy + sqz;
-    const float y2 = 2.0f * (q.x * q.y + q.w * q.z), x2 = squ + sqx - sqy - sqz;
-    const float x1 = __builtin_amdgcn_sqrtf((1.0f - sarg) * (1.0f + sarg));   // fasin_(sarg)
-    const float yy = a == 0 ? y0 : (a == 1 ? sarg : y2), xx = a == 0 ? x0 : (a == 1 ? x1 : x2);
+    const Real sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
+    const Real y0 = Real(2) * (q.y * q.z + q.w * q.x), x0 = squ - sqx - sqy + sqz;
+    const Real y2 = Real(2) * (q.x * q.y + q.w * q.z), x2 = squ + sqx - sqy - sqz;
+    const Real x1 = hsqrt_((Real(1) - sarg) * (Real(1) + sarg));   // fasin_(sarg)
+    const Real yy = a == 0 ? y0 : (a == 1 ? sarg : y2), xx = a == 0 ? x0 : (a == 1 ? x1 : x2);
     return fatan2_(yy, xx);
 }
 
 // MellingerControl.computeControl (154-262) for the quad: lane ql owns axis min(ql, 2) of the
 // rates / gyro filter (rpy_a, prv, l1, l2) and motor ql of the PWM chain (noise_m).  Same
-// arithmetic as mellinger_compute<float> (FP contraction off), split across the quad.
-__device__ __forceinline__ void mellinger_q4(RDrone<float>& d, const Lpf& lpf, const float sp[3], float xc_x,
-                                             float xc_y, float rpy_a, float& prv, float& l1, float& l2, float noise_m,
-                                             int ql, const M3<float>& Rq) {
+// arithmetic as mellinger_compute<Real> (FP contraction off; fp32: reciprocal multiplies, fp64:
+// numpy's divisions and the firmware's C float divisions), split across the quad.
+template <typename Real>
+__device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, const float sp[3], float xc_x,
+                                             float xc_y, Real rpy_a, Real& prv, float& l1, float& l2, Real noise_m,
+                                             int ql, const M3<Real>& Rq) {
 #pragma clang fp contract(off)
-    const float rate = (rpy_a - prv) * 500.0f;
+    constexpr bool F32 = sizeof(Real) == 4;
+    const Real rate = F32 ? (rpy_a - prv) * Real(500) : (rpy_a - prv) / Real(0.002);
     prv = rpy_a;
-    const float acc_z = (d.vel.z - d.prev_vel[2]) * float(500.0 / 9.8) + 1.0f;
+    const Real acc_z = F32 ? (d.vel.z - d.prev_vel[2]) * Real(500.0 / 9.8) + Real(1)
+                           : (d.vel.z - d.prev_vel[2]) / Real(0.002) / Real(9.8) + Real(1);
     d.prev_vel[0] = d.vel.x; d.prev_vel[1] = d.vel.y; d.prev_vel[2] = d.vel.z;
-    const float g_a = lpf_apply(lpf, l1, l2, float(rate * 57.29577951308232f));
+    const float g_a = lpf_apply(lpf, l1, l2, float(rate * Real(57.29577951308232)));
     const float gyro[3] = {qbc(g_a, 0), qbc(g_a, 1), qbc(g_a, 2)};
-    float pwm;
-    if (acc_z < -0.5f) d.tumble += 1; else d.tumble = 0;
+    Real pwm;
+    if (float(acc_z) < -0.5f) d.tumble += 1; else d.tumble = 0;
     if (d.tumble >= 30) {
         d.tick += 1;
-        pwm = 0.0f;
+        pwm = Real(0);
     } else {
         const int da = d.tick - d.last_att, dp = d.tick - d.last_pos, bit = d.tick - d.tick_base;
         const bool att_due = (da >= 2) | ((da == 1) & (((d.att_bits >> bit) & 1u) != 0));
@@ -109,42 +127,45 @@ __device__ __forceinline__ void mellinger_q4(RDrone<float>& d, const Lpf& lpf, c
         d.last_att = att_due ? d.tick : d.last_att;
         if (att_due) {
             float Rm[9];
-            const float sarg = -2.0f * (d.q.x * d.q.z - d.q.w * d.q.y);
-            Rm[0] = Rq.a00; Rm[1] = Rq.a01; Rm[2] = Rq.a02;
-            Rm[3] = Rq.a10; Rm[4] = Rq.a11; Rm[5] = Rq.a12;
-            Rm[6] = Rq.a20; Rm[7] = Rq.a21; Rm[8] = Rq.a22;
-            if (__builtin_expect(__any(!(fabs_(sarg) < 0.99999f)), 0)) {
-                if (!(fabs_(sarg) < 0.99999f)) {
-                    const V3<float> rpy = euler_xyz_fast(d.q);
+            const Real sarg = Real(-2) * (d.q.x * d.q.z - d.q.w * d.q.y);
+            Rm[0] = float(Rq.a00); Rm[1] = float(Rq.a01); Rm[2] = float(Rq.a02);
+            Rm[3] = float(Rq.a10); Rm[4] = float(Rq.a11); Rm[5] = float(Rq.a12);
+            Rm[6] = float(Rq.a20); Rm[7] = float(Rq.a21); Rm[8] = float(Rq.a22);
+            if (__builtin_expect(__any(!(fabs_(sarg) < Real(0.99999))), 0)) {
+                if (!(fabs_(sarg) < Real(0.99999))) {
+                    const V3<Real> rpy = euler_xyz_fast(d.q);
                     float sr, cr, sp_, cp, sy, cy;
-                    sincosf(rpy.x, &sr, &cr);
-                    sincosf(rpy.y, &sp_, &cp);
-                    sincosf(rpy.z, &sy, &cy);
+                    sincosf(float(rpy.x), &sr, &cr);
+                    sincosf(float(rpy.y), &sp_, &cp);
+                    sincosf(float(rpy.z), &sy, &cy);
                     Rm[0] = cy * cp; Rm[1] = cy * sp_ * sr - sy * cr; Rm[2] = cy * sp_ * cr + sy * sr;
                     Rm[3] = sy * cp; Rm[4] = sy * sp_ * sr + cy * cr; Rm[5] = sy * sp_ * cr - cy * sr;
                     Rm[6] = -sp_; Rm[7] = cp * sr; Rm[8] = cp * cr;
                 }
             }
-            const float pos[3] = {d.pos.x, d.pos.y, d.pos.z};
-            const float vel[3] = {d.vel.x, d.vel.y, d.vel.z};
+            const float pos[3] = {float(d.pos.x), float(d.pos.y), float(d.pos.z)};
+            const float vel[3] = {float(d.vel.x), float(d.vel.y), float(d.vel.z)};
 #ifndef ADRP_EXP_NOFW   // measurement-only switch (phase profile without the firmware)
-            mellinger_fw(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
+            mellinger_fw<Real, F32, false>(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
 #endif
         }
         d.tick += 1;
         // _compute_pwms (423-442), motor ql of [t-r+p+y, t-r-p-y, t+r-p+y, t+r+p-y]
-        const float r = d.ctl[0] / 2.0f, p = d.ctl[1] / 2.0f, y = d.ctl[2], th = d.ctl[3];
-        const float m = ((th + (ql < 2 ? -r : r)) + ((ql == 0 || ql == 3) ? p : -p)) + ((ql & 1) ? -y : y);
-        const float x = clampr_(m, 0.0f, 65535.0f) * float(60.0 / 65535);
-        const float volts = -0.0006239f * x * x + 0.088f * x;
-        pwm = minr_(volts * float(1.0 / 3), 1.0f) * 65535.0f;
+        const Real r = Real(d.ctl[0]) / Real(2), p = Real(d.ctl[1]) / Real(2), y = Real(d.ctl[2]), th = Real(d.ctl[3]);
+        const Real m = ((th + (ql < 2 ? -r : r)) + ((ql == 0 || ql == 3) ? p : -p)) + ((ql & 1) ? -y : y);
+        const Real x = F32 ? clampr_(m, Real(0), Real(65535)) * Real(60.0 / 65535)
+                           : clampr_(m, Real(0), Real(65535)) / Real(65535) * Real(60);
+        const Real volts = Real(-0.0006239) * x * x + Real(0.088) * x;
+        pwm = minr_(F32 ? volts * Real(1.0 / 3) : volts / Real(3), Real(1)) * Real(65535);
     }
     // clip -> thrust -> reorder [3,2,1,0] -> + noise -> _thr2pwm -> rpm (246-262)
-    const float rp = 0.2685f * clampr_(pwm, 20000.0f, 65535.0f) + 4070.3f;
-    const float thr = qmirror(3.16e-10f * rp * rp);
-    const float t = maxr_(thr + noise_m, 0.0f);
-    const float mp = clampr_((hsqrt_(t * float(1.0 / 3.16e-10)) - 4070.3f) * float(1.0 / 0.2685), 20000.0f, 65535.0f);
-    const float rnew = 0.2685f * mp + 4070.3f;
+    const Real rp = Real(0.2685) * clampr_(pwm, Real(20000), Real(65535)) + Real(4070.3);
+    const Real thr = qmirror(Real(3.16e-10) * rp * rp);
+    const Real t = maxr_(thr + noise_m, Real(0));
+    const Real mp = clampr_(F32 ? (hsqrt_(t * Real(1.0 / 3.16e-10)) - Real(4070.3)) * Real(1.0 / 0.2685)
+                                : (sqrt_(t / Real(1) / Real(3.16e-10)) - Real(4070.3)) / Real(0.2685),
+                            Real(20000), Real(65535));
+    const Real rnew = Real(0.2685) * mp + Real(4070.3);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         d.prev[k] = d.rpm[k];
@@ -153,10 +174,11 @@ __device__ __forceinline__ void mellinger_q4(RDrone<float>& d, const Lpf& lpf, c
 }
 
 // the block's LDS copy of its drones' env tracks, [field][drone] (owner lane l -> drone l / 4)
+template <typename Real>
 struct TrackSrcQ {
-    const float* lds;
+    const Real* lds;
     int qd;
-    __device__ __forceinline__ float operator()(int field) const { return lds[(field - RF_GATE) * kQuadDrones + qd]; }
+    __device__ __forceinline__ Real operator()(int field) const { return lds[(field - RF_GATE) * kQuadDrones + qd]; }
     __device__ __forceinline__ TrackSrcQ lane(int l, int, int, int) const { return TrackSrcQ{lds, l >> 2}; }
 };
 
@@ -168,11 +190,10 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {   // OR over the quad 
 
 // track_bounds with the track dealt over the quad: lane ql tests gate ql and obstacle ql (same
 // per-part arithmetic), the bit masks are OR-ed over the quad
-template <class TS>
-__device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const TS& T, const Shape<float>& ds,
-                                                float cut, float ccut, int ql, bool want_contact, uint32_t& gin,
+template <typename Real, class TS>
+__device__ __forceinline__ void track_bounds_q4(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds,
+                                                Real cut, Real ccut, int ql, bool want_contact, uint32_t& gin,
                                                 uint32_t& oin, uint32_t& amb, uint32_t& camb_all, bool& ccert) {
-    using Real = float;
     const Real tol = Real(1e-5);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
     const V3<Real> p = ds.c, ax = col2(ds.R);
@@ -250,8 +271,8 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<float>& C, const
     ccert = quad_or(ccert ? 1u : 0u) != 0;
 }
 
-template <typename T3>
-__device__ __forceinline__ float sel3(const T3& v, int a) { return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]); }
+template <typename T>
+__device__ __forceinline__ T sel3(const T (&v)[3], int a) { return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]); }
 
 // ---- auto-reset of a done drone by its quad ----
 // race_reset_lane's arithmetic (MultiRaceAviary.reset 127-167, _addObstacles 347-403, _drone_init
@@ -262,10 +283,11 @@ __device__ __forceinline__ float sel3(const T3& v, int a) { return a == 0 ? v[0]
 
 // this lane's own gate ql / obstacle ql, addressed like the track fields (the bounds pass and the
 // part shapes of lane ql only ask for gate ql and obstacle ql)
+template <typename Real>
 struct TrackOne {
-    float g[4], o[3];
+    Real g[4], o[3];
     int ql;
-    __device__ __forceinline__ float operator()(int field) const {
+    __device__ __forceinline__ Real operator()(int field) const {
         if (field < RF_OBST) {
             const int c = field - RF_GATE - 4 * ql;
             return c == 0 ? g[0] : c == 1 ? g[1] : c == 2 ? g[2] : g[3];
@@ -275,20 +297,20 @@ struct TrackOne {
     }
 };
 // the whole track in registers (field indices fold to constants in the unrolled obs-row loops)
+template <typename Real>
 struct TrackRegs {
-    float v[kTrackFields];
-    __device__ __forceinline__ float operator()(int field) const { return v[field - RF_GATE]; }
+    Real v[kTrackFields];
+    __device__ __forceinline__ Real operator()(int field) const { return v[field - RF_GATE]; }
 };
 
-template <int G>
-__device__ __forceinline__ void race_reset_q4(const RaceArgs<float>& a, const RaceConst<float>& C, int e, int dn, int ql,
+template <typename Real, int G>
+__device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const RaceConst<Real>& C, int e, int dn, int ql,
                                               bool active, size_t EN, size_t slot, int episode, float* obs_row) {
-    using Real = float;
     const bool owner = active && ql == 0;
     const uint64_t gid = uint64_t(a.env_offset + e);
     const uint32_t ep = uint32_t(episode);
     Real* f = a.f;
-    TrackOne own;
+    TrackOne<Real> own;
     own.ql = ql;
     {   // gate ql, obstacle ql of the next track
         const int g = ql;
@@ -317,7 +339,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<float>& a, const Ra
             for (int k = 0; k < 3; ++k) st(f, RF_OBST + 3 * o + k, EN, slot, own.o[k]);
         }
     }
-    TrackRegs T;
+    TrackRegs<Real> T;
 #pragma unroll
     for (int g = 0; g < ADRP_MAX_GATES; ++g)
 #pragma unroll
@@ -450,13 +472,15 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<float>& a, const Ra
 // Block = 64 lanes = 16 drones (kQuadDrones); one wave.  DRAWS: the disturbance draws of the
 // step's S <= kRacePreS sub-steps go through LDS (disturbances on); else none are needed, or (S
 // larger) each lane draws in the loop.
-template <int PH, int G, bool DRAWS>
-__global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
-    using Real = float;
+template <typename Real, int PH, int G, bool DRAWS>
+__global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
+    constexpr bool F32 = sizeof(Real) == 4;
     RACE_MARK(t0);
     const RaceConst<Real>& C = *a.c;
-    __shared__ float pre_draws[DRAWS ? kRacePreS * 7 * kQuadDrones : 1];   // [s][7][drone]
-    __shared__ float trk_lds[kTrackFields * kQuadDrones];                  // [field][drone]
+    // [s][7][drone]: fp32 the 3 force components and the 4 motor noises; fp64 the 3 force uniforms
+    // (exact in float; the force is formed in Real at use) and the 4 noises (float samples)
+    __shared__ float pre_draws[DRAWS ? kRacePreS * 7 * kQuadDrones : 1];
+    __shared__ Real trk_lds[kTrackFields * kQuadDrones];                   // [field][drone]
     __shared__ float4 rows4[kQuadDrones * kRaceMaxD / 4];
     __shared__ TrackJobs tjobs;
     const int tl = threadIdx.x;
@@ -496,11 +520,11 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
     uint32_t att0, pos0;
     tick_window(a.ticks, tick0, att0, pos0);
     // the env's actual track: 7 of its 28 fields per lane, into LDS after the loop
-    float trk[(kTrackFields + 3) / 4];
+    Real trk[(kTrackFields + 3) / 4];
 #pragma unroll
     for (int i = 0; i < (kTrackFields + 3) / 4; ++i) {
         const int k = ql + 4 * i;
-        trk[i] = k < kTrackFields ? ld(a.f, RF_GATE + k, EN, slot) : 0.0f;
+        trk[i] = k < kTrackFields ? ld(a.f, RF_GATE + k, EN, slot) : Real(0);
     }
     RDrone<Real> d;
     load_drone<Real, false>(a, EN, slot, d);
@@ -522,18 +546,34 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
     const Lpf lpf = {C.lpf[0], C.lpf[1], C.lpf[2], C.lpf[3], C.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
     if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
         for (int s = ql; s < H.S; s += 4) {
-            Real fd[3], nz[4];
-            race_substep_draws(H, a.seed, gid, ep, dn, uint32_t(sc0 + s), fd, nz);
             float* dst = pre_draws + s * 7 * kQuadDrones + qd;
+            if constexpr (F32) {
+                Real fd[3], nz[4];
+                race_substep_draws(H, a.seed, gid, ep, dn, uint32_t(sc0 + s), fd, nz);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) dst[k * kQuadDrones] = fd[k];
+                for (int k = 0; k < 3; ++k) dst[k * kQuadDrones] = fd[k];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) dst[(3 + k) * kQuadDrones] = nz[k];
+                for (int k = 0; k < 4; ++k) dst[(3 + k) * kQuadDrones] = nz[k];
+            } else {
+                const U4 u = draw(a.seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), uint32_t(sc0 + s));
+                dst[0] = u01r<float>(u.a); dst[kQuadDrones] = u01r<float>(u.b); dst[2 * kQuadDrones] = u01r<float>(u.c);
+                const U4 v = draw(a.seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), uint32_t(sc0 + s));
+                const uint32_t x[4] = {v.a, v.b, v.c, v.d};
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {   // race_noise_draws' float samples (before the std scale)
+                    const float u1 = (float(x[2 * p] >> 8) + 1.0f) * float(1.0 / 16777216.0);
+                    const float u2 = float(x[2 * p + 1] >> 8) * float(1.0 / 16777216.0);
+                    const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+                    dst[(3 + 2 * p) * kQuadDrones] = r * __builtin_amdgcn_cosf(u2);
+                    dst[(4 + 2 * p) * kQuadDrones] = r * __builtin_amdgcn_sinf(u2);
+                }
+            }
         }
         __syncthreads();
     }
     // lane-distributed controller state: axis cax of the rate history and the gyro filter
-    float prv = sel3(d.prev_rpy, cax), l1 = sel3(d.lpf1, cax), l2 = sel3(d.lpf2, cax);
+    Real prv = sel3(d.prev_rpy, cax);
+    float l1 = sel3(d.lpf1, cax), l2 = sel3(d.lpf2, cax);
     M3<Real> Rq = rot(d.q), Rl = rot(d.ql);
     RACE_MARK(t1);
 #ifdef ADRP_RACE_TIMING
@@ -551,7 +591,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
 #endif
         const uint32_t idx = uint32_t(sc0 + s);
         if (PH != ADRP_PHYS_PYB) d.kpos = d.pos;
-        float noise_m = 0.0f;
+        Real noise_m = Real(0);
         if constexpr (PH == ADRP_PHYS_DYN) {
             race_dyn_substep(H, d);
             Rq = rot(d.q);
@@ -560,7 +600,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
             if constexpr (PH == ADRP_PHYS_PYB_DW || PH == ADRP_PHYS_PYB_GND_DRAG_DW) {
                 // _downwash (BaseAviary.py:792-818): lane ql evaluates partner drones ql, ql + 4;
                 // the sum runs in partner order with the one-lane loop's fused update
-                float al[(G + 3) / 4], ex[(G + 3) / 4];
+                Real al[(G + 3) / 4], ex[(G + 3) / 4];
 #pragma unroll
                 for (int j = 0; j < (G + 3) / 4; ++j) {
                     const int k = ql + 4 * j;
@@ -568,8 +608,8 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
                     const Real ox = __shfl(d.pos.x, src), oy = __shfl(d.pos.y, src), oz = __shfl(d.pos.z, src);
                     const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
                     const Real dxy = hsqrt_(dx * dx + dy * dy);
-                    al[j] = 0.0f;
-                    ex[j] = 0.0f;
+                    al[j] = Real(0);
+                    ex[j] = Real(0);
                     if (k < N && dz > Real(0) && dxy < Real(10)) {
                         const Real kk = H.prop_r * rcp_(Real(4) * dz);
                         al[j] = H.dw1 * kk * kk;
@@ -588,8 +628,15 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
                 V3<Real> fd;
                 if constexpr (DRAWS) {
                     const float* src = pre_draws + s * 7 * kQuadDrones + qd;
-                    fd = v3(src[0], src[kQuadDrones], src[2 * kQuadDrones]);
-                    noise_m = src[(3 + ql) * kQuadDrones];
+                    if constexpr (F32) {
+                        fd = v3(src[0], src[kQuadDrones], src[2 * kQuadDrones]);
+                        noise_m = src[(3 + ql) * kQuadDrones];
+                    } else {   // race_substep_draws' arithmetic on the stored uniforms / samples
+                        fd = v3(H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * Real(src[0]),
+                                H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * Real(src[kQuadDrones]),
+                                H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * Real(src[2 * kQuadDrones]));
+                        noise_m = Real(src[(3 + ql) * kQuadDrones]) * H.noise_std;
+                    }
                 } else {
                     Real f3[3], nz[4];
                     race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, nz);
@@ -631,7 +678,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
         if (k < kTrackFields) trk_lds[k * kQuadDrones + qd] = trk[i];
     }
     __syncthreads();
-    const TrackSrcQ T{trk_lds, qd};
+    const TrackSrcQ<Real> T{trk_lds, qd};
     // ---- _gate_progress (471-506) ----
     V3<Real> gpos[ADRP_MAX_DRONES];
     Q4<Real> gq[ADRP_MAX_DRONES];
@@ -687,7 +734,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
     uint32_t amb, camb_all;
     bool ccert;
     track_bounds_q4(C, T, ds, Real(0.45), Real(1e-6), ql, !(d.flags & 1), gin, oin, amb, camb_all, ccert);
-    bool crashed = track_gjk_pool<Real, TrackSrcQ, 2>(C, T, ds, owner, Real(0.45), Real(1e-6), gin, oin, amb, camb_all,
+    bool crashed = track_gjk_pool<Real, TrackSrcQ<Real>, 2>(C, T, ds, owner, Real(0.45), Real(1e-6), gin, oin, amb, camb_all,
                                                      tjobs, tl, G, N, a.E) || ccert;
     V3<Real> rpy;
     race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, owner, row0, gin, oin, &rpy);
@@ -788,7 +835,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<float> a) {
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
         }
     }
-    if (reset) race_reset_q4<G>(a, C, e, dn, ql, active, EN, slot, episode, row);
+    if (reset) race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, row);
 #ifdef ADRP_RACE_TIMING
     RACE_MARK(t6);   // tail: reward, flags, stores and the auto-reset of done envs
     if (threadIdx.x == 0) {

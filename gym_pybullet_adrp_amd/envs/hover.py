@@ -17,6 +17,7 @@ from .. import _lib
 from ..utils import abi
 from ..utils.enums import ActionType, DroneModel, ObservationType, Physics, PHYSICS_CODE
 from ..utils.spaces import Box
+from .base import AviaryEnv
 
 
 # ActionType -> C-ABI code, and the per-drone action width (BaseRLAviary.py:141-147).  PID /
@@ -28,7 +29,7 @@ _ACT_SIZE = {ActionType.RPM: 4, ActionType.VEL: 4, ActionType.PID: 3, ActionType
              ActionType.ONE_D_PID: 1}
 
 
-class HoverAviary:
+class HoverAviary(AviaryEnv):
     """Batched counterpart of gym_pybullet_adrp.envs.HoverAviary."""
 
     def __init__(self, drone_model: DroneModel = DroneModel.CF2X, initial_xyzs=None, initial_rpys=None,
@@ -167,3 +168,8 @@ class HoverAviary:
 
     def step_bytes(self):
         return self.h.step_bytes()
+
+    @property
+    def kernel_name(self):
+        """the step-kernel instantiation this env launches now (include/adrp.h adrp_handle_kernel_name)"""
+        return self.h.kernel_name()

@@ -21,6 +21,7 @@ from .. import _lib
 from ..utils import abi
 from ..utils.enums import ActionType, DroneModel, ObservationType, Physics, PHYSICS_CODE, RaceMode
 from ..utils.spaces import Box
+from .base import AviaryEnv
 from .tracks import fill_track
 
 
@@ -39,7 +40,7 @@ def race_config(race_config="level0", num_drones=2, physics="PYB", racemode="COM
     return cfg
 
 
-class MultiRaceAviary:
+class MultiRaceAviary(AviaryEnv):
     """Batched counterpart of gym_pybullet_adrp.envs.MultiRaceAviary."""
 
     def __init__(self, race_config="level0", drone_model: DroneModel = DroneModel.CF2X, num_drones: int = 2,
@@ -96,6 +97,7 @@ class MultiRaceAviary:
         self._trunc = torch.zeros(E, dtype=torch.bool, device=self.device)
         self._act_shape = (E, N, 4)
         self._info = {"answer": 42, "terminal_observation": self._tobs}
+        self._last_act = None      # the last ndarray (FULLSTATE) action tensor, by reference
         self.commands = False
         if commands:
             self.enable_commands()
@@ -129,16 +131,40 @@ class MultiRaceAviary:
                 raise ValueError("reset(seed=...) re-keys every env: call it without a mask")
             self.h.reseed(seed)
         self.h.reset(self._obs, m)
+        if m is None:
+            self._last_act = None
         return self._obs, {"answer": 42}
 
     def enable_commands(self):
         """High-level command mode (include/adrp.h adrp_enable_commands): step() then also takes
         (Command, args) tuples, run through the firmware's high-level commander (commands.py).
-        Enabled implicitly by the first tuple action; exact for envs that have not stepped since
-        their reset (the reference's controllers start from the initial obs)."""
+        Enabled implicitly by the first tuple action.  The command state starts as a reset leaves
+        it; drones that have stepped since their reset then get the FULLSTATE command their last
+        ndarray step sent (MultiRaceAviary.py:190-202: (act[:3], 0, 0, act[3], 0, step_counter);
+        eliminated drones STOP), so a drone given Command.NONE keeps flying to that target as in
+        the reference.  The last action tensor is read again here (kept by reference, as
+        BaseRLAviary keeps the caller's array): do not overwrite it between that step and this
+        call.  From here on the steps run the command-mode kernel (one lane per drone)."""
         if not self.commands:
             self.h.enable_commands()
             self.commands = True
+            if self._last_act is not None:
+                self._resend_fullstate(self._last_act)
+
+    def _resend_fullstate(self, act):
+        from ..commands import CMD_ARGS, COMMAND_CODE, TIME_SLOT
+        from ..utils.enums import Command
+        E, N = self.num_envs, self.NUM_DRONES
+        _, i = self.h.get_state()
+        sc = i[self.h.field_names()[1].index("step_counter")].reshape(E, N)
+        stepped = sc > 0                     # envs reset since (auto-reset) keep the reset state
+        codes = torch.where(stepped, COMMAND_CODE[Command.FULLSTATE], COMMAND_CODE[Command.NONE]).to(torch.int32)
+        args = torch.zeros((E, N, CMD_ARGS), dtype=torch.float64, device=self.device)
+        a = act.reshape(E, N, 4).to(torch.float64)
+        args[..., 0:3] = a[..., 0:3]
+        args[..., 9] = a[..., 3]            # the kernel zeroes it under the DroneObservationWrapper
+        args[..., TIME_SLOT] = (sc - self.PYB_STEPS_PER_CTRL).to(torch.float64)   # the step_counter it was sent at
+        self.h.command(codes, args)
 
     def command(self, actions):
         """Send one (Command, args) per drone without stepping: a list per env of N tuples (the
@@ -164,6 +190,7 @@ class MultiRaceAviary:
             act = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(self._act_shape)
             act = act.contiguous()
         self.h.step(act, self._obs, self._rew, self._term, self._trunc, self._tobs)
+        self._last_act = act
         return self._obs, self._rew, self._term, self._trunc, self._info
 
     def close(self):
@@ -211,6 +238,11 @@ class MultiRaceAviary:
 
     def step_bytes(self):
         return self.h.step_bytes()
+
+    @property
+    def kernel_name(self):
+        """the step-kernel instantiation this env launches now (include/adrp.h adrp_handle_kernel_name)"""
+        return self.h.kernel_name()
 
     def get_command_state(self):
         return self.h.get_command_state()

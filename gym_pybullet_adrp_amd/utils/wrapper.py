@@ -10,6 +10,11 @@ wrapper of one) and switch the matching stage of the fused step on (``adrp_set_w
 * RewardWrapper (wrapper.py:68-186): gate-progress reward of drone 0 (``info["task_completed"]``,
   absent in the reference, := every drone finished).
 
+Unlike a gymnasium wrapper these switch a stage of the BASE env's fused step: from construction on
+the unwrapped env (and every other stack over it) steps with yaw 0 / the early termination / the
+gate reward too.  ``detach()`` restores the base env's previous wrapper flags (the wrapper object
+must not be stepped afterwards).
+
 Stacking order matters as in the reference: ``RewardWrapper(DroneObservationWrapper(env))`` gives
 the reward's terminal terms the early termination, ``DroneObservationWrapper(RewardWrapper(env))``
 does not.  Everything else is delegated to the wrapped env (gymnasium 0.28 ``Wrapper`` semantics:
@@ -20,6 +25,12 @@ public attributes forward).
 class _Wrapper:
     def __init__(self, env):
         self.env = env
+        base = self.unwrapped
+        self._saved = (base.reward_wrapper, base.obs_wrapper)   # flags before this wrapper
+
+    def detach(self):
+        """switch the base env's fused stage back to what it was before this wrapper"""
+        self.unwrapped.set_wrappers(*self._saved)
 
     def __getattr__(self, name):
         if name.startswith("_") or name == "env":

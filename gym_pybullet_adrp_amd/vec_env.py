@@ -15,9 +15,23 @@ Outputs are numpy (what SB3's rollout buffer consumes) unless ``as_torch=True``,
 returns the device tensors untouched (for torch-native learners).  When
 stable_baselines3 is importable the class derives from its ``VecEnv`` so
 ``isinstance`` checks in SB3 pass; otherwise it is a plain class with the same methods.
+
+Host path (SURVEY.md §7 hard part 7).  The env writes obs / reward / terminated / truncated
+into ONE packed device buffer (``bind_outputs``); ``step_wait`` issues one asynchronous copy of
+it into pinned host memory and waits once; the actions go the other way through a pinned
+staging buffer (one asynchronous copy).  Terminal observations are fetched only for the envs
+that finished (a second small copy, only then).  ``infos`` is built lazily: the envs that
+finished get their own dict, every other entry is one shared read-only empty mapping (SB3
+reads infos and copies the dicts it annotates; writing into a shared entry raises).  Returned
+arrays are fresh copies (DummyVecEnv semantics) unless ``zero_copy=True``: then they are views
+of a ring of ``ring`` pinned buffers, valid until ``ring`` more steps have been taken.
 """
+import types
+
 import numpy as np
 import torch
+
+_NO_INFO = types.MappingProxyType({})
 
 try:  # pragma: no cover - SB3 is not part of this image
     from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _VecEnvBase
@@ -28,17 +42,47 @@ except ImportError:  # pragma: no cover
 class AviaryVecEnv(_VecEnvBase):
     """SB3 VecEnv over one batched aviary (HoverAviary / MultiRaceAviary of this package)."""
 
-    def __init__(self, env, as_torch=False):
+    def __init__(self, env, as_torch=False, zero_copy=False, ring=2, packed=None):
         self.env = env
         self.num_envs = env.num_envs
         self.observation_space = env.observation_space
         self.action_space = env.action_space
         self.render_mode = None
         self.as_torch = as_torch
+        self.zero_copy = zero_copy
         self._actions = None
         self._seed = None
+        # packed host path: numpy outputs of an env that can write into caller buffers (None: auto)
+        self._packed = (not as_torch) and hasattr(env, "bind_outputs") and packed is not False
+        if self._packed:
+            self._bind_packed(max(1, int(ring)))
         if _VecEnvBase is not object:  # pragma: no cover
             _VecEnvBase.__init__(self, self.num_envs, self.observation_space, self.action_space)
+
+    def _bind_packed(self, ring):
+        env, E = self.env, self.num_envs
+        obs_shape = tuple(env._obs.shape)
+        dev = env._obs.device
+        nobs = int(np.prod(obs_shape)) * 4
+        self._off = (nobs, nobs + 4 * E, nobs + 5 * E)
+        self._nbytes = (nobs + 6 * E + 15) // 16 * 16
+        self._dev = torch.zeros(self._nbytes, dtype=torch.uint8, device=dev)
+        o_rew, o_term, o_trunc = self._off
+        d = self._dev
+        env.bind_outputs(d[:nobs].view(torch.float32).view(obs_shape), d[o_rew:o_term].view(torch.float32),
+                         d[o_term:o_trunc].view(torch.bool), d[o_trunc:o_trunc + E].view(torch.bool))
+        pin = dev.type == "cuda"
+        self._host = [torch.zeros(self._nbytes, dtype=torch.uint8, pin_memory=pin) for _ in range(ring)]
+        self._slot = 0
+        self._views = []
+        for h in self._host:
+            hn = h.numpy()
+            self._views.append((hn[:nobs].view(np.float32).reshape(obs_shape), hn[o_rew:o_term].view(np.float32),
+                                hn[o_term:o_trunc].view(np.bool_), hn[o_trunc:o_trunc + E].view(np.bool_)))
+        act_shape = tuple(getattr(env, "_act_shape", (E,) + tuple(self.action_space.shape)))
+        self._act_host = torch.zeros(act_shape, dtype=torch.float32, pin_memory=pin)
+        self._act_dev = torch.zeros(act_shape, dtype=torch.float32, device=dev)
+        self._event = torch.cuda.Event() if pin else None
 
     # ---- conversion ----
     def _out(self, x):
@@ -48,12 +92,50 @@ class AviaryVecEnv(_VecEnvBase):
     def reset(self):
         seed, self._seed = self._seed, None
         obs, _ = self.env.reset(seed=seed)
+        if self._packed:
+            o = self._copy_out()[0]
+            return o if self.zero_copy else o.copy()
         return self._out(obs).copy() if not self.as_torch else obs.clone()
 
     def step_async(self, actions):
         self._actions = actions
 
+    def _copy_out(self):
+        """one async device -> pinned copy of the packed outputs, one wait"""
+        self._slot = (self._slot + 1) % len(self._host)
+        h = self._host[self._slot]
+        h.copy_(self._dev, non_blocking=True)
+        if self._event is not None:
+            self._event.record()
+            self._event.synchronize()
+        return self._views[self._slot]
+
+    def _act_in(self, actions):
+        """numpy / host actions -> the persistent device action buffer through pinned staging"""
+        if isinstance(actions, torch.Tensor) and actions.device == self._act_dev.device:
+            return actions
+        self._act_host.numpy()[...] = np.asarray(actions, np.float32).reshape(self._act_host.shape)
+        self._act_dev.copy_(self._act_host, non_blocking=True)
+        return self._act_dev
+
+    def _step_wait_packed(self):
+        _, _, _, _, info = self.env.step(self._act_in(self._actions))
+        obs, rew, term, trunc = self._copy_out()
+        done = term | trunc
+        idx = np.flatnonzero(done)
+        infos = [_NO_INFO] * self.num_envs
+        if len(idx):
+            tobs = info["terminal_observation"].index_select(
+                0, torch.from_numpy(idx).to(self._dev.device, non_blocking=True)).cpu().numpy()
+            for j, e in enumerate(idx):
+                infos[e] = {"terminal_observation": tobs[j], "TimeLimit.truncated": bool(trunc[e] and not term[e])}
+        if not self.zero_copy:
+            obs, rew = obs.copy(), rew.copy()
+        return obs, rew, done, infos
+
     def step_wait(self):
+        if self._packed:
+            return self._step_wait_packed()
         obs, rew, term, trunc, info = self.env.step(self._actions)
         done = term | trunc
         if self.as_torch:
@@ -111,12 +193,12 @@ class AviaryVecEnv(_VecEnvBase):
         return list(indices)
 
 
-def HoverAviaryVec(n_envs=1, as_torch=False, **env_kwargs):
+def HoverAviaryVec(n_envs=1, as_torch=False, zero_copy=False, **env_kwargs):
     """``make_vec_env(HoverAviary, env_kwargs=..., n_envs=...)`` counterpart"""
     from .envs.hover import HoverAviary
-    return AviaryVecEnv(HoverAviary(num_envs=n_envs, **env_kwargs), as_torch=as_torch)
+    return AviaryVecEnv(HoverAviary(num_envs=n_envs, **env_kwargs), as_torch=as_torch, zero_copy=zero_copy)
 
 
-def MultiRaceAviaryVec(n_envs=1, as_torch=False, **env_kwargs):
+def MultiRaceAviaryVec(n_envs=1, as_torch=False, zero_copy=False, **env_kwargs):
     from .envs.race import MultiRaceAviary
-    return AviaryVecEnv(MultiRaceAviary(num_envs=n_envs, **env_kwargs), as_torch=as_torch)
+    return AviaryVecEnv(MultiRaceAviary(num_envs=n_envs, **env_kwargs), as_torch=as_torch, zero_copy=zero_copy)

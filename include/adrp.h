@@ -258,6 +258,9 @@ int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev, void* str
  * reference default drone at 240/30 Hz, chosen only when the config's derived constants
  * are bit-identical), "generic" = read from the handle's device-resident block. */
 const char* adrp_kernel_name(const adrp_config* cfg);
+/* the instantiation this handle launches now (after adrp_enable_commands a race handle runs the
+   command-mode kernel, "...,CMD>"; ADRP_RACE_QUAD as read at create) */
+const char* adrp_handle_kernel_name(const adrp_t* h);
 
 /* Algorithmic HBM bytes one adrp_step moves (roofline accounting). */
 int64_t adrp_step_bytes(const adrp_t* h);

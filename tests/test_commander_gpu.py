@@ -150,3 +150,49 @@ def test_enable_commands_matches_reset_state():
     np.testing.assert_allclose(fb, fo, atol=1e-6)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("obs_wrapper", [0, 1])
+def test_commands_after_ndarray_steps(obs_wrapper):
+    """commands enabled implicitly mid-episode.  After ndarray (FULLSTATE) steps the
+    reference's controllers hold the last FULLSTATE setpoint (override on), so a drone given
+    Command.NONE keeps flying to it while another gets a GOTO; the enabled command state must match
+    the oracle's (which runs the command path on every step) and so must the next steps."""
+    from gym_pybullet_adrp_amd.utils.wrapper import DroneObservationWrapper
+    E, N = 32, 2
+    env = MultiRaceAviary("level0", num_drones=N, num_envs=E, seed=5, autoreset=False)
+    wenv = DroneObservationWrapper(env) if obs_wrapper else env
+    orc = O.Oracle(env.cfg.copy())
+    wenv.reset()
+    obs0 = orc.reset()
+    rng = np.random.default_rng(3)
+    tgt = np.concatenate([obs0[..., :3] + rng.uniform(-0.3, 0.3, (E, N, 3)) + [0, 0, 0.5],
+                          rng.uniform(-1, 1, (E, N, 1))], -1).astype(np.float32)
+    at = torch.from_numpy(tgt).to(env.device)
+    for _ in range(4):
+        orc.step(tgt)
+        wenv.step(at)
+        sync(env, orc)
+    assert not env.commands and env.kernel_name.endswith(",Q4>")
+    cmds = [[(Command.NONE, []), (Command.GOTO, [obs0[e, 1, :3] + [0.2, 0.0, 0.6], 0.3, 1.0, False])]
+            for e in range(E)]
+    codes, args = encode_commands(cmds, E, N)
+    orc.command(codes, args)
+    obs_o, *_ = orc.step(None)
+    obs_g, *_ = wenv.step(cmds)            # implicit enable: re-sends the last FULLSTATE, then the commands
+    assert env.commands and env.kernel_name == "race_step<f32,PYB,G8,CMD>"
+    check_cmd(env, orc, 2e-3)
+    check_state(env, orc, 2e-3)
+    for _ in range(3):
+        sync(env, orc)
+        sync_cmd(env, orc)
+        none = [[(Command.NONE, [])] * N] * E
+        orc.command(*encode_commands(none, E, N))
+        orc.step(None)
+        wenv.step(none)
+        check_cmd(env, orc, 2e-3)
+        check_state(env, orc, 2e-3)
+    if obs_wrapper:
+        wenv.detach()
+        assert env.obs_wrapper == 0
+    env.close()

@@ -123,6 +123,20 @@ def check_state(env, orc, rtol=1e-4):
     return worst
 
 
+def plane_contact(fo, names):
+    """drones on which the documented plane contact model (DESIGN.md §6 deviation 1: lowest point of
+    the collision cylinder kept at z >= 0, inward velocity zeroed) acted in this sub-step on either
+    side: the oracle's post-step lowest point within 1 um of the plane (it is projected to exactly 0
+    when the model acts).  The north star excludes contact sub-steps from the 1e-4 statistic and
+    counts them separately."""
+    idx = {n: k for k, n in enumerate(names)}
+    x, y, z, w = (fo[idx[f"quat_{a}"]] for a in "xyzw")
+    r22 = 1 - 2 * (x * x + y * y)
+    r02, r12 = 2 * (x * z + y * w), 2 * (y * z - x * w)
+    low = fo[idx["pos_z"]] - 0.0125 * np.abs(r22) - 0.06 * np.sqrt(r02 * r02 + r12 * r12)
+    return low < 1e-6
+
+
 def range_flags_ok(cfg, obs_g, obs_o, f):
     """in-range flags may differ only within 1e-4 m of the 0.45 m range"""
     E, N = obs_o.shape[:2]
@@ -225,7 +239,9 @@ def test_physics_substep_identical_rpm_config4_size(physics):
     action noise on; also PYB_GND_DRAG_DW): one 500 Hz sub-step per env.step.  The GPU flies 0.4 s,
     then EVERY drone is teacher-forced against the (OpenMP) oracle from the identical state for 4
     sub-steps: pos / quat / vel / omega within the north-star 1e-4 bar (the physics consumes the
-    synced RPMs and the same Philox disturbance draws)."""
+    synced RPMs and the same Philox disturbance draws).  Sub-steps in which the plane contact model
+    acts (eliminated drones sliding along the ground; float rounding decides a grazing touch) are
+    excluded and counted, as the north star prescribes: at most 1 % of the drone sub-steps."""
     import os
     E, N = 4096, 4
     rng = np.random.default_rng(41)
@@ -244,7 +260,7 @@ def test_physics_substep_identical_rpm_config4_size(physics):
     idx = {n: k for k, n in enumerate(names)}
     O.set_threads(min(16, os.cpu_count() or 1))
     try:
-        worst = {}
+        worst, contacts = {}, 0
         for k in range(4):
             orc.set_state(f, i)
             env.set_state(torch.from_numpy(f.astype(np.float32)), torch.from_numpy(i))
@@ -252,13 +268,18 @@ def test_physics_substep_identical_rpm_config4_size(physics):
             env.step(at)
             fg = env.get_state()[0].double().cpu().numpy()
             fo, io = orc.get_state()
+            free = ~plane_contact(fo, names)
+            contacts += int((~free).sum())
             for g in ("pos", "quat", "vel", "omega"):
                 rows = [idx[n] for n in GROUPS[g]]
                 err = np.linalg.norm(fg[rows] - fo[rows], axis=0) / np.maximum(np.linalg.norm(fo[rows], axis=0), FLOORS[g])
+                err = np.where(free, err, 0.0)
                 worst[g] = max(worst.get(g, 0.0), float(err.max()))
                 assert err.max() <= 1e-4, f"sub-step {k} {g}: {err.max():.3e} at drone slot {err.argmax()}"
             f, i = fo.astype(np.float32).astype(np.float64), io
-        print(physics, "worst relative error over 16,384 drones x 4 sub-steps:", worst)
+        assert contacts <= 0.01 * 4 * E * N, contacts
+        print(physics, "worst relative error over 16,384 drones x 4 sub-steps:", worst,
+              f"plane-contact sub-steps excluded: {contacts}")
     finally:
         O.set_threads(1)
     env.close()
@@ -485,13 +506,14 @@ def test_full_size_subset_vs_oracle(E, N, level, physics, mode):
     env.close()
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
 @pytest.mark.parametrize("level,N,physics,mode", [("level0", 2, Physics.PYB, RaceMode.COMPARE),
                                                   ("level3", 4, Physics.PYB_DW, RaceMode.COMPETE),
                                                   ("level2", 3, Physics.PYB_GND_DRAG_DW, RaceMode.COMPETE)])
-def test_quad_matches_lane(monkeypatch, level, N, physics, mode):
-    """the fp32 race step in its two layouts, four lanes per drone (default, race_quad.h) and one
-    (ADRP_RACE_QUAD=0), teacher-forced from the same states: the per-element arithmetic is the same,
-    so one env.step agrees to float rounding and every discrete output is identical"""
+def test_quad_matches_lane(monkeypatch, level, N, physics, mode, precision):
+    """the race step in its two layouts, four lanes per drone (default, race_quad.h) and one
+    (ADRP_RACE_QUAD=0), teacher-forced from the same states, in both precisions: the per-element
+    arithmetic is the same, so one env.step agrees to rounding and every discrete output is identical"""
     E = 256
     rng = np.random.default_rng(23)
     orc = None
@@ -499,7 +521,8 @@ def test_quad_matches_lane(monkeypatch, level, N, physics, mode):
     for quad in ("1", "0"):
         monkeypatch.setenv("ADRP_RACE_QUAD", quad)
         env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=3,
-                              autoreset=True, reward="wrapper")
+                              autoreset=True, reward="wrapper", precision=precision)
+        assert env.kernel_name.endswith(",Q4>") == (quad == "1")
         if orc is None:
             orc = O.Oracle(env.cfg.copy())
             obs0 = orc.reset()
@@ -507,7 +530,7 @@ def test_quad_matches_lane(monkeypatch, level, N, physics, mode):
             for _ in range(15):
                 orc.step(act)
             f, i = orc.get_state()
-            f = f.astype(np.float32)
+            f = f.astype(np.float32) if precision == "fp32" else f
         env.reset()
         env.set_state(torch.from_numpy(f), torch.from_numpy(i))
         o, r, te, tr, _ = env.step(torch.from_numpy(act).to(env.device))

@@ -32,3 +32,114 @@ def test_make_builds_the_batched_env():
     obs, _ = env.reset()
     assert tuple(obs.shape) == (16, 1, 72)
     env.close()
+
+
+# ---- gymnasium.make through a stub gymnasium (the real one is absent in this image) ----------
+STUB = '''
+class Env:
+    metadata = {"render_modes": []}
+    render_mode = None
+    spec = None
+    @property
+    def unwrapped(self):
+        return self
+
+class Wrapper(Env):
+    def __init__(self, env):
+        # gymnasium >= 0.26: Wrapper requires a gymnasium.Env
+        assert isinstance(env, Env), f"Expected env to be a `gymnasium.Env` but got {type(env)}"
+        self.env = env
+    def __getattr__(self, name):
+        return getattr(self.env, name)
+    @property
+    def unwrapped(self):
+        return self.env.unwrapped
+    def reset(self, **kw):
+        self._has_reset = True
+        return self.env.reset(**kw)
+    def step(self, a):
+        assert getattr(self, "_has_reset", False), "OrderEnforcing: reset first"
+        return self.env.step(a)
+'''
+REG = '''
+import importlib
+class EnvSpec:
+    def __init__(self, id, entry_point, kwargs):
+        self.id, self.entry_point, self.kwargs = id, entry_point, kwargs
+registry = {}
+def register(id, entry_point, disable_env_checker=False, **kw):
+    registry[id] = EnvSpec(id, entry_point, kw)
+def make(id, **kwargs):
+    from gymnasium import Wrapper
+    spec = registry[id]
+    mod, cls = spec.entry_point.split(":")
+    env = getattr(importlib.import_module(mod), cls)(**kwargs)
+    env.unwrapped.spec = spec          # gymnasium.make does this, then OrderEnforcing
+    return Wrapper(env)
+'''
+
+
+def _stub_gymnasium(tmp_path):
+    pkg = tmp_path / "gymnasium"
+    (pkg / "envs").mkdir(parents=True)
+    (pkg / "__init__.py").write_text(STUB + "from . import envs\n")
+    (pkg / "envs" / "__init__.py").write_text("from . import registration\n")
+    (pkg / "envs" / "registration.py").write_text(REG)
+    return str(tmp_path)
+
+
+def _run(tmp_path, body):
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([_stub_gymnasium(tmp_path), root]))
+    r = subprocess.run([sys.executable, "-c", body], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_gymnasium_surface_with_stub(tmp_path):
+    """with gymnasium importable, the ids register as the reference registers them and the env
+    classes are gymnasium.Env subclasses with its surface (spec settable, unwrapped, metadata,
+    render_mode), so gymnasium.make's spec assignment and OrderEnforcing wrapper accept them"""
+    out = _run(tmp_path, """
+import gymnasium
+import gym_pybullet_adrp_amd as pkg
+from gym_pybullet_adrp_amd.envs import HoverAviary, MultiRaceAviary
+from gymnasium.envs.registration import registry
+for i, entry in pkg.ENV_IDS.items():
+    assert registry[i].entry_point == entry
+for cls in (HoverAviary, MultiRaceAviary):
+    assert issubclass(cls, gymnasium.Env)
+    e = cls.__new__(cls)                      # the surface without a GPU handle
+    assert e.unwrapped is e and e.render_mode is None and isinstance(e.metadata, dict)
+    e.unwrapped.spec = registry['hover-aviary-v0']
+    assert e.spec.id == 'hover-aviary-v0'
+    w = gymnasium.Wrapper(e)
+    assert w.unwrapped is e
+print('ok')
+""")
+    assert out.strip().endswith("ok")
+
+
+@pytest.mark.gpu
+def test_gymnasium_make_with_stub(tmp_path):
+    out = _run(tmp_path, """
+import gymnasium, torch
+import gym_pybullet_adrp_amd  # registers
+from gymnasium.envs.registration import make
+env = make('multi-race-aviary-v0', race_config='level1', num_drones=2, num_envs=8)
+assert env.unwrapped.spec.id == 'multi-race-aviary-v0'
+obs, info = env.reset()
+assert tuple(obs.shape) == (8, 2, 49)
+o, r, te, tr, info = env.step(torch.cat([obs[..., :3], torch.zeros_like(obs[..., :1])], -1))
+assert tuple(r.shape) == (8,)
+env.close()
+env = make('hover-aviary-v0', num_envs=16)
+obs, _ = env.reset()
+env.step(torch.zeros((16, 1, 4), device=obs.device))
+env.close()
+print('ok')
+""")
+    assert out.strip().endswith("ok")

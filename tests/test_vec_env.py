@@ -18,44 +18,66 @@ class _Scripted:
         self.action_space = Box(low=-np.ones((1, 4)), high=np.ones((1, 4)), dtype=np.float32)
         self.tobs = torch.zeros((E, 1, D))
         self.closed = False
+        self._obs = torch.zeros((E, 1, D))
+        self._rew = torch.zeros(E)
+        self._term = torch.zeros(E, dtype=torch.bool)
+        self._trunc = torch.zeros(E, dtype=torch.bool)
+        self._act_shape = (E, 1, 4)
+        self.actions = []
+
+    def bind_outputs(self, obs, rew, term, trunc):      # the batched envs' contract
+        for old, new in ((self._obs, obs), (self._rew, rew), (self._term, term), (self._trunc, trunc)):
+            assert new.shape == old.shape and new.dtype == old.dtype and new.is_contiguous()
+        self._obs, self._rew, self._term, self._trunc = obs, rew, term, trunc
 
     def reset(self, seed=None):
-        return torch.zeros((self.num_envs, 1, self.D)), {}
+        self._obs.zero_()
+        return self._obs, {}
 
     def step(self, action):
+        self.actions.append(torch.as_tensor(action).clone())
         self.k += 1
         E = self.num_envs
-        obs = torch.full((E, 1, self.D), float(self.k))
-        rew = torch.arange(E, dtype=torch.float32) * self.k
-        term = torch.zeros(E, dtype=torch.bool)
-        trunc = torch.zeros(E, dtype=torch.bool)
+        self._obs.fill_(float(self.k))
+        self._rew.copy_(torch.arange(E, dtype=torch.float32) * self.k)
+        self._term.zero_()
+        self._trunc.zero_()
         if self.k == 2:
-            trunc[1] = True
+            self._trunc[1] = True
             self.tobs[1] = 100.0
-            obs[1] = -1.0
+            self._obs[1] = -1.0
         if self.k == 3:
-            term[2] = True
+            self._term[2] = True
             self.tobs[2] = 200.0
-        return obs, rew, term, trunc, {"answer": 42, "terminal_observation": self.tobs}
+        return self._obs, self._rew, self._term, self._trunc, {"answer": 42, "terminal_observation": self.tobs}
 
     def close(self):
         self.closed = True
 
 
-def test_vecenv_protocol_and_infos():
-    venv = AviaryVecEnv(_Scripted())
+@pytest.mark.parametrize("packed,zero_copy", [(False, False), (True, False), (True, True)])
+def test_vecenv_protocol_and_infos(packed, zero_copy):
+    venv = AviaryVecEnv(_Scripted(), packed=packed, zero_copy=zero_copy)
+    assert venv._packed == packed
     assert venv.num_envs == 4 and venv.observation_space.shape == (1, 5)
     obs = venv.reset()
     assert isinstance(obs, np.ndarray) and obs.shape == (4, 1, 5)
-    o, r, d, infos = venv.step(np.zeros((4, 1, 4), np.float32))
+    o, r, d, infos = venv.step(np.full((4, 1, 4), 0.5, np.float32))
     assert not d.any() and all(i == {} for i in infos)
+    np.testing.assert_array_equal(venv.env.actions[-1].cpu().numpy(), np.full((4, 1, 4), 0.5, np.float32))
+    if packed:
+        with pytest.raises(TypeError):        # the shared empty info of a running env is read-only
+            infos[0]["x"] = 1
     o, r, d, infos = venv.step(np.zeros((4, 1, 4), np.float32))
     np.testing.assert_array_equal(d, [False, True, False, False])
     assert infos[1]["TimeLimit.truncated"] is True
     np.testing.assert_array_equal(infos[1]["terminal_observation"], np.full((1, 5), 100.0))
     np.testing.assert_array_equal(o[1], np.full((1, 5), -1.0))     # already the reset observation
+    o_prev = o
     o, r, d, infos = venv.step(np.zeros((4, 1, 4), np.float32))
     assert d[2] and infos[2]["TimeLimit.truncated"] is False
+    np.testing.assert_array_equal(infos[2]["terminal_observation"], np.full((1, 5), 200.0))
+    np.testing.assert_array_equal(o_prev[1], np.full((1, 5), -1.0))  # ring of 2 / copies: still valid
     np.testing.assert_array_equal(r, np.arange(4) * 3.0)
     assert venv.get_attr("num_envs") == [4] * 4 and venv.env_is_wrapped(object) == [False] * 4
     venv.close()
@@ -86,3 +108,45 @@ def test_hover_and_race_vecenv_on_gpu():
     obs, rew, done, infos = r.step(act)
     assert obs.shape == (32, 2, 49) and len(infos) == 32
     r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["hover", "race"])
+def test_packed_host_path_matches_legacy(kind):
+    """the packed pinned-copy host path returns what the per-tensor .cpu() path returns: same obs,
+    rewards, dones, terminal observations and TimeLimit.truncated (same seed, same actions)"""
+    from gym_pybullet_adrp_amd.vec_env import HoverAviaryVec, MultiRaceAviaryVec
+    outs = []
+    for packed in (True, False):
+        if kind == "hover":
+            v = HoverAviaryVec(n_envs=256, seed=3, initial_xyzs=[0, 0, 1.0], init_noise={"rpy": 0.3, "omega": 1.0})
+        else:
+            v = MultiRaceAviaryVec(n_envs=128, race_config="level3", num_drones=4, seed=3)
+        v = type(v)(v.env, packed=packed)
+        assert v._packed == packed
+        obs = v.reset()
+        rng = np.random.default_rng(0)
+        seq = [obs.copy()]
+        for k in range(60):
+            if kind == "hover":
+                a = rng.uniform(-1, 1, (256, 1, 4)).astype(np.float32)
+            else:
+                a = np.concatenate([obs[..., :3] + rng.uniform(-2, 2, obs[..., :3].shape), np.zeros(obs.shape[:2] + (1,))],
+                                   -1).astype(np.float32)
+            obs, rew, done, infos = v.step(a)
+            seq.append((obs.copy(), rew.copy(), done.copy(),
+                        [(bool(i.get("TimeLimit.truncated")), i.get("terminal_observation")) for i in infos]))
+        outs.append(seq)
+        v.close()
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    ndone = 0
+    for (o1, r1, d1, i1), (o2, r2, d2, i2) in zip(outs[0][1:], outs[1][1:]):
+        np.testing.assert_array_equal(o1, o2)
+        np.testing.assert_array_equal(r1, r2)
+        np.testing.assert_array_equal(d1, d2)
+        ndone += int(d1.sum())
+        for (t1, x1), (t2, x2) in zip(i1, i2):
+            assert t1 == t2 and (x1 is None) == (x2 is None)
+            if x1 is not None:
+                np.testing.assert_array_equal(x1, x2)
+    assert ndone > 0
