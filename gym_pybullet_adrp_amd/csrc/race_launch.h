@@ -4,10 +4,12 @@
 #include "adrp_internal.h"
 
 // four lanes per drone (race_quad.h): 16 drones per 64-lane block
+// RH (auto-reset on, ADRP_RACE_RESET_HELPER != 0): a reset helper wave per block (128 threads)
 template <typename Real, int PH>
 static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
     const bool draws = h->cfg.track.disturbances && h->S <= kRacePreS;
-    const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G * 4 + kRaceBlock - 1) / kRaceBlock));
+    const bool rh = h->cfg.autoreset && h->race_reset_helper;
+    const dim3 blk(rh ? 2 * kRaceBlock : kRaceBlock), grid((unsigned)((size_t(h->E) * G * 4 + kRaceBlock - 1) / kRaceBlock));
     auto go = [&](auto kernel) {
         if (h->prof_n < h->prof_cap) {
             hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
@@ -16,19 +18,24 @@ static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t
             hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
         }
     };
-    auto by_g = [&](auto dr) {
-        constexpr bool D = decltype(dr)::value;
+    auto by_g = [&](auto dr, auto rr) {
+        constexpr bool D = decltype(dr)::value, R = decltype(rr)::value;
         switch (G) {
 #ifndef ADRP_DEV_FAST
-            case 1: go(race_step_q4<Real, PH, 1, D>); break;
-            case 8: go(race_step_q4<Real, PH, 8, D>); break;
+            case 1: go(race_step_q4<Real, PH, 1, D, R>); break;
+            case 8: go(race_step_q4<Real, PH, 8, D, R>); break;
 #endif
-            case 2: go(race_step_q4<Real, PH, 2, D>); break;
-            default: go(race_step_q4<Real, PH, 4, D>); break;
+            case 2: go(race_step_q4<Real, PH, 2, D, R>); break;
+            default: go(race_step_q4<Real, PH, 4, D, R>); break;
         }
     };
-    if (draws) by_g(std::true_type{});
-    else by_g(std::false_type{});
+    if (rh) {
+        if (draws) by_g(std::true_type{}, std::true_type{});
+        else by_g(std::false_type{}, std::true_type{});
+    } else {
+        if (draws) by_g(std::true_type{}, std::false_type{});
+        else by_g(std::false_type{}, std::false_type{});
+    }
 }
 
 // command mode: the lane kernel with the commander (commander.h), G = 8 lanes per env for every N
@@ -98,12 +105,10 @@ int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term
     a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
     const int G = race_group(h->N);
 #ifdef ADRP_DEV_FAST   // experiment build (make dev): the benched race instantiations only
-    if (sizeof(Real) != 4 || (h->cfg.physics != ADRP_PHYS_PYB && h->cfg.physics != ADRP_PHYS_PYB_DW) || (G != 2 && G != 4))
+    if ((h->cfg.physics != ADRP_PHYS_PYB && h->cfg.physics != ADRP_PHYS_PYB_DW) || (G != 2 && G != 4))
         return seterr(h, ADRP_ERR_INVALID, "dev build: race config not instantiated");
-    if constexpr (sizeof(Real) == 4) {
-        if (h->cfg.physics == ADRP_PHYS_PYB) race_step_ph<Real, ADRP_PHYS_PYB>(h, a, G, s);
-        else race_step_ph<Real, ADRP_PHYS_PYB_DW>(h, a, G, s);
-    }
+    if (h->cfg.physics == ADRP_PHYS_PYB) race_step_ph<Real, ADRP_PHYS_PYB>(h, a, G, s);
+    else race_step_ph<Real, ADRP_PHYS_PYB_DW>(h, a, G, s);
 #else
     switch (h->cfg.physics) {
         case ADRP_PHYS_PYB: race_step_ph<Real, ADRP_PHYS_PYB>(h, a, G, s); break;

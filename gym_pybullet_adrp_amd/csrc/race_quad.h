@@ -24,6 +24,8 @@
 // cross-lane moves of doubles are two 32-bit DPP / swizzle moves.
 #pragma once
 
+#include <type_traits>
+
 #include "race_kernel.h"
 
 namespace adrp {
@@ -303,13 +305,90 @@ struct TrackRegs {
     __device__ __forceinline__ Real operator()(int field) const { return v[field - RF_GATE]; }
 };
 
-template <typename Real, int G>
+// Where a reset's results go.  ResetToHBM: the drone slot's state in HBM (the chain wave resetting a
+// done env after its step).  ResetToLDS: a block's LDS staging (the reset helper wave computes every
+// drone's next episode during the sub-steps; reset_replay_q4 then writes the done ones out with the
+// same stores ResetToHBM makes).
+template <typename Real>
+struct ResetToHBM {
+    const RaceArgs<Real>* a;
+    __device__ __forceinline__ void track(bool active, size_t EN, size_t slot, int ql, const TrackOne<Real>& own) const {
+        if (!active) return;   // the quad stores the drone slot's replicated track, a gate and an obstacle per lane
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st(a->f, RF_GATE + 4 * ql + k, EN, slot, own.g[k]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) st(a->f, RF_OBST + 3 * ql + k, EN, slot, own.o[k]);
+    }
+    __device__ __forceinline__ void wrapper(size_t EN, size_t slot, const Real tgt[3], const Real prv[3]) const {
+        for (int k = 0; k < 3; ++k) {
+            st(a->f, RF_WR_TARGET + k, EN, slot, tgt[k]);
+            st(a->f, RF_WR_PREV + k, EN, slot, prv[k]);
+        }
+    }
+    __device__ __forceinline__ void drone(size_t EN, size_t slot, const RDrone<Real>& d, int episode) const {
+        store_drone(*a, EN, slot, d, true);
+        a->ist[RI_STEP * EN + slot] = 0;
+        a->ist[RI_EPISODE * EN + slot] = episode + 1;
+        a->ist[RI_WR_GATE * EN + slot] = 0;
+    }
+};
+
+// the values of a reset that are not constants, per drone of the block (qd), and the lanes' track parts
+constexpr int kRsDrone = 26;   // pos 3, q 4, vel 3, w 3, angv 3, prev_rpy 3, mass 1, inertia 3, kpos 3
+template <typename Real>
+struct ResetLds {
+    Real trk[7][kRaceBlock];                 // lane's gate ql (4) and obstacle ql (3)
+    Real drone[kRsDrone][kQuadDrones];
+    Real wr[6][kQuadDrones];
+};
+template <typename Real>
+struct ResetToLDS {
+    ResetLds<Real>* s;
+    int tl, qd;
+    __device__ __forceinline__ void track(bool, size_t, size_t, int, const TrackOne<Real>& own) const {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s->trk[k][tl] = own.g[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s->trk[4 + k][tl] = own.o[k];
+    }
+    __device__ __forceinline__ void wrapper(size_t, size_t, const Real tgt[3], const Real prv[3]) const {
+        for (int k = 0; k < 3; ++k) {
+            s->wr[k][qd] = tgt[k];
+            s->wr[3 + k][qd] = prv[k];
+        }
+    }
+    __device__ __forceinline__ void drone(size_t, size_t, const RDrone<Real>& d, int) const {
+        const Real v[kRsDrone] = {d.pos.x, d.pos.y, d.pos.z, d.q.x, d.q.y, d.q.z, d.q.w, d.vel.x, d.vel.y, d.vel.z,
+                                  d.w.x, d.w.y, d.w.z, d.angv.x, d.angv.y, d.angv.z, d.prev_rpy[0], d.prev_rpy[1],
+                                  d.prev_rpy[2], d.mass, d.inertia[0], d.inertia[1], d.inertia[2], d.kpos.x, d.kpos.y,
+                                  d.kpos.z};
+#pragma unroll
+        for (int k = 0; k < kRsDrone; ++k) s->drone[k][qd] = v[k];
+    }
+};
+
+// the reset state a race_reset_q4 leaves in an RDrone besides its non-constant values
+template <typename Real>
+__device__ __forceinline__ void reset_drone_constants(RDrone<Real>& d) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        d.prev_vel[k] = Real(0); d.lpf1[k] = d.lpf2[k] = 0.0f; d.ierr[k] = d.ierrm[k] = 0.0f;
+    }
+    d.tick = d.last_att = d.last_pos = d.tumble = 0;
+    d.pw_roll = d.pw_pitch = __builtin_nanf("");
+    d.psp_roll = d.psp_pitch = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d.ctl[k] = 0.0f; d.rpm[k] = d.prev[k] = Real(0); }
+    d.gate = 0; d.flags = 0;
+}
+
+template <typename Real, int G, class Sink>
 __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const RaceConst<Real>& C, int e, int dn, int ql,
-                                              bool active, size_t EN, size_t slot, int episode, float* obs_row) {
+                                              bool active, size_t EN, size_t slot, int episode, float* obs_row,
+                                              const Sink& out) {
     const bool owner = active && ql == 0;
     const uint64_t gid = uint64_t(a.env_offset + e);
     const uint32_t ep = uint32_t(episode);
-    Real* f = a.f;
     TrackOne<Real> own;
     own.ql = ql;
     {   // gate ql, obstacle ql of the next track
@@ -332,12 +411,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
             oy += lo + (hi - lo) * Real(u01(u.b));
         }
         own.o[0] = ox; own.o[1] = oy; own.o[2] = C.obst_nom[o][2];
-        if (active) {   // the quad stores the drone slot's replicated track, a gate and an obstacle per lane
-#pragma unroll
-            for (int k = 0; k < 4; ++k) st(f, RF_GATE + 4 * g + k, EN, slot, own.g[k]);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) st(f, RF_OBST + 3 * o + k, EN, slot, own.o[k]);
-        }
+        out.track(active, EN, slot, ql, own);
     }
     TrackRegs<Real> T;
 #pragma unroll
@@ -419,22 +493,17 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
 #pragma unroll
         for (int k = 0; k < 4; ++k) uq[j][k] = qbc(u[k], j);
     if (!owner) return;
-    for (int k = 0; k < 3; ++k) {   // RewardWrapper.reset: current_target = obs[0, 12:15], previous_pos = obs[0, :3]
-        st(f, RF_WR_TARGET + k, EN, slot, dn == 0 && C.num_gates > 0 ? row0[3 + k] : Real(0));
-        st(f, RF_WR_PREV + k, EN, slot, dn == 0 ? row0[k] : Real(0));
+    {   // RewardWrapper.reset: current_target = obs[0, 12:15], previous_pos = obs[0, :3]
+        Real tgt[3], prv[3];
+        for (int k = 0; k < 3; ++k) {
+            tgt[k] = dn == 0 && C.num_gates > 0 ? row0[3 + k] : Real(0);
+            prv[k] = dn == 0 ? row0[k] : Real(0);
+        }
+        out.wrapper(EN, slot, tgt, prv);
     }
     RDrone<Real> d;
     d.prev_rpy[0] = nrpy.x; d.prev_rpy[1] = nrpy.y; d.prev_rpy[2] = nrpy.z;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        d.prev_vel[k] = Real(0); d.lpf1[k] = d.lpf2[k] = 0.0f; d.ierr[k] = d.ierrm[k] = 0.0f;
-    }
-    d.tick = d.last_att = d.last_pos = d.tumble = 0;
-    d.pw_roll = d.pw_pitch = __builtin_nanf("");
-    d.psp_roll = d.psp_pitch = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { d.ctl[k] = 0.0f; d.rpm[k] = d.prev[k] = Real(0); }
-    d.gate = 0; d.flags = 0;
+    reset_drone_constants(d);
     d.mass = C.race_mass;
     d.inertia[0] = C.race_inertia[0]; d.inertia[1] = C.race_inertia[1]; d.inertia[2] = C.race_inertia[2];
     if (C.random_inertia) {
@@ -463,26 +532,151 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
     d.ql = d.q;
     d.lpos = d.pos;
     d.kpos = C.physics == ADRP_PHYS_PYB ? npos : d.pos;   // self.pos: nominal until the first read
-    store_drone(a, EN, slot, d, true);
-    a.ist[RI_STEP * EN + slot] = 0;
-    a.ist[RI_EPISODE * EN + slot] = episode + 1;
-    a.ist[RI_WR_GATE * EN + slot] = 0;
+    out.drone(EN, slot, d, episode);
 }
 
-// Block = 64 lanes = 16 drones (kQuadDrones); one wave.  DRAWS: the disturbance draws of the
+// a done drone's reset from the helper wave's LDS staging: the stores ResetToHBM makes, the same values
+template <typename Real>
+__device__ __forceinline__ void reset_replay_q4(const RaceArgs<Real>& a, const ResetLds<Real>& s, int tl, int qd,
+                                                int ql, bool active, size_t EN, size_t slot, int episode) {
+    const ResetToHBM<Real> out{&a};
+    TrackOne<Real> own;
+    own.ql = ql;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) own.g[k] = s.trk[k][tl];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) own.o[k] = s.trk[4 + k][tl];
+    out.track(active, EN, slot, ql, own);
+    if (!(active && ql == 0)) return;
+    Real tgt[3], prv[3];
+    for (int k = 0; k < 3; ++k) { tgt[k] = s.wr[k][qd]; prv[k] = s.wr[3 + k][qd]; }
+    out.wrapper(EN, slot, tgt, prv);
+    RDrone<Real> d;
+    reset_drone_constants(d);
+    Real v[kRsDrone];
+#pragma unroll
+    for (int k = 0; k < kRsDrone; ++k) v[k] = s.drone[k][qd];
+    d.pos = v3(v[0], v[1], v[2]);
+    d.q = {v[3], v[4], v[5], v[6]};
+    d.vel = v3(v[7], v[8], v[9]);
+    d.w = v3(v[10], v[11], v[12]);
+    d.angv = v3(v[13], v[14], v[15]);
+    d.prev_rpy[0] = v[16]; d.prev_rpy[1] = v[17]; d.prev_rpy[2] = v[18];
+    d.mass = v[19]; d.inertia[0] = v[20]; d.inertia[1] = v[21]; d.inertia[2] = v[22];
+    d.kpos = v3(v[23], v[24], v[25]);
+    d.ql = d.q;
+    d.lpos = d.pos;
+    out.drone(EN, slot, d, episode);
+}
+
+// the sub-step draws of drone qd's sub-steps s = ql, ql + 4, ... into the LDS table [s][7][drone]:
+// fp32 the 3 force components and the 4 motor noises; fp64 the 3 force uniforms (exact in float;
+// the force is formed in Real at use) and the 4 noise samples (float, scaled at use)
+template <typename Real>
+__device__ __forceinline__ void quad_draws(const RaceConst<Real>& H, float* pre_draws, uint64_t seed, uint64_t gid,
+                                           uint32_t ep, int dn, int sc0, int ql, int qd, int S) {
+    for (int s = ql; s < S; s += 4) {
+        float* dst = pre_draws + s * 7 * kQuadDrones + qd;
+        if constexpr (sizeof(Real) == 4) {
+            Real fd[3], nz[4];
+            race_substep_draws(H, seed, gid, ep, dn, uint32_t(sc0 + s), fd, nz);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) dst[k * kQuadDrones] = fd[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dst[(3 + k) * kQuadDrones] = nz[k];
+        } else {
+            const U4 u = draw(seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), uint32_t(sc0 + s));
+            dst[0] = u01r<float>(u.a); dst[kQuadDrones] = u01r<float>(u.b); dst[2 * kQuadDrones] = u01r<float>(u.c);
+            const U4 v = draw(seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), uint32_t(sc0 + s));
+            const uint32_t x[4] = {v.a, v.b, v.c, v.d};
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {   // race_noise_draws' float samples (before the std scale)
+                const float u1 = (float(x[2 * p] >> 8) + 1.0f) * float(1.0 / 16777216.0);
+                const float u2 = float(x[2 * p + 1] >> 8) * float(1.0 / 16777216.0);
+                const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+                dst[(3 + 2 * p) * kQuadDrones] = r * __builtin_amdgcn_cosf(u2);
+                dst[(4 + 2 * p) * kQuadDrones] = r * __builtin_amdgcn_sinf(u2);
+            }
+        }
+    }
+}
+
+// Block = 64 lanes = 16 drones (kQuadDrones): the chain wave.  DRAWS: the disturbance draws of the
 // step's S <= kRacePreS sub-steps go through LDS (disturbances on); else none are needed, or (S
 // larger) each lane draws in the loop.
-template <typename Real, int PH, int G, bool DRAWS>
-__global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
+// RH (auto-reset on): a second wave per block, the reset helper, on another SIMD of the CU.  It makes
+// the sub-step draws (while the chain loads its state), then computes the NEXT episode of each of the
+// block's 16 drones (race_reset_q4 into LDS: track, drone state, nominal obs row) while the chain runs
+// the sub-steps; after the chain's tail decides which envs are done (barrier B1) it writes those out
+// (reset_replay_q4: the same stores the chain's own reset makes) and their reset rows into the block's
+// obs rows.  A done env no longer puts its ~25k-cycle reset on the chain wave.
+// Barriers: both waves pass the same sequence: [draws], track copy, 2 in track_gjk_pool, B1, copy-out.
+template <typename Real, int PH, int G, bool DRAWS, bool RH = false>
+__global__ void __launch_bounds__(RH ? 2 * kRaceBlock : kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     constexpr bool F32 = sizeof(Real) == 4;
     RACE_MARK(t0);
     const RaceConst<Real>& C = *a.c;
-    // [s][7][drone]: fp32 the 3 force components and the 4 motor noises; fp64 the 3 force uniforms
-    // (exact in float; the force is formed in Real at use) and the 4 noises (float samples)
-    __shared__ float pre_draws[DRAWS ? kRacePreS * 7 * kQuadDrones : 1];
+    constexpr int kRowF = 49 + 6 * (G - 1);   // widest obs row of this G
+    // the sub-step draw table is dead after the loop: the GJK job pool reuses its LDS
+    constexpr size_t kDrawBytes = DRAWS ? size_t(kRacePreS) * 7 * kQuadDrones * sizeof(float) : 16;
+    constexpr size_t kScratchBytes = kDrawBytes > sizeof(TrackJobs) ? kDrawBytes : sizeof(TrackJobs);
+    __shared__ __attribute__((aligned(16))) unsigned char scratch_lds[kScratchBytes];
+    float* const pre_draws = reinterpret_cast<float*>(scratch_lds);
+    TrackJobs& tjobs = *reinterpret_cast<TrackJobs*>(scratch_lds);
     __shared__ Real trk_lds[kTrackFields * kQuadDrones];                   // [field][drone]
-    __shared__ float4 rows4[kQuadDrones * kRaceMaxD / 4];
-    __shared__ TrackJobs tjobs;
+    __shared__ float4 rows4[kQuadDrones * kRowF / 4];
+    __shared__ std::conditional_t<RH, ResetLds<Real>, char> rs_lds;
+    __shared__ float rs_rows[RH ? kQuadDrones * kRowF : 1];
+    __shared__ int rs_done[kQuadDrones];
+    if constexpr (RH) {
+        if (threadIdx.x >= kRaceBlock) {   // ---- the reset helper wave ----
+            const int tl = threadIdx.x - kRaceBlock;
+            const int ql = tl & 3, qd = tl >> 2;
+            const int dl = blockIdx.x * kQuadDrones + qd;
+            const int e_raw = dl / G, d_raw = dl % G;
+            const int N = C.N;
+            const bool active = e_raw < a.E && d_raw < N;
+            const int e = e_raw < a.E ? e_raw : a.E - 1;
+            const int dn = d_raw < N ? d_raw : 0;
+            const size_t EN = size_t(a.E) * N;
+            const size_t slot = size_t(e) * N + dn;
+            const int sc0 = a.ist[RI_STEP * EN + slot];
+            const int episode = a.ist[RI_EPISODE * EN + slot];
+            if constexpr (DRAWS) {
+                quad_draws<Real>(C, pre_draws, a.seed, uint64_t(a.env_offset + e), uint32_t(episode - 1), dn, sc0, ql,
+                                 qd, C.S);
+                __syncthreads();   // the draws are in LDS
+            }
+            float* const rrow = rs_rows + ((qd / G) * N + dn) * C.D;
+            race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, rrow,
+                                   ResetToLDS<Real>{&rs_lds, tl, qd});
+            __syncthreads();   // the chain's track copy
+            __syncthreads();   // track_gjk_pool: jobs queued
+            __syncthreads();   // track_gjk_pool: results
+            __syncthreads();   // B1: the chain's done flags and terminal-obs copies
+            if (rs_done[qd]) {
+                reset_replay_q4(a, rs_lds, tl, qd, ql, active, EN, slot, episode);
+                float* const row = reinterpret_cast<float*>(rows4) + ((qd / G) * N + dn) * C.D;
+                if (active)
+                    for (int k = ql; k < C.D; k += 4) row[k] = rrow[k];
+            }
+            __syncthreads();   // B2: rows complete
+            const int e0 = blockIdx.x * (kQuadDrones / G);
+            const int ne = a.E - e0 < kQuadDrones / G ? a.E - e0 : kQuadDrones / G;
+            const int total = ne * N * C.D;
+            float* dst = a.obs + size_t(e0) * N * C.D;
+            const float* rows = reinterpret_cast<const float*>(rows4);
+            if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {   // the second half of the copy-out
+                float4* dst4 = reinterpret_cast<float4*>(dst);
+                const int n4 = total >> 2;
+                for (int i = kRaceBlock + tl; i < n4; i += 2 * kRaceBlock) store_out(dst4 + i, rows4[i]);
+                for (int i = 4 * n4 + kRaceBlock + tl; i < total; i += 2 * kRaceBlock) dst[i] = rows[i];
+            } else {
+                for (int i = kRaceBlock + tl; i < total; i += 2 * kRaceBlock) dst[i] = rows[i];
+            }
+            return;
+        }
+    }
     const int tl = threadIdx.x;
     const int ql = tl & 3, qd = tl >> 2;                 // quad lane, drone within the block
     const int cax = ql < 3 ? ql : 2;                     // this lane's Euler axis
@@ -544,31 +738,8 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         xc_y = sinf(radf_(yaw_deg));
     }
     const Lpf lpf = {C.lpf[0], C.lpf[1], C.lpf[2], C.lpf[3], C.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
-    if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
-        for (int s = ql; s < H.S; s += 4) {
-            float* dst = pre_draws + s * 7 * kQuadDrones + qd;
-            if constexpr (F32) {
-                Real fd[3], nz[4];
-                race_substep_draws(H, a.seed, gid, ep, dn, uint32_t(sc0 + s), fd, nz);
-#pragma unroll
-                for (int k = 0; k < 3; ++k) dst[k * kQuadDrones] = fd[k];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) dst[(3 + k) * kQuadDrones] = nz[k];
-            } else {
-                const U4 u = draw(a.seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), uint32_t(sc0 + s));
-                dst[0] = u01r<float>(u.a); dst[kQuadDrones] = u01r<float>(u.b); dst[2 * kQuadDrones] = u01r<float>(u.c);
-                const U4 v = draw(a.seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), uint32_t(sc0 + s));
-                const uint32_t x[4] = {v.a, v.b, v.c, v.d};
-#pragma unroll
-                for (int p = 0; p < 2; ++p) {   // race_noise_draws' float samples (before the std scale)
-                    const float u1 = (float(x[2 * p] >> 8) + 1.0f) * float(1.0 / 16777216.0);
-                    const float u2 = float(x[2 * p + 1] >> 8) * float(1.0 / 16777216.0);
-                    const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-                    dst[(3 + 2 * p) * kQuadDrones] = r * __builtin_amdgcn_cosf(u2);
-                    dst[(4 + 2 * p) * kQuadDrones] = r * __builtin_amdgcn_sinf(u2);
-                }
-            }
-        }
+    if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone (RH: the helper wave draws them)
+        if constexpr (!RH) quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
         __syncthreads();
     }
     // lane-distributed controller state: axis cax of the rate history and the gyro filter
@@ -835,7 +1006,12 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
         }
     }
-    if (reset) race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, row);
+    if constexpr (RH) {
+        if (ql == 0) rs_done[qd] = active && reset ? 1 : 0;
+        __syncthreads();   // B1: the helper writes the done drones' next episode and their reset rows
+    } else {
+        if (reset) race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, row, ResetToHBM<Real>{&a});
+    }
 #ifdef ADRP_RACE_TIMING
     RACE_MARK(t6);   // tail: reward, flags, stores and the auto-reset of done envs
     if (threadIdx.x == 0) {
@@ -849,13 +1025,14 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     const int ne = a.E - e0 < kQuadDrones / G ? a.E - e0 : kQuadDrones / G;
     const int total = ne * N * C.D;
     float* dst = a.obs + size_t(e0) * N * C.D;
+    constexpr int kCopyStride = RH ? 2 * kRaceBlock : kRaceBlock;   // RH: the helper copies every other chunk
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
         float4* dst4 = reinterpret_cast<float4*>(dst);
         const int n4 = total >> 2;
-        for (int i = tl; i < n4; i += kRaceBlock) store_out(dst4 + i, rows4[i]);
-        for (int i = 4 * n4 + tl; i < total; i += kRaceBlock) dst[i] = rows[i];
+        for (int i = tl; i < n4; i += kCopyStride) store_out(dst4 + i, rows4[i]);
+        for (int i = 4 * n4 + tl; i < total; i += kCopyStride) dst[i] = rows[i];
     } else {
-        for (int i = tl; i < total; i += kRaceBlock) dst[i] = rows[i];
+        for (int i = tl; i < total; i += kCopyStride) dst[i] = rows[i];
     }
 }
 

@@ -68,9 +68,26 @@ def valu(out_path, rest):
     json.dump(rec, open(out_path, "w"), indent=1)
 
 
+def calib(out_path, fdir, wdir, bytes_per_launch):
+    """tools/fetch_calib: FETCH_SIZE / WRITE_SIZE per launch over the known streamed bytes, per
+    access width (4 / 8 / 16 B per lane)"""
+    rec = {"bytes_per_launch": bytes_per_launch,
+           "method": "tools/fetch_calib.hip: one coalesced streaming pass over 256 MiB per launch, "
+                     "median over launches after the first 8; ratio = counter bytes / streamed bytes"}
+    for w in (4, 8, 16):
+        f, _ = counter(fdir, "FETCH_SIZE", f"calib_read{w}")
+        wr, _ = counter(wdir, "WRITE_SIZE", f"calib_write{w}")
+        rec[f"read{w}"] = {"fetch_size_kib": f, "ratio": f * 1024 / bytes_per_launch}
+        rec[f"write{w}"] = {"write_size_kib": wr, "ratio": wr * 1024 / bytes_per_launch}
+        print(w, rec[f"read{w}"], rec[f"write{w}"])
+    json.dump(rec, open(out_path, "w"), indent=1)
+
+
 def main():
     if sys.argv[1] == "--valu":
         return valu(sys.argv[2], sys.argv[3:])
+    if sys.argv[1] == "--calib":
+        return calib(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]))
     out_path, rest = sys.argv[1], sys.argv[2:]
     try:
         rec = json.load(open(out_path))

@@ -2,7 +2,7 @@
 
 usage: ADRP_LIB=gym_pybullet_adrp_amd/libadrp_timing.so python tools/race_phases.py [LEVEL DRONES PHYSICS MODE E]
        RACE_POLICY=example|twogates: setpoints from the on-device PPO actor (closed loop) instead of
-       fixed random targets
+       fixed random targets; RACE_PRECISION=fp64: the float64 kernel
 Prints, per configuration, the s_memtime cycles per wave spent in each phase (mean over
 waves, and the slowest wave per launch averaged over launches) and the kernel time from
 dispatch events.
@@ -28,12 +28,15 @@ if len(sys.argv) > 5:
 
 lib = ctypes.CDLL(_lib.LIB_PATH)
 lib.adrp_race_phase_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-lib.adrp_race_wave_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+PREC = os.environ.get("RACE_PRECISION", "fp32")
+wave_read = lib.adrp_race_wave_read_f64 if PREC == "fp64" else lib.adrp_race_wave_read
+wave_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 buf = (ctypes.c_ulonglong * 32)()
 QUAD = os.environ.get("ADRP_RACE_QUAD", "1") != "0"
 
 for level, n, phys, mode, E in CONFIGS:
-    env = MultiRaceAviary(level, num_drones=n, physics=Physics[phys], racemode=RaceMode[mode], num_envs=E, seed=7)
+    env = MultiRaceAviary(level, num_drones=n, physics=Physics[phys], racemode=RaceMode[mode], num_envs=E, seed=7,
+                          precision=PREC)
     obs0, _ = env.reset()
     gen = torch.Generator(device=env.device)
     gen.manual_seed(3)
@@ -69,14 +72,14 @@ for level, n, phys, mode, E in CONFIGS:
             _, _, te, tr, _ = step(acts[k % 16])
             torch.cuda.synchronize()
             done += float((te | tr).float().mean())
-            assert lib.adrp_race_wave_read(wbuf, nb) == 0
+            assert wave_read(wbuf, nb) == 0
             w = np.array(list(wbuf), dtype=np.float64).reshape(nb, 8)
             means.append(w.mean(0))
             maxs.append(w.max(0))
         ms = env.h.profile_end(nk)
         lib.adrp_race_phase_read(buf, 1)   # GJK counters (timing build with -DADRP_RACE_GJK_STATS)
         gv = np.array(list(buf), dtype=np.float64)
-        print(json.dumps({"config": f"{level} N={n} {phys} {mode} E={E}", "kernel": _lib.kernel_name(env.cfg),
+        print(json.dumps({"config": f"{level} N={n} {phys} {mode} E={E}", "kernel": env.kernel_name,
                           "gjk": {"calls_per_launch": gv[9] / nk, "mean_iters": gv[18] / max(gv[9], 1),
                                   "max_iters": gv[19], "contact_calls_per_launch": gv[20] / nk,
                                   "contact_max_iters": gv[21], "capped_calls": gv[22]},
