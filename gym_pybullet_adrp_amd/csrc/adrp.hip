@@ -312,8 +312,8 @@ extern "C" const char* adrp_handle_kernel_name(const adrp_t* h) {
     const int p = h->cfg.physics >= 0 && h->cfg.physics <= 5 ? h->cfg.physics : 0;
     const char* prec = h->real_size == 8 ? "f64" : "f32";
     if (h->cmdf) snprintf(buf, sizeof buf, "race_step<%s,%s,G8,CMD>", prec, ph[p]);
-    else snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s%s>", prec, ph[p], race_group(h->N),
-                  h->race_quad ? ",Q4" : "", h->race_quad && h->cfg.autoreset && h->race_reset_helper ? ",RH" : "");
+    else snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s>", prec, ph[p], race_group(h->N),
+                  h->race_quad ? ",Q4" : "");
     return buf;
 }
 
@@ -388,7 +388,6 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     if (const char* env = getenv("ADRP_RESET_HELPER")) h->reset_helper = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RACE_HELPERS")) h->race_helpers = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RACE_QUAD")) h->race_quad = atoi(env) != 0;
-    if (const char* env = getenv("ADRP_RACE_RESET_HELPER")) h->race_reset_helper = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RACE_REFINE")) h->race_refine = atoi(env) != 0;
     const int rc = race ? (h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h))
                         : (h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h));

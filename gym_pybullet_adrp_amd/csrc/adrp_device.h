@@ -43,6 +43,17 @@ __device__ unsigned long long g_race_wave[kWaveSlots * 8];
 #endif
 
 
+// XCD-aware workgroup order.  The command processor deals consecutive workgroups round-robin over the
+// 8 XCDs, each with its own L2; this bijection gives XCD x the contiguous range of logical blocks
+// [x q + min(x, r), ...) (q, r = n / 8, n % 8), so neighbouring blocks that share cache lines (the race
+// quad kernel: 16 drones x 4 B = half a 128-B line per field per block) share one L2 instead of each
+// fetching the line into its own.
+__device__ __forceinline__ int xcd_block(int b, int n) {
+    constexpr int X = 8;
+    const int x = b % X, i = b / X, q = n / X, r = n % X;
+    return x * q + (x < r ? x : r) + i;
+}
+
 template <typename Real>
 struct V3 {
     Real x, y, z;

@@ -37,7 +37,6 @@ struct adrp_handle {
     bool reset_helper = true;     // staged kernels: reset states from a helper wave (ADRP_RESET_HELPER=0)
     bool race_helpers = true;     // race fp32: helper waves (track copy, draws) (ADRP_RACE_HELPERS=0)
     bool race_quad = true;        // race: four lanes per drone (race_quad.h) (ADRP_RACE_QUAD=0: one lane)
-    bool race_reset_helper = true;   // race quad + auto-reset: reset helper wave (ADRP_RACE_RESET_HELPER=0: off)
     bool race_refine = true;      // race: support-function bounds before GJK (ADRP_RACE_REFINE=0: centre bounds only)
     float* cmdf = nullptr;        // race command mode (adrp_enable_commands): [ADRP_CMD_NF][E*N]
     int32_t* cmdi = nullptr;      // [ADRP_CMD_NI][E*N]

@@ -4,12 +4,10 @@
 #include "adrp_internal.h"
 
 // four lanes per drone (race_quad.h): 16 drones per 64-lane block
-// RH (auto-reset on, ADRP_RACE_RESET_HELPER != 0): a reset helper wave per block (128 threads)
 template <typename Real, int PH>
 static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
     const bool draws = h->cfg.track.disturbances && h->S <= kRacePreS;
-    const bool rh = h->cfg.autoreset && h->race_reset_helper;
-    const dim3 blk(rh ? 2 * kRaceBlock : kRaceBlock), grid((unsigned)((size_t(h->E) * G * 4 + kRaceBlock - 1) / kRaceBlock));
+    const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G * 4 + kRaceBlock - 1) / kRaceBlock));
     auto go = [&](auto kernel) {
         if (h->prof_n < h->prof_cap) {
             hipExtLaunchKernelGGL(kernel, grid, blk, 0, s, h->ev_start[h->prof_n], h->ev_stop[h->prof_n], 0, a);
@@ -18,24 +16,19 @@ static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t
             hipLaunchKernelGGL(kernel, grid, blk, 0, s, a);
         }
     };
-    auto by_g = [&](auto dr, auto rr) {
-        constexpr bool D = decltype(dr)::value, R = decltype(rr)::value;
+    auto by_g = [&](auto dr) {
+        constexpr bool D = decltype(dr)::value;
         switch (G) {
 #ifndef ADRP_DEV_FAST
-            case 1: go(race_step_q4<Real, PH, 1, D, R>); break;
-            case 8: go(race_step_q4<Real, PH, 8, D, R>); break;
+            case 1: go(race_step_q4<Real, PH, 1, D>); break;
+            case 8: go(race_step_q4<Real, PH, 8, D>); break;
 #endif
-            case 2: go(race_step_q4<Real, PH, 2, D, R>); break;
-            default: go(race_step_q4<Real, PH, 4, D, R>); break;
+            case 2: go(race_step_q4<Real, PH, 2, D>); break;
+            default: go(race_step_q4<Real, PH, 4, D>); break;
         }
     };
-    if (rh) {
-        if (draws) by_g(std::true_type{}, std::true_type{});
-        else by_g(std::false_type{}, std::true_type{});
-    } else {
-        if (draws) by_g(std::true_type{}, std::false_type{});
-        else by_g(std::false_type{}, std::false_type{});
-    }
+    if (draws) by_g(std::true_type{});
+    else by_g(std::false_type{});
 }
 
 // command mode: the lane kernel with the commander (commander.h), G = 8 lanes per env for every N

@@ -305,10 +305,9 @@ struct TrackRegs {
     __device__ __forceinline__ Real operator()(int field) const { return v[field - RF_GATE]; }
 };
 
-// Where a reset's results go.  ResetToHBM: the drone slot's state in HBM (the chain wave resetting a
-// done env after its step).  ResetToLDS: a block's LDS staging (the reset helper wave computes every
-// drone's next episode during the sub-steps; reset_replay_q4 then writes the done ones out with the
-// same stores ResetToHBM makes).
+// Where a reset's results go: the drone slot's state in HBM (the quad resetting a done env after its
+// step).  A sink, so a staging variant can take the same values (a reset helper wave computing every
+// drone's next episode into LDS during the sub-steps was measured and dropped: DESIGN.md §3.2.1).
 template <typename Real>
 struct ResetToHBM {
     const RaceArgs<Real>* a;
@@ -333,40 +332,6 @@ struct ResetToHBM {
     }
 };
 
-// the values of a reset that are not constants, per drone of the block (qd), and the lanes' track parts
-constexpr int kRsDrone = 26;   // pos 3, q 4, vel 3, w 3, angv 3, prev_rpy 3, mass 1, inertia 3, kpos 3
-template <typename Real>
-struct ResetLds {
-    Real trk[7][kRaceBlock];                 // lane's gate ql (4) and obstacle ql (3)
-    Real drone[kRsDrone][kQuadDrones];
-    Real wr[6][kQuadDrones];
-};
-template <typename Real>
-struct ResetToLDS {
-    ResetLds<Real>* s;
-    int tl, qd;
-    __device__ __forceinline__ void track(bool, size_t, size_t, int, const TrackOne<Real>& own) const {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s->trk[k][tl] = own.g[k];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) s->trk[4 + k][tl] = own.o[k];
-    }
-    __device__ __forceinline__ void wrapper(size_t, size_t, const Real tgt[3], const Real prv[3]) const {
-        for (int k = 0; k < 3; ++k) {
-            s->wr[k][qd] = tgt[k];
-            s->wr[3 + k][qd] = prv[k];
-        }
-    }
-    __device__ __forceinline__ void drone(size_t, size_t, const RDrone<Real>& d, int) const {
-        const Real v[kRsDrone] = {d.pos.x, d.pos.y, d.pos.z, d.q.x, d.q.y, d.q.z, d.q.w, d.vel.x, d.vel.y, d.vel.z,
-                                  d.w.x, d.w.y, d.w.z, d.angv.x, d.angv.y, d.angv.z, d.prev_rpy[0], d.prev_rpy[1],
-                                  d.prev_rpy[2], d.mass, d.inertia[0], d.inertia[1], d.inertia[2], d.kpos.x, d.kpos.y,
-                                  d.kpos.z};
-#pragma unroll
-        for (int k = 0; k < kRsDrone; ++k) s->drone[k][qd] = v[k];
-    }
-};
-
 // the reset state a race_reset_q4 leaves in an RDrone besides its non-constant values
 template <typename Real>
 __device__ __forceinline__ void reset_drone_constants(RDrone<Real>& d) {
@@ -382,10 +347,20 @@ __device__ __forceinline__ void reset_drone_constants(RDrone<Real>& d) {
     d.gate = 0; d.flags = 0;
 }
 
+#if defined(ADRP_RACE_TIMING) && defined(ADRP_RESET_PHASES)
+// measurement-only (tools/race_phases.py with a -DADRP_RESET_PHASES timing build): s_memtime marks
+// inside the reset, reported in the kernel's 8 per-block phase slots instead of the step phases
+__shared__ uint64_t g_reset_mark[9];   // per workgroup (LDS): blocks do not race
+#define RESET_MARK(k) g_reset_mark[k] = __builtin_amdgcn_s_memtime()
+#else
+#define RESET_MARK(k)
+#endif
+
 template <typename Real, int G, class Sink>
 __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const RaceConst<Real>& C, int e, int dn, int ql,
                                               bool active, size_t EN, size_t slot, int episode, float* obs_row,
                                               const Sink& out) {
+    RESET_MARK(0);
     const bool owner = active && ql == 0;
     const uint64_t gid = uint64_t(a.env_offset + e);
     const uint32_t ep = uint32_t(episode);
@@ -411,8 +386,10 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
             oy += lo + (hi - lo) * Real(u01(u.b));
         }
         own.o[0] = ox; own.o[1] = oy; own.o[2] = C.obst_nom[o][2];
+        RESET_MARK(1);
         out.track(active, EN, slot, ql, own);
     }
+    RESET_MARK(2);
     TrackRegs<Real> T;
 #pragma unroll
     for (int g = 0; g < ADRP_MAX_GATES; ++g)
@@ -427,6 +404,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
     const V3<Real> npos = v3(C.init_pos[dn][0], C.init_pos[dn][1], C.init_pos[dn][2]);
     const Q4<Real> nq = quat_from_euler_fast(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
     const Shape<Real> ds = drone_shape(C, npos, nq);
+    RESET_MARK(3);
     uint32_t gin, oin, amb, camb_all;
     bool ccert;
 #ifdef ADRP_EXP_RESET_NOQ
@@ -446,6 +424,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
     }
     gin |= quad_or(g2);
     oin |= quad_or(o2);
+    RESET_MARK(4);
     Real row0[15];
     const V3<Real> zero = v3(Real(0), Real(0), Real(0));
 #ifdef ADRP_EXP_RESET_NOROW
@@ -453,6 +432,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
 #else
     race_obs_row(C, T, npos, nq, zero, zero, 0, obs_row, owner, row0, gin, oin);
 #endif
+    RESET_MARK(5);
     // the nominal Euler angles of drone k (lane k % 4 computes drones ql, ql + 4)
     V3<Real> nrpy_j[(G + 3) / 4];
 #pragma unroll
@@ -479,6 +459,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
             }
         }
     }
+    RESET_MARK(6);
     // _drone_init draws: lane 0 position offsets, lane 1 rotation offsets, lane 2 mass / inertia
     // (the uniforms travel; the ranges are applied as race_reset_lane does)
     const uint32_t dtag = TAG_RACE_DRONE | uint32_t(dn);
@@ -492,6 +473,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
     for (int j = 0; j < 3; ++j)
 #pragma unroll
         for (int k = 0; k < 4; ++k) uq[j][k] = qbc(u[k], j);
+    RESET_MARK(7);
     if (!owner) return;
     {   // RewardWrapper.reset: current_target = obs[0, 12:15], previous_pos = obs[0, :3]
         Real tgt[3], prv[3];
@@ -533,40 +515,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
     d.lpos = d.pos;
     d.kpos = C.physics == ADRP_PHYS_PYB ? npos : d.pos;   // self.pos: nominal until the first read
     out.drone(EN, slot, d, episode);
-}
-
-// a done drone's reset from the helper wave's LDS staging: the stores ResetToHBM makes, the same values
-template <typename Real>
-__device__ __forceinline__ void reset_replay_q4(const RaceArgs<Real>& a, const ResetLds<Real>& s, int tl, int qd,
-                                                int ql, bool active, size_t EN, size_t slot, int episode) {
-    const ResetToHBM<Real> out{&a};
-    TrackOne<Real> own;
-    own.ql = ql;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) own.g[k] = s.trk[k][tl];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) own.o[k] = s.trk[4 + k][tl];
-    out.track(active, EN, slot, ql, own);
-    if (!(active && ql == 0)) return;
-    Real tgt[3], prv[3];
-    for (int k = 0; k < 3; ++k) { tgt[k] = s.wr[k][qd]; prv[k] = s.wr[3 + k][qd]; }
-    out.wrapper(EN, slot, tgt, prv);
-    RDrone<Real> d;
-    reset_drone_constants(d);
-    Real v[kRsDrone];
-#pragma unroll
-    for (int k = 0; k < kRsDrone; ++k) v[k] = s.drone[k][qd];
-    d.pos = v3(v[0], v[1], v[2]);
-    d.q = {v[3], v[4], v[5], v[6]};
-    d.vel = v3(v[7], v[8], v[9]);
-    d.w = v3(v[10], v[11], v[12]);
-    d.angv = v3(v[13], v[14], v[15]);
-    d.prev_rpy[0] = v[16]; d.prev_rpy[1] = v[17]; d.prev_rpy[2] = v[18];
-    d.mass = v[19]; d.inertia[0] = v[20]; d.inertia[1] = v[21]; d.inertia[2] = v[22];
-    d.kpos = v3(v[23], v[24], v[25]);
-    d.ql = d.q;
-    d.lpos = d.pos;
-    out.drone(EN, slot, d, episode);
+    RESET_MARK(8);
 }
 
 // the sub-step draws of drone qd's sub-steps s = ql, ql + 4, ... into the LDS table [s][7][drone]:
@@ -601,21 +550,13 @@ __device__ __forceinline__ void quad_draws(const RaceConst<Real>& H, float* pre_
     }
 }
 
-// Block = 64 lanes = 16 drones (kQuadDrones): the chain wave.  DRAWS: the disturbance draws of the
+// Block = 64 lanes = 16 drones (kQuadDrones); one wave.  DRAWS: the disturbance draws of the
 // step's S <= kRacePreS sub-steps go through LDS (disturbances on); else none are needed, or (S
 // larger) each lane draws in the loop.
-// RH (auto-reset on): a second wave per block, the reset helper, on another SIMD of the CU.  It makes
-// the sub-step draws (while the chain loads its state), then computes the NEXT episode of each of the
-// block's 16 drones (race_reset_q4 into LDS: track, drone state, nominal obs row) while the chain runs
-// the sub-steps; after the chain's tail decides which envs are done (barrier B1) it writes those out
-// (reset_replay_q4: the same stores the chain's own reset makes) and their reset rows into the block's
-// obs rows.  A done env no longer puts its ~25k-cycle reset on the chain wave.
-// Barriers: both waves pass the same sequence: [draws], track copy, 2 in track_gjk_pool, B1, copy-out.
-template <typename Real, int PH, int G, bool DRAWS, bool RH = false>
-__global__ void __launch_bounds__(RH ? 2 * kRaceBlock : kRaceBlock) race_step_q4(RaceArgs<Real> a) {
+template <typename Real, int PH, int G, bool DRAWS>
+__global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     constexpr bool F32 = sizeof(Real) == 4;
     RACE_MARK(t0);
-    const RaceConst<Real>& C = *a.c;
     constexpr int kRowF = 49 + 6 * (G - 1);   // widest obs row of this G
     // the sub-step draw table is dead after the loop: the GJK job pool reuses its LDS
     constexpr size_t kDrawBytes = DRAWS ? size_t(kRacePreS) * 7 * kQuadDrones * sizeof(float) : 16;
@@ -625,79 +566,39 @@ __global__ void __launch_bounds__(RH ? 2 * kRaceBlock : kRaceBlock) race_step_q4
     TrackJobs& tjobs = *reinterpret_cast<TrackJobs*>(scratch_lds);
     __shared__ Real trk_lds[kTrackFields * kQuadDrones];                   // [field][drone]
     __shared__ float4 rows4[kQuadDrones * kRowF / 4];
-    __shared__ std::conditional_t<RH, ResetLds<Real>, char> rs_lds;
-    __shared__ float rs_rows[RH ? kQuadDrones * kRowF : 1];
-    __shared__ int rs_done[kQuadDrones];
-    if constexpr (RH) {
-        if (threadIdx.x >= kRaceBlock) {   // ---- the reset helper wave ----
-            const int tl = threadIdx.x - kRaceBlock;
-            const int ql = tl & 3, qd = tl >> 2;
-            const int dl = blockIdx.x * kQuadDrones + qd;
-            const int e_raw = dl / G, d_raw = dl % G;
-            const int N = C.N;
-            const bool active = e_raw < a.E && d_raw < N;
-            const int e = e_raw < a.E ? e_raw : a.E - 1;
-            const int dn = d_raw < N ? d_raw : 0;
-            const size_t EN = size_t(a.E) * N;
-            const size_t slot = size_t(e) * N + dn;
-            const int sc0 = a.ist[RI_STEP * EN + slot];
-            const int episode = a.ist[RI_EPISODE * EN + slot];
-            if constexpr (DRAWS) {
-                quad_draws<Real>(C, pre_draws, a.seed, uint64_t(a.env_offset + e), uint32_t(episode - 1), dn, sc0, ql,
-                                 qd, C.S);
-                __syncthreads();   // the draws are in LDS
-            }
-            float* const rrow = rs_rows + ((qd / G) * N + dn) * C.D;
-            race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, rrow,
-                                   ResetToLDS<Real>{&rs_lds, tl, qd});
-            __syncthreads();   // the chain's track copy
-            __syncthreads();   // track_gjk_pool: jobs queued
-            __syncthreads();   // track_gjk_pool: results
-            __syncthreads();   // B1: the chain's done flags and terminal-obs copies
-            if (rs_done[qd]) {
-                reset_replay_q4(a, rs_lds, tl, qd, ql, active, EN, slot, episode);
-                float* const row = reinterpret_cast<float*>(rows4) + ((qd / G) * N + dn) * C.D;
-                if (active)
-                    for (int k = ql; k < C.D; k += 4) row[k] = rrow[k];
-            }
-            __syncthreads();   // B2: rows complete
-            const int e0 = blockIdx.x * (kQuadDrones / G);
-            const int ne = a.E - e0 < kQuadDrones / G ? a.E - e0 : kQuadDrones / G;
-            const int total = ne * N * C.D;
-            float* dst = a.obs + size_t(e0) * N * C.D;
-            const float* rows = reinterpret_cast<const float*>(rows4);
-            if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {   // the second half of the copy-out
-                float4* dst4 = reinterpret_cast<float4*>(dst);
-                const int n4 = total >> 2;
-                for (int i = kRaceBlock + tl; i < n4; i += 2 * kRaceBlock) store_out(dst4 + i, rows4[i]);
-                for (int i = 4 * n4 + kRaceBlock + tl; i < total; i += 2 * kRaceBlock) dst[i] = rows[i];
-            } else {
-                for (int i = kRaceBlock + tl; i < total; i += 2 * kRaceBlock) dst[i] = rows[i];
-            }
-            return;
-        }
+    // the constant block in LDS: the post-loop phases and the auto-reset index it by drone / gate /
+    // obstacle (lane-varying), which from global memory is a dependent miss per table
+    __shared__ __attribute__((aligned(16))) RaceConst<Real> c_lds;
+    {
+        constexpr int nw = int(sizeof(RaceConst<Real>) / 4);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.c);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&c_lds);
+        for (int i = threadIdx.x; i < nw; i += kRaceBlock) dst[i] = src[i];
     }
+    const RaceConst<Real>& CG = *a.c;   // uniform fields: scalar loads (SGPRs)
+    const RaceConst<Real>& C = c_lds;   // after the loop
     const int tl = threadIdx.x;
     const int ql = tl & 3, qd = tl >> 2;                 // quad lane, drone within the block
     const int cax = ql < 3 ? ql : 2;                     // this lane's Euler axis
     RaceConst<Real> H;
-    H.S = C.S; H.link_lag = C.link_lag; H.disturbances = C.disturbances;
-    H.dt = C.dt; H.gravity = C.gravity; H.kf = C.kf; H.km = C.km;
+    H.S = CG.S; H.link_lag = CG.link_lag; H.disturbances = CG.disturbances;
+    H.dt = CG.dt; H.gravity = CG.gravity; H.kf = CG.kf; H.km = CG.km;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { H.px[i] = C.px[i]; H.py[i] = C.py[i]; H.pz[i] = C.pz[i]; }
-    H.gnd_kf = C.gnd_kf; H.prop_r4 = C.prop_r4; H.gnd_clip = C.gnd_clip;
+    for (int i = 0; i < 4; ++i) { H.px[i] = CG.px[i]; H.py[i] = CG.py[i]; H.pz[i] = CG.pz[i]; }
+    H.gnd_kf = CG.gnd_kf; H.prop_r4 = CG.prop_r4; H.gnd_clip = CG.gnd_clip;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        H.drag[i] = C.drag[i]; H.dist_lo[i] = C.dist_lo[i]; H.dist_hi[i] = C.dist_hi[i];
-        H.dyn_i[i] = C.dyn_i[i]; H.dyn_inv_i[i] = C.dyn_inv_i[i];
+        H.drag[i] = CG.drag[i]; H.dist_lo[i] = CG.dist_lo[i]; H.dist_hi[i] = CG.dist_hi[i];
+        H.dyn_i[i] = CG.dyn_i[i]; H.dyn_inv_i[i] = CG.dyn_inv_i[i];
     }
-    H.dw1 = C.dw1; H.dw2 = C.dw2; H.dw3 = C.dw3; H.prop_r = C.prop_r;
-    H.dyn_mass = C.dyn_mass; H.dyn_inv_mass = C.dyn_inv_mass; H.dyn_arm = C.dyn_arm;
-    H.coll_hh = C.coll_hh; H.coll_r = C.coll_r; H.coll_zoff = C.coll_zoff; H.ang_max = C.ang_max;
-    H.noise_std = C.noise_std;
-    const int dl = blockIdx.x * kQuadDrones + qd;        // drone lane of the one-lane layout
+    H.dw1 = CG.dw1; H.dw2 = CG.dw2; H.dw3 = CG.dw3; H.prop_r = CG.prop_r;
+    H.dyn_mass = CG.dyn_mass; H.dyn_inv_mass = CG.dyn_inv_mass; H.dyn_arm = CG.dyn_arm;
+    H.coll_hh = CG.coll_hh; H.coll_r = CG.coll_r; H.coll_zoff = CG.coll_zoff; H.ang_max = CG.ang_max;
+    H.noise_std = CG.noise_std;
+    const int lb = xcd_block(blockIdx.x, gridDim.x);     // logical block (XCD-aware order)
+    const int dl = lb * kQuadDrones + qd;                // drone lane of the one-lane layout
     const int e_raw = dl / G, d_raw = dl % G;
-    const int N = C.N;
+    const int N = CG.N;
     const bool active = e_raw < a.E && d_raw < N;
     const bool owner = active && ql == 0;
     const int e = e_raw < a.E ? e_raw : a.E - 1;
@@ -731,15 +632,15 @@ __global__ void __launch_bounds__(RH ? 2 * kRaceBlock : kRaceBlock) race_step_q4
     {
 #pragma clang fp contract(off)
         Real qs, qc;
-        sincos_(Real(C.obs_wrapper ? 0.0f : av.w) * Real(0.5), &qs, &qc);   // DroneObservationWrapper: yaw 0
+        sincos_(Real(CG.obs_wrapper ? 0.0f : av.w) * Real(0.5), &qs, &qc);   // DroneObservationWrapper: yaw 0
         const float qz = float(qs), qw = float(qc);
         const float yaw_deg = degf_(atan2f(2.0f * (qw * qz + 0.0f * 0.0f), 1 - 2 * (0.0f * 0.0f + qz * qz)));
         xc_x = cosf(radf_(yaw_deg));
         xc_y = sinf(radf_(yaw_deg));
     }
-    const Lpf lpf = {C.lpf[0], C.lpf[1], C.lpf[2], C.lpf[3], C.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
-    if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone (RH: the helper wave draws them)
-        if constexpr (!RH) quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
+    const Lpf lpf = {CG.lpf[0], CG.lpf[1], CG.lpf[2], CG.lpf[3], CG.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
+    if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
+        quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
         __syncthreads();
     }
     // lane-distributed controller state: axis cax of the rate history and the gyro filter
@@ -1006,26 +907,25 @@ __global__ void __launch_bounds__(RH ? 2 * kRaceBlock : kRaceBlock) race_step_q4
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
         }
     }
-    if constexpr (RH) {
-        if (ql == 0) rs_done[qd] = active && reset ? 1 : 0;
-        __syncthreads();   // B1: the helper writes the done drones' next episode and their reset rows
-    } else {
-        if (reset) race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, row, ResetToHBM<Real>{&a});
-    }
+    if (reset) race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, row, ResetToHBM<Real>{&a});
 #ifdef ADRP_RACE_TIMING
     RACE_MARK(t6);   // tail: reward, flags, stores and the auto-reset of done envs
     if (threadIdx.x == 0) {
+#ifdef ADRP_RESET_PHASES   // the reset's sub-phases of this block's last reset (0 if none)
+        for (int k = 0; k < 8; ++k) RACE_WAVE(k, reset ? g_reset_mark[k + 1] - g_reset_mark[k] : 0);
+#else
         RACE_WAVE(0, t1 - t0); RACE_WAVE(1, acc_phys); RACE_WAVE(2, (t2 - t1) - acc_phys); RACE_WAVE(3, t3 - t2);
         RACE_WAVE(4, t4 - t3); RACE_WAVE(5, t5 - t4); RACE_WAVE(6, t6 - t5); RACE_WAVE(7, t6 - t0);
+#endif
     }
 #endif
     // ---- coalesced copy-out of the block's rows ----
     __syncthreads();
-    const int e0 = blockIdx.x * (kQuadDrones / G);
+    const int e0 = lb * (kQuadDrones / G);
     const int ne = a.E - e0 < kQuadDrones / G ? a.E - e0 : kQuadDrones / G;
     const int total = ne * N * C.D;
     float* dst = a.obs + size_t(e0) * N * C.D;
-    constexpr int kCopyStride = RH ? 2 * kRaceBlock : kRaceBlock;   // RH: the helper copies every other chunk
+    constexpr int kCopyStride = kRaceBlock;
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
         float4* dst4 = reinterpret_cast<float4*>(dst);
         const int n4 = total >> 2;

@@ -613,46 +613,3 @@ def test_support_bounds_bit_identical(monkeypatch, variant, level, N, physics, m
     gates = outs[0][..., [k * env.h.D + 48 for k in range(N)]]
     assert gates.max() >= 1, "the actor passed no gate: the test would not reach the gate parts"
     assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("precision", ["fp32", "fp64"])
-@pytest.mark.parametrize("E,N,level,physics,mode", [(256, 4, "level3", Physics.PYB_DW, RaceMode.COMPETE),
-                                                    (300, 2, "level0", Physics.PYB, RaceMode.COMPARE),
-                                                    (37, 3, "level2", Physics.PYB_GND_DRAG_DW, RaceMode.COMPETE)])
-def test_reset_helper_bit_identical(monkeypatch, E, N, level, physics, mode, precision):
-    """the four-lane kernel's reset helper wave (speculative next-episode state in LDS, written out for
-    the envs the chain wave finds done; RH) changes who computes the auto-reset, not what: 40 env.steps
-    with many terminations (targets outside the bounds / at the ground for a quarter of the envs, the
-    DroneObservationWrapper's gate-2 termination) agree bit for bit with ADRP_RACE_RESET_HELPER=0:
-    obs, reward, flags, terminal obs and the full state"""
-    from gym_pybullet_adrp_amd.utils.wrapper import DroneObservationWrapper
-    outs, names = [], []
-    for rh in ("1", "0"):
-        monkeypatch.setenv("ADRP_RACE_RESET_HELPER", rh)
-        env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=3,
-                              autoreset=True, reward="wrapper", precision=precision)
-        DroneObservationWrapper(env)
-        names.append(env.kernel_name)
-        obs, _ = env.reset()
-        rng = np.random.default_rng(4)
-        act = targets(rng, obs.cpu().numpy(), E, N)
-        wild = rng.uniform([-4, -4, 0.0, -1], [4, 4, 2.6, 1], (E, N, 4)).astype(np.float32)
-        act[::4] = wild[::4]
-        at = torch.from_numpy(act).to(env.device)
-        seq, done = [], 0
-        for _ in range(40):
-            obs, rew, te, tr, info = env.step(at)
-            d = te | tr
-            done += int(d.sum())
-            tob = torch.where(d[:, None, None], info["terminal_observation"], torch.zeros_like(obs))
-            seq.append(torch.cat([obs.reshape(E, -1), tob.reshape(E, -1), rew.reshape(E, 1).float(),
-                                  te.reshape(E, 1).float(), tr.reshape(E, 1).float()], 1).cpu())
-        f, i = env.get_state()
-        outs.append((torch.stack(seq), f.cpu().numpy(), i.cpu().numpy(), done))
-        env.close()
-    assert names[0].endswith(",Q4,RH>") and names[1].endswith(",Q4>"), names
-    (s1, f1, i1, d1), (s0, f0, i0, d0) = outs
-    assert d1 == d0 and d1 > 0, "the run should auto-reset envs"
-    assert torch.equal(s1, s0)
-    np.testing.assert_array_equal(i1, i0)
-    np.testing.assert_array_equal(f1, f0)     # NaN == NaN (the reset's D-term memory)

@@ -3,7 +3,7 @@
 # bench.py line each.  An arm is a library path, optionally followed by ,VAR=value switches, e.g.
 #   tools/ab.sh gym_pybullet_adrp_amd/libadrp.so,ADRP_RACE_QUAD=0 gym_pybullet_adrp_amd/libadrp.so 3 --task race
 # usage: tools/ab.sh ARM_A ARM_B ROUNDS [bench.py args...]
-# prints per run: arm, kernel_us (dispatch events), us per step (graph replay), value
+# prints per run: arm, kernel_us (events around the graph-replayed timed region / K), eager dispatch events, us per step, value
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 A="$1"; B="$2"; R="$3"; shift 3
 mkdir -p gpurun_out
@@ -15,7 +15,8 @@ for r in $(seq 1 "$R"); do
     python3 -c "
 import json,sys
 d=json.loads([l for l in open('gpurun_out/ab_last.log') if l.startswith('{')][-1])
-print(f\"{sys.argv[1]:60s} kernel_us {d['roofline']['kernel_us']:8.3f} med {d['roofline']['kernel_us_median']:8.3f} step_us {d['ms_per_step']*1e3:8.3f} value {d['value']:.4e}\")
+r=d['roofline']
+print(f\"{sys.argv[1]:60s} kernel_us {r['kernel_us']:8.3f} eager {r.get('eager_dispatch_us', float('nan')):8.3f} step_us {d['ms_per_step']*1e3:8.3f} value {d['value']:.4e}\")
 " "$ARM"
   done
 done

@@ -1,6 +1,6 @@
 """Per-phase cost of hover_step_kernel (needs the timing build: make -C gym_pybullet_adrp_amd/csrc timing).
 
-usage: ADRP_LIB=gym_pybullet_adrp_amd/libadrp_timing.so python tools/hover_phases.py [E ...]
+usage: ADRP_LIB=gym_pybullet_adrp_amd/libadrp_timing.so [HOVER_PRECISION=fp64] python tools/hover_phases.py [E ...]
 Workload = bench.py's default (airborne starts around (0,0,1), U[-1,1] RPM actions, auto-reset).
 Prints, per E, the s_memtime cycles per wave spent in each phase (mean over waves, and the
 slowest wave per launch averaged over launches), the share of waves that ran the auto-reset
@@ -8,6 +8,7 @@ path, and the kernel time from dispatch events.
 """
 import ctypes
 import json
+import os
 import sys
 
 import numpy as np
@@ -25,7 +26,7 @@ lib.adrp_race_phase_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.
 buf = (ctypes.c_ulonglong * 32)()
 
 for E in SIZES:
-    env = HoverAviary(num_envs=E, seed=2024, initial_xyzs=[0, 0, 1.0],
+    env = HoverAviary(num_envs=E, seed=2024, initial_xyzs=[0, 0, 1.0], precision=os.environ.get("HOVER_PRECISION", "fp32"),
                       init_noise={"xyz": 0.1, "rpy": 0.05, "vel": 0.1, "omega": 0.1})
     env.reset()
     gen = torch.Generator(device=env.device)
@@ -48,7 +49,7 @@ for E in SIZES:
         mx += v[10:18]
     ms = env.h.profile_end(nk)
     waves = sums[8]
-    print(json.dumps({"E": E, "kernel": _lib.kernel_name(env.cfg), "kernel_us": float(np.mean(ms)) * 1e3,
+    print(json.dumps({"E": E, "kernel": env.kernel_name, "kernel_us": float(np.mean(ms)) * 1e3,
                       "mean_cycles_per_wave": {p: round(sums[i] / waves) for i, p in enumerate(PHASES)},
                       "max_cycles_per_launch": {p: round(mx[i] / nk) for i, p in enumerate(PHASES)},
                       "waves_with_reset": sums[9] / waves, "done_lanes_per_step": sums[7] / nk}), flush=True)
