@@ -66,6 +66,9 @@ def load():
     lib.adrp_profile_end.restype = I
     lib.adrp_reseed.argtypes = [P, ctypes.c_uint64, P]
     lib.adrp_reseed.restype = I
+    if hasattr(lib, "adrp_set_noise"):       # (older experiment builds lack it)
+        lib.adrp_set_noise.argtypes = [P, P, P]
+        lib.adrp_set_noise.restype = I
     lib.adrp_set_wrappers.argtypes = [P, I, I]
     lib.adrp_set_wrappers.restype = I
     lib.adrp_enable_commands.argtypes = [P]
@@ -218,6 +221,12 @@ class Handle:
         seed = int(seed) & (2 ** 64 - 1)
         self._check(self.lib.adrp_reseed(self.h, seed, self._stream()), "adrp_reseed")
         self.cfg.seed = seed
+
+    def set_noise(self, act_noise, force):
+        """parity mode (include/adrp.h adrp_set_noise): float64 device tensors [E*N, S, 4] / [E*N, S, 3]
+        (kept referenced here: the library keeps the pointers), or None, None"""
+        self._noise = (act_noise, force)
+        self._check(self.lib.adrp_set_noise(self.h, _p(act_noise), _p(force)), "adrp_set_noise")
 
     def set_wrappers(self, reward_wrapper, obs_wrapper):
         self._check(self.lib.adrp_set_wrappers(self.h, int(bool(reward_wrapper)), int(obs_wrapper)), "adrp_set_wrappers")

@@ -429,6 +429,16 @@ extern "C" int adrp_set_wrappers(adrp_t* h, int reward_wrapper, int obs_wrapper)
     return rc == ADRP_OK ? rc : seterr(h, rc, "constant block upload failed");
 }
 
+extern "C" int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_dev) {
+    if (!h) return seterr(h, ADRP_ERR_INVALID, "adrp_set_noise: NULL handle");
+    if (h->cfg.task != ADRP_TASK_RACE) return seterr(h, ADRP_ERR_INVALID, "noise injection is MultiRaceAviary's");
+    if ((act_noise_dev == nullptr) != (force_dev == nullptr))
+        return seterr(h, ADRP_ERR_INVALID, "adrp_set_noise: both arrays or neither");
+    h->inj_act = act_noise_dev;
+    h->inj_force = force_dev;
+    return ADRP_OK;
+}
+
 extern "C" int adrp_obs_dim(const adrp_t* h) { return h ? h->D : ADRP_ERR_INVALID; }
 extern "C" int adrp_act_dim(const adrp_t* h) { return h ? h->A : ADRP_ERR_INVALID; }
 

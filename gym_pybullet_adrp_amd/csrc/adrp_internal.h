@@ -40,6 +40,8 @@ struct adrp_handle {
     bool race_refine = true;      // race: support-function bounds before GJK (ADRP_RACE_REFINE=0: centre bounds only)
     float* cmdf = nullptr;        // race command mode (adrp_enable_commands): [ADRP_CMD_NF][E*N]
     int32_t* cmdi = nullptr;      // [ADRP_CMD_NI][E*N]
+    const double* inj_act = nullptr;    // adrp_set_noise (parity mode): caller's device arrays
+    const double* inj_force = nullptr;
     int diagnostics = 0;
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -101,6 +103,8 @@ inline RaceArgs<Real> race_args(const adrp_t* h) {
     a.E = h->E;
     a.cf = h->cmdf;
     a.ci = h->cmdi;
+    a.inj_act = h->inj_act;
+    a.inj_force = h->inj_force;
     return a;
 }
 

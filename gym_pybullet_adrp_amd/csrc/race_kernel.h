@@ -86,6 +86,8 @@ struct RaceArgs {
     int32_t* ci;         // [ADRP_CMD_NI][E*N]
     const int32_t* cmd;  // race_command_kernel: [E*N] ADRP_CMD_*
     const double* cargs; // [E*N][ADRP_CMD_ARGS]
+    const double* inj_act;    // parity mode (adrp_set_noise): [E*N][S][4] action noise, or null (Philox)
+    const double* inj_force;  // [E*N][S][3] disturbance force, or null
     uint64_t seed;
     int64_t env_offset;
     int E;
@@ -250,6 +252,7 @@ __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Re
     B.c = B0.c - A0.c;
     A.c = v3(Real(0), Real(0), Real(0));
     const Real eps = sizeof(Real) == 4 ? Real(4e-6) : Real(1e-13);
+    const Real tol2 = sizeof(Real) == 4 ? Real(1e-14) : Real(1e-26);   // (1e-7 m)^2, (1e-13 m)^2
     V3<Real> W0, W1, W2, W3;
     int n = 0;
     V3<Real> v = A.c - B.c;
@@ -260,6 +263,10 @@ __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Re
         const Real vv = dot(v, v), vw = dot(v, w);
         if (vw > Real(0) && vw * vw >= cut2 * vv) { GJK_STAT(it + 1); return false; }   // lower bound
         if (vv - vw <= eps * vv) { GJK_STAT(it + 1); return vv < cut2; }
+        // absolute gap: the distance is known to within tol (|v| - vw/|v| <= tol).  Near contact
+        // (cut = 1 um, touching or penetrating shapes) |v| is tiny and the relative test above can
+        // not pass under the rounding of O(0.1 m) support points, which ran such queries to the cap
+        if ((vv - vw) * (vv - vw) <= tol2 * vv) { GJK_STAT(it + 1); return vv < cut2; }
         const V3<Real> dw0 = W0 - w, dw1 = W1 - w, dw2 = W2 - w;
         if ((n > 0 && dot(dw0, dw0) < Real(1e-20)) || (n > 1 && dot(dw1, dw1) < Real(1e-20)) ||
             (n > 2 && dot(dw2, dw2) < Real(1e-20))) {
@@ -1407,6 +1414,18 @@ __device__ __forceinline__ void race_substep_draws(const RaceConst<Real>& H, uin
     fd[2] = H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * u01r<Real>(u.c);
     race_noise_draws(H, seed, gid, ep, dn, idx, noise);
 }
+
+// parity mode (adrp_set_noise): the caller's draws of sub-step s of drone slot instead of Philox's
+template <typename Real>
+__device__ __forceinline__ void injected_draws(const RaceArgs<Real>& a, size_t slot, int S, int s, Real fd[3],
+                                               Real noise[4]) {
+    const double* pf = a.inj_force + (slot * S + s) * 3;
+    const double* pa = a.inj_act + (slot * S + s) * 4;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) fd[k] = Real(pf[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) noise[k] = Real(pa[k]);
+}
 // Block = kRaceBlock drone lanes.  Wave 0 runs the serial sub-step chain (physics -> controller ->
 // physics ...; one wave per CU at the race batch sizes, one instruction per 4 cycles).  With
 // disturbances on, kRaceHelpers more waves, on the CU's otherwise idle SIMDs, pre-compute every
@@ -1454,7 +1473,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
                 for (int s = hw; s < C.S; s += kRaceHelpers) {
                     if ((s < half) != (part == 0)) continue;
                     Real fd[3], nz[4];
-                    race_substep_draws(C, a.seed, hgid, hep, hd, uint32_t(hsc0 + s), fd, nz);
+                    if (a.inj_force) injected_draws(a, hslot, C.S, s, fd, nz);
+                    else race_substep_draws(C, a.seed, hgid, hep, hd, uint32_t(hsc0 + s), fd, nz);
                     float* dst = pre_draws + s * 7 * kRaceBlock + tl;
 #pragma unroll
                     for (int k = 0; k < 3; ++k) dst[k * kRaceBlock] = float(fd[k]);
@@ -1579,7 +1599,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
                     fd = v3(Real(src[0]), Real(src[kRaceBlock]), Real(src[2 * kRaceBlock]));
                 } else {
                     Real f3[3], nz[4];
-                    race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, nz);
+                    if (a.inj_force) injected_draws(a, slot, H.S, s, f3, nz);
+                    else race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, nz);
                     fd = v3(f3[0], f3[1], f3[2]);
                 }
                 const V3<Real> lo = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? d.pos : d.lpos;
@@ -1605,7 +1626,8 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
                     for (int k = 0; k < 4; ++k) noise[k] = Real(src[k * kRaceBlock]);
                 } else {
                     Real f3[3];
-                    race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, noise);
+                    if (a.inj_force) injected_draws(a, slot, H.S, s, f3, noise);
+                    else race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, noise);
                 }
             }
             mellinger_compute<Real, CMD>(d, lpf, sp, xc_x, xc_y, euler_xyz_fast_u(d.q), noise, &cs, coefp, EN, slot);

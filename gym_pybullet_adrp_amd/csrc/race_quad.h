@@ -639,8 +639,9 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         xc_y = sinf(radf_(yaw_deg));
     }
     const Lpf lpf = {CG.lpf[0], CG.lpf[1], CG.lpf[2], CG.lpf[3], CG.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
+    const bool inj = a.inj_force != nullptr;   // parity mode: the caller's draws, read in the loop
     if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
-        quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
+        if (!inj) quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
         __syncthreads();
     }
     // lane-distributed controller state: axis cax of the rate history and the gyro filter
@@ -698,7 +699,14 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
             }
             if (H.disturbances) {
                 V3<Real> fd;
-                if constexpr (DRAWS) {
+                if (inj) {
+                    Real f3[3], nz[4];
+                    injected_draws(a, slot, H.S, s, f3, nz);
+                    fd = v3(f3[0], f3[1], f3[2]);
+                    noise_m = nz[0];
+#pragma unroll
+                    for (int k = 1; k < 4; ++k) noise_m = ql == k ? nz[k] : noise_m;
+                } else if constexpr (DRAWS) {
                     const float* src = pre_draws + s * 7 * kQuadDrones + qd;
                     if constexpr (F32) {
                         fd = v3(src[0], src[kQuadDrones], src[2 * kQuadDrones]);

@@ -193,6 +193,26 @@ class MultiRaceAviary(AviaryEnv):
         self._last_act = act
         return self._obs, self._rew, self._term, self._trunc, self._info
 
+    def set_noise(self, act_noise=None, force=None):
+        """Parity mode: the next steps take the action noise [E, N, S, 4] and the disturbance force
+        [E, N, S, 3] of every drone and sub-step from these arrays instead of the device Philox
+        streams (include/adrp.h adrp_set_noise): e.g. the values the reference draws from its
+        np_random (MultiRaceAviary.py:223-228, 532-537).  The arrays are copied into persistent
+        device buffers here, so call it before every step; set_noise() returns to Philox."""
+        if act_noise is None and force is None:
+            self._noise_bufs = None
+            self.h.set_noise(None, None)
+            return
+        E, N, S = self.num_envs, self.NUM_DRONES, self.PYB_STEPS_PER_CTRL
+        a = torch.as_tensor(act_noise, dtype=torch.float64).reshape(E * N, S, 4)
+        f = torch.as_tensor(force, dtype=torch.float64).reshape(E * N, S, 3)
+        if getattr(self, "_noise_bufs", None) is None:
+            self._noise_bufs = (torch.empty((E * N, S, 4), dtype=torch.float64, device=self.device),
+                                torch.empty((E * N, S, 3), dtype=torch.float64, device=self.device))
+            self.h.set_noise(*self._noise_bufs)
+        self._noise_bufs[0].copy_(a)
+        self._noise_bufs[1].copy_(f)
+
     def close(self):
         self.h.close()
 

@@ -305,6 +305,19 @@ int adrp_policy_act(adrp_policy_t* p, const float* obs_dev, int rows, int obs_st
 void adrp_policy_destroy(adrp_policy_t* p);
 
 /* ---------------------------------------------------------------------------------------
+ * Parity mode noise (MultiRaceAviary).  The reference draws, per sub-step, the disturbance force
+ * of every drone (np_random.<distrib>(low, high), MultiRaceAviary.py:532-537) and then the (N, 4)
+ * action noise (np_random.<distrib>(0, std, (N, 4)), :223-228).  After adrp_set_noise the race
+ * step takes them from these caller-owned DEVICE arrays instead of its Philox streams:
+ *   act_noise_dev [E*N][S][4], force_dev [E*N][S][3] float64, drone slot e*N + n, sub-step s of
+ *   the NEXT adrp_step (S = pyb_freq / ctrl_freq); the caller refills them (stream-ordered)
+ *   before every step.  The pointers are kept until adrp_set_noise(h, NULL, NULL).  Only used when
+ *   the track has disturbances on.  Replaces: nothing in the reference's API (its RNG is internal);
+ *   lets a noisy reference step be replayed with the reference's own draws.
+ * --------------------------------------------------------------------------------------- */
+int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_dev);
+
+/* ---------------------------------------------------------------------------------------
  * Numerics probe (no reference counterpart: test support).  Evaluates one of the fp64
  * fast transcendentals the fp64 step kernels inline (csrc/adrp_device.h namespace f64:
  * refined v_rcp_f64 / v_rsq_f64, range-reduced polynomials) on n device doubles:

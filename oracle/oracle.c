@@ -245,6 +245,8 @@ struct orc_handle {
     double* pid;            /* [E][9] DSLPIDControl state (PID / VEL / ONE_D_PID), else NULL */
     struct rdrone_s* rd;    /* [E*N] MultiRace per-drone state (race.c) */
     struct renv_s* re;      /* [E] MultiRace per-env state */
+    const double* inj_act;    /* orc_set_noise: [E*N][S][4] action noise, or NULL (Philox) */
+    const double* inj_force;  /* [E*N][S][3] disturbance force, or NULL */
 };
 
 /* MultiRaceAviary (race.c, included at the end of this file) */

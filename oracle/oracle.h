@@ -42,6 +42,10 @@ int orc_step(orc_t* o, const float* act, float* obs, float* rew, uint8_t* term,
    [E*N][ADRP_CMD_ARGS]; then orc_step(o, NULL, ...) keeps the setpoints.  The command state
    snapshot has the adrp_get_command_state layout (float [ADRP_CMD_NF][E*N], int [ADRP_CMD_NI][E*N]). */
 int orc_race_command(orc_t* o, const int32_t* cmd, const double* args);
+/* MultiRace parity mode (adrp.h adrp_set_noise): the next steps take the action noise [E*N][S][4]
+   and the disturbance force [E*N][S][3] of sub-step s of drone slot e*N+n from these host arrays
+   (kept by pointer) instead of the Philox draws; NULL, NULL returns to Philox */
+int orc_set_noise(orc_t* o, const double* act_noise, const double* force);
 int orc_get_command_state(const orc_t* o, float* f, int32_t* i);
 int orc_set_command_state(orc_t* o, const float* f, const int32_t* i);
 /* one poly4d_eval of the commander's trajectory (tests): coef [4][8], out = pos 3, vel 3, acc 3,

@@ -75,6 +75,7 @@ def _load():
     lib.orc_race_reward.argtypes = [P, P, P, P, I, I]
     lib.orc_race_reward.restype = D
     lib.orc_race_command.argtypes = [P, P, P]
+    lib.orc_set_noise.argtypes = [P, P, P]
     lib.orc_get_command_state.argtypes = [P, P, P]
     lib.orc_set_command_state.argtypes = [P, P, P]
     lib.orc_poly4d_eval.argtypes = [P, ctypes.c_float, P]
@@ -146,6 +147,16 @@ class Oracle:
         return obs, rew, term.astype(bool), trunc.astype(bool), tobs
 
     CMD_NF, CMD_NI, CMD_ARGS = 63, 3, 14
+
+    def set_noise(self, act_noise=None, force=None):
+        """parity mode (orc_set_noise): action noise [E, N, S, 4] and disturbance force [E, N, S, 3]
+        of the next step's sub-steps, or None, None for the Philox draws"""
+        if act_noise is None:
+            self._noise = None
+            assert lib().orc_set_noise(self.h, None, None) == 0
+            return
+        self._noise = (np.ascontiguousarray(act_noise, np.float64), np.ascontiguousarray(force, np.float64))
+        assert lib().orc_set_noise(self.h, _ptr(self._noise[0]), _ptr(self._noise[1])) == 0
 
     def command(self, cmd, args):
         """One high-level command per drone: cmd int32 [E, N], args float64 [E, N, 14]."""

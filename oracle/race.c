@@ -1087,11 +1087,17 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
             for (int i = 0; i < N; ++i) {
                 assemble_forces(o, &F[i], bs, i, ds[i].rpm, ds[i].prev_rpm);
                 if (t->disturbances) {       /* world-frame force on link 4 at posObj = self.pos (532-544) */
-                    double u[4];
-                    draw4(c->seed, gid, ep, TAG_RACE_DIST | (uint32_t)i, idx, u);
-                    v3 f = V(t->dyn_dist_low[0] + (t->dyn_dist_high[0] - t->dyn_dist_low[0]) * u[0],
-                             t->dyn_dist_low[1] + (t->dyn_dist_high[1] - t->dyn_dist_low[1]) * u[1],
-                             t->dyn_dist_low[2] + (t->dyn_dist_high[2] - t->dyn_dist_low[2]) * u[2]);
+                    v3 f;
+                    if (o->inj_force) {      /* parity mode: the caller's draws (orc_set_noise) */
+                        const double* p = o->inj_force + (((size_t)e * N + i) * o->S + s) * 3;
+                        f = V(p[0], p[1], p[2]);
+                    } else {
+                        double u[4];
+                        draw4(c->seed, gid, ep, TAG_RACE_DIST | (uint32_t)i, idx, u);
+                        f = V(t->dyn_dist_low[0] + (t->dyn_dist_high[0] - t->dyn_dist_low[0]) * u[0],
+                              t->dyn_dist_low[1] + (t->dyn_dist_high[1] - t->dyn_dist_low[1]) * u[1],
+                              t->dyn_dist_low[2] + (t->dyn_dist_high[2] - t->dyn_dist_low[2]) * u[2]);
+                    }
                     v3 rel = vsub(ds[i].kin_pos, bs[i].link_pos);   /* posObj - cached link origin */
                     F[i].f_world[4] = vadd(F[i].f_world[4], f);
                     F[i].t_world[4] = vadd(F[i].t_world[4], vcross(rel, f));
@@ -1114,8 +1120,13 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
             }
             double noise[4] = {0, 0, 0, 0};
             if (t->disturbances) {           /* (223-228) */
-                draw_normal4(c->seed, gid, ep, TAG_RACE_NOISE | (uint32_t)i, idx, noise);
-                for (int k = 0; k < 4; ++k) noise[k] *= t->action_noise_std;
+                if (o->inj_act) {            /* parity mode: the caller's draws (orc_set_noise) */
+                    const double* p = o->inj_act + (((size_t)e * N + i) * o->S + s) * 4;
+                    for (int k = 0; k < 4; ++k) noise[k] = p[k];
+                } else {
+                    draw_normal4(c->seed, gid, ep, TAG_RACE_NOISE | (uint32_t)i, idx, noise);
+                    for (int k = 0; k < 4; ++k) noise[k] *= t->action_noise_std;
+                }
             }
             double rpy[3], pos[3] = {bs[i].pos.x, bs[i].pos.y, bs[i].pos.z}, vel[3] = {bs[i].vel.x, bs[i].vel.y, bs[i].vel.z};
             body_rpy(&bs[i], rpy);
@@ -1241,6 +1252,14 @@ static void race_set_row(orc_t* o, size_t slot, int e, int first, const double* 
     }
     d->tick = iv[2]; d->last_att_tick = iv[3]; d->last_pos_tick = iv[4]; d->tumble = iv[5]; d->gate = iv[6];
     d->elim = iv[7] & 1; d->fin = (iv[7] >> 1) & 1;
+}
+
+int orc_set_noise(orc_t* o, const double* act_noise, const double* force) {
+    if (o->cfg.task != ADRP_TASK_RACE) return fail("noise injection: MultiRaceAviary only");
+    if ((act_noise == NULL) != (force == NULL)) return fail("noise injection: both arrays or neither");
+    o->inj_act = act_noise;
+    o->inj_force = force;
+    return 0;
 }
 
 /* ---- high-level commands ---------------------------------------------------------------- */
