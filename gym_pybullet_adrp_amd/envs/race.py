@@ -179,7 +179,15 @@ class MultiRaceAviary(AviaryEnv):
 
     def step(self, action):
         """action [E,N,4]: absolute FULLSTATE target (x, y, z, yaw) per drone; or per drone a
-        (Command, args) tuple (MultiRaceAviary.py:190-210; lists per env, commands.py)."""
+        (Command, args) tuple (MultiRaceAviary.py:190-210; lists per env, commands.py); or the
+        encoded pair (codes int32 [E,N], args float64 [E,N,14]) as tensors, e.g. from
+        hardcoded.HardCodedCommander.predict: no per-drone Python on that path."""
+        if isinstance(action, tuple) and len(action) == 2 and isinstance(action[0], torch.Tensor) \
+                and isinstance(action[1], torch.Tensor) and action[1].dim() == 3:
+            self.enable_commands()
+            self.h.command(*action)
+            self.h.step(None, self._obs, self._rew, self._term, self._trunc, self._tobs)
+            return self._obs, self._rew, self._term, self._trunc, self._info
         if isinstance(action, (list, tuple)) and not _numeric(action):
             self.command(action)
             self.h.step(None, self._obs, self._rew, self._term, self._trunc, self._tobs)

@@ -847,6 +847,49 @@ def policy_fixtures(pb, m):
     return out
 
 
+def hardcoded_fixtures(pb, m):
+    """HardCodedController (user_controller/HardCodedController.py:14-190) as scripts/sim.py:68-106
+    drives it: config/getting_started.yaml, 2 drones, COMPARE, info["delay"] = drone_id, one
+    predict(obs[i], ep_time=episode_step / ctrl_freq) per drone per step, for the 33 s episode.
+    Recorded: the reset observation the controllers are built from, and per step and drone the
+    command's value string and its arguments flattened in the reference's order (args[-1] last)."""
+    import yaml
+    E = m.enums
+    MR = m.MultiRace
+    MR.mp = types.SimpleNamespace(Pipe=lambda: (_Conn(), _Conn()), Process=_Proc)
+    with open(os.path.join(REF, "config", "getting_started.yaml")) as f:
+        cfg = sys.modules["munch"].munchify(yaml.safe_load(f))
+    N = 2
+    env = MR.MultiRaceAviary(race_config=cfg, num_drones=N, racemode=E.RaceMode.COMPARE)
+    obs, info = env.reset()
+    obs = np.asarray(obs, float)
+    uc = types.ModuleType("user_controller")          # bypass the package __init__ (SB3 imports)
+    uc.__path__ = [os.path.join(REF, "user_controller")]
+    sys.modules["user_controller"] = uc
+    uc.BaseController = importlib.import_module("user_controller.BaseController").BaseController
+    HC = importlib.import_module("user_controller.HardCodedController").HardCodedController
+    agents = []
+    for i in range(N):
+        inf = dict(info)
+        inf["delay"] = i
+        agents.append(HC(i, obs[i], inf))
+    K = int(cfg.episode_len_sec * cfg.ctrl_freq)
+    cmd = np.zeros((K, N), "<U3")
+    flat = np.zeros((K, N, 14))
+    nflat = np.zeros((K, N), np.int32)
+    for k in range(K):
+        t = k / cfg.ctrl_freq
+        for i, a in enumerate(agents):
+            c, args = a.predict(obs[i], ep_time=t)
+            v = np.concatenate([np.atleast_1d(np.asarray(x, float)).reshape(-1) for x in args]) if args else np.zeros(0)
+            cmd[k, i] = c.value
+            flat[k, i, :v.size] = v
+            nflat[k, i] = v.size
+    return {"hc_obs0": obs, "hc_cmd": cmd, "hc_flat": flat, "hc_nflat": nflat,
+            "hc_ref": np.stack([np.stack([a.ref_x, a.ref_y, a.ref_z], -1) for a in agents]),
+            "hc_ctrl_freq": np.array(cfg.ctrl_freq)}
+
+
 def logger_fixtures(pb, m):
     """utils/logger.py Logger.log / save array layout (states reordered, controls, timestamps),
     on scripted 20-d state vectors, for both the growing and the preallocated mode."""
@@ -890,6 +933,12 @@ def main():
         np.savez_compressed(path, **px)
         print("wrote", path, len(px), "arrays")
         return
+    if os.environ.get("GOLDEN_ONLY") == "hardcoded":
+        px = hardcoded_fixtures(pb, m)
+        path = os.path.join(HERE, "hardcoded_golden.npz")
+        np.savez_compressed(path, **px)
+        print("wrote", path, len(px), "arrays")
+        return
     if os.environ.get("GOLDEN_ONLY") == "pid":
         px = pid_fixtures(pb, m)
         path = os.path.join(HERE, "pid_golden.npz")
@@ -922,6 +971,10 @@ def main():
     print("wrote", path, len(px), "arrays")
     px = obswrap_fixtures(pb, m)
     path = os.path.join(HERE, "obswrap_golden.npz")
+    np.savez_compressed(path, **px)
+    print("wrote", path, len(px), "arrays")
+    px = hardcoded_fixtures(pb, m)
+    path = os.path.join(HERE, "hardcoded_golden.npz")
     np.savez_compressed(path, **px)
     print("wrote", path, len(px), "arrays")
 

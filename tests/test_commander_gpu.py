@@ -62,6 +62,23 @@ def sync_cmd(env, orc):
     env.set_command_state(torch.from_numpy(f), torch.from_numpy(i))
 
 
+CMD_GROUPS = {"sp_pos": range(0, 3), "sp_vel": range(3, 6), "sp_acc": range(6, 9), "sp_rate": range(9, 12),
+              "sp_quat": range(12, 14), "sp_yaw": range(14, 15), "c_pos": range(15, 18), "c_vel": range(18, 21),
+              "c_yaw": range(21, 22), "st_pos": range(22, 25), "st_vel": range(25, 28), "st_yaw": range(28, 29)}
+
+
+def cmd_errors(env, orc, worst=None):
+    """max |gpu - cpu| / max(|cpu|, 1e-3) per command-state field group (per-group bounds)"""
+    fg = env.get_command_state()[0].cpu().numpy().astype(np.float64)
+    fo = orc.get_command_state()[0].astype(np.float64)
+    worst = {} if worst is None else worst
+    for g, rows in CMD_GROUPS.items():
+        r = list(rows)
+        d = np.linalg.norm(fg[r] - fo[r], axis=0) / np.maximum(np.linalg.norm(fo[r], axis=0), 1e-3)
+        worst[g] = max(worst.get(g, 0.0), float(d.max()))
+    return worst
+
+
 def check_cmd(env, orc, rtol):
     fg, ig = (t.cpu().numpy() for t in env.get_command_state())
     fo, io = orc.get_command_state()
@@ -85,19 +102,23 @@ def test_commands_teacher_forced(level, N, physics, mode, precision):
     obs0 = orc.reset()
     sync(env, orc)
     sync_cmd(env, orc)
+    worst, worst_s = {}, {}
     for k in range(8):
         codes, args = encode_step(k, obs0, E, N)
         orc.command(codes, args)
         obs_o, rew_o, te_o, tr_o, _ = orc.step(None)
         obs_g, rew_g, te_g, tr_g, _ = env.step((codes, args))
         rtol = 5e-3 if precision == "fp32" else 2e-3
+        cmd_errors(env, orc, worst)
         check_cmd(env, orc, rtol)
-        check_state(env, orc, rtol)
+        for g, v in check_state(env, orc, rtol).items():
+            worst_s[g] = max(worst_s.get(g, 0.0), v)
         og = obs_g.cpu().numpy()
         np.testing.assert_allclose(og[..., :3], obs_o[..., :3], rtol=rtol, atol=1e-3)
         np.testing.assert_array_equal(te_g.cpu().numpy(), te_o)
         sync(env, orc)
         sync_cmd(env, orc)
+    print(f"\n[cmd-errors] {level} {precision} command state {worst} body {worst_s}")
     env.close()
 
 
@@ -195,4 +216,82 @@ def test_commands_after_ndarray_steps(obs_wrapper):
     if obs_wrapper:
         wenv.detach()
         assert env.obs_wrapper == 0
+    env.close()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+def test_hardcoded_controller_teacher_forced(precision):
+    """the reference's HardCodedController command stream (tests/golden/
+    hardcoded_golden.npz, made from user_controller/HardCodedController.py itself) through the
+    tensor-in command path: HardCodedCommander.predict on the device (its stream must equal the
+    fixture's) -> MultiRaceAviary.step((codes, args)) -> adrp_race_command, against the oracle given
+    the fixture's commands; teacher-forced for the whole flight (take-off, 12 s of FULLSTATE
+    setpoints, NOTIFY, LAND) on getting_started, where it passes all four gates."""
+    from gym_pybullet_adrp_amd.hardcoded import HardCodedCommander
+    from test_hardcoded import fixture_commands, G
+    E, N = 8, 2
+    env = MultiRaceAviary("getting_started", num_drones=N, racemode=RaceMode.COMPARE, num_envs=E, seed=1,
+                          autoreset=False, precision=precision)
+    orc = O.Oracle(env.cfg.copy())
+    obs, _ = env.reset()
+    orc.reset()
+    hc = HardCodedCommander(obs)
+    f = float(G["hc_ctrl_freq"])
+    worst, worst_s = {}, {}
+    rtol = 5e-3 if precision == "fp32" else 2e-3
+    for k in range(460):
+        codes, args = hc.predict(k / f)
+        want_c, want_a = fixture_commands(k, E)
+        np.testing.assert_array_equal(codes.cpu().numpy(), want_c)
+        np.testing.assert_allclose(args.cpu().numpy(), want_a, atol=1e-12)
+        orc.command(want_c, want_a)
+        obs_o, _, te_o, tr_o, _ = orc.step(None)
+        obs_g, _, te_g, tr_g, _ = env.step((codes, args))
+        if k % 10 == 0 or te_o.any():
+            cmd_errors(env, orc, worst)
+            check_cmd(env, orc, rtol)
+            for g, v in check_state(env, orc, rtol).items():
+                worst_s[g] = max(worst_s.get(g, 0.0), v)
+        np.testing.assert_array_equal(te_g.cpu().numpy(), te_o, err_msg=f"step {k}")
+        if te_o.all():
+            break
+        sync(env, orc)
+        sync_cmd(env, orc)
+    assert te_o.all(), "the scripted flight finishes the track"
+    assert env.current_gate.cpu().numpy().tolist() == [[4, 4]] * E
+    print(f"\n[cmd-errors] hardcoded {precision} steps {k + 1} command state {worst} body {worst_s}")
+    env.close()
+
+
+def test_hardcoded_controller_free_flight():
+    """no teacher forcing: 256 envs fly the device-side HardCodedCommander stream in fp64 and finish
+    the track at the step the oracle's free flight (fixture stream) finishes it, +-3 steps"""
+    from gym_pybullet_adrp_amd.hardcoded import HardCodedCommander
+    from test_hardcoded import fixture_commands, G
+    E, N = 256, 2
+    env = MultiRaceAviary("getting_started", num_drones=N, racemode=RaceMode.COMPARE, num_envs=E, seed=1,
+                          autoreset=False, precision="fp64")
+    orc = O.Oracle(MultiRaceAviary("getting_started", num_drones=N, racemode=RaceMode.COMPARE, num_envs=1,
+                                   seed=1, autoreset=False).cfg.copy())
+    obs, _ = env.reset()
+    orc.reset()
+    hc = HardCodedCommander(obs)
+    f = float(G["hc_ctrl_freq"])
+    done_o = None
+    done_g = torch.full((E,), -1, dtype=torch.int64, device=env.device)
+    for k in range(G["hc_cmd"].shape[0]):
+        if done_o is None:
+            orc.command(*fixture_commands(k))
+            _, _, te_o, _, _ = orc.step(None)
+            if te_o.any():
+                done_o = k
+        _, _, te_g, tr_g, _ = env.step(hc.predict(k / f))
+        assert not tr_g.any()
+        done_g = torch.where((done_g < 0) & te_g, k, done_g)
+        if done_o is not None and bool((done_g >= 0).all()):
+            break
+    assert done_o is not None
+    dg = done_g.cpu().numpy()
+    assert (np.abs(dg - done_o) <= 3).all(), (done_o, np.unique(dg))
+    print(f"\n[hardcoded] oracle finished at step {done_o}, gpu fp64 at {np.unique(dg)}")
     env.close()
