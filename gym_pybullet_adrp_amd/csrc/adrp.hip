@@ -274,6 +274,9 @@ static int upload_race_const(adrp_t* h) {
     if (hipMemcpy(h->cblk, &k, sizeof k, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy((char*)h->cblk + off, ticks.data(), ticks.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return ADRP_ERR_DEVICE;
+    // the nominal attitudes, with the kernels' own transcendentals (RaceConst::nom_q / nom_rpy)
+    hipLaunchKernelGGL(race_const_init_kernel<Real>, dim3(1), dim3(64), 0, 0, (RaceConst<Real>*)h->cblk);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return ADRP_ERR_DEVICE;
     return ADRP_OK;
 }
 
@@ -389,6 +392,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     if (const char* env = getenv("ADRP_RACE_HELPERS")) h->race_helpers = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RACE_QUAD")) h->race_quad = atoi(env) != 0;
     if (const char* env = getenv("ADRP_RACE_REFINE")) h->race_refine = atoi(env) != 0;
+    if (const char* env = getenv("ADRP_RACE_PREDRAW")) h->race_predraw = atoi(env) != 0;
     const int rc = race ? (h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h))
                         : (h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h));
     if (rc != ADRP_OK) return cleanup(seterr(h, rc, "constant block upload failed"));
@@ -722,6 +726,13 @@ extern "C" int adrp_race_phase_read(unsigned long long* out, int reset) {
 // rays, obs, contacts, tail, total] s_memtime cycles (RACE_WAVE), written by the last launch
 extern "C" int adrp_race_wave_read(unsigned long long* out, int n) { return wave_read_race_f32(out, n); }
 extern "C" int adrp_race_wave_read_f64(unsigned long long* out, int n) { return wave_read_race_f64(out, n); }
+#ifdef ADRP_RACE_GJK_STATS
+// capped GJK queries of the PYB / PYB_DW race kernels (race_f32.hip / race_f64.hip code objects):
+// up to `max` records of kGjkDumpF doubles; returns the count copied (-1 on error)
+extern "C" int adrp_gjk_dump_read(double* out, int max, int f64, int reset) {
+    return f64 ? gjk_dump_read_f64(out, max, reset) : gjk_dump_read_f32(out, max, reset);
+}
+#endif
 #endif
 
 extern "C" int adrp_diagnostic_contact_count(adrp_t* h, int reset) {

@@ -35,6 +35,13 @@ __device__ unsigned long long g_race_phase[32];   // [0..8] sums, [10..17] per-p
 constexpr int kWaveSlots = 16384;
 __device__ unsigned long long g_race_wave[kWaveSlots * 8];
 #define RACE_WAVE(i, dt) do { if (blockIdx.x < kWaveSlots) g_race_wave[blockIdx.x * 8 + (i)] = (unsigned long long)(dt); } while (0)
+#ifdef ADRP_RACE_GJK_STATS
+// GJK queries that reached the iteration cap: the first kGjkDumps of them (two shapes, the cut,
+// the last |v|^2 and v.w), for a CPU replay (tools/gjk_replay.py)
+constexpr int kGjkDumps = 64, kGjkDumpF = 40;
+__device__ double g_gjk_dump[kGjkDumps * kGjkDumpF];
+__device__ unsigned int g_gjk_dump_n;
+#endif
 #else
 #define RACE_MARK(var)
 #define RACE_SET(var)

@@ -38,6 +38,7 @@ struct adrp_handle {
     bool race_helpers = true;     // race fp32: helper waves (track copy, draws) (ADRP_RACE_HELPERS=0)
     bool race_quad = true;        // race: four lanes per drone (race_quad.h) (ADRP_RACE_QUAD=0: one lane)
     bool race_refine = true;      // race: support-function bounds before GJK (ADRP_RACE_REFINE=0: centre bounds only)
+    bool race_predraw = true;     // race quad: sub-step draws up front into LDS (ADRP_RACE_PREDRAW=0: in the loop)
     float* cmdf = nullptr;        // race command mode (adrp_enable_commands): [ADRP_CMD_NF][E*N]
     int32_t* cmdi = nullptr;      // [ADRP_CMD_NI][E*N]
     const double* inj_act = nullptr;    // adrp_set_noise (parity mode): caller's device arrays
@@ -146,6 +147,21 @@ int wave_read_race_f64(unsigned long long* out, int n);
         }                                                                                        \
         return ADRP_OK;                                                                          \
     }
+#ifdef ADRP_RACE_GJK_STATS
+int gjk_dump_read_f32(double* out, int max, int reset);
+int gjk_dump_read_f64(double* out, int max, int reset);
+#define ADRP_GJK_DUMP_READER(name)                                                               \
+    int name(double* out, int max, int reset) {                                                  \
+        unsigned int n = 0;                                                                      \
+        if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_gjk_dump_n), sizeof n) != hipSuccess) return -1; \
+        const int m = int(n < unsigned(kGjkDumps) ? n : unsigned(kGjkDumps));                   \
+        const int c = m < max ? m : max;                                                         \
+        if (c > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gjk_dump), size_t(c) * kGjkDumpF * sizeof(double)) \
+                         != hipSuccess) return -1;                                               \
+        if (reset) { const unsigned int z = 0; if (hipMemcpyToSymbol(HIP_SYMBOL(g_gjk_dump_n), &z, sizeof z) != hipSuccess) return -1; } \
+        return c;                                                                                \
+    }
+#endif
 #define ADRP_WAVE_READER(name)                                                                   \
     int name(unsigned long long* out, int n) {                                                   \
         if (n < 0 || n > kWaveSlots) return ADRP_ERR_INVALID;                                    \

@@ -18,5 +18,8 @@ template int race_cmd_init<float>(adrp_t*, hipStream_t);
 
 #ifdef ADRP_RACE_TIMING
 ADRP_PHASE_READER(phase_read_race_f32)
+#ifdef ADRP_RACE_GJK_STATS
+ADRP_GJK_DUMP_READER(gjk_dump_read_f32)
+#endif
 ADRP_WAVE_READER(wave_read_race_f32)
 #endif

@@ -17,5 +17,8 @@ template int race_cmd_init<double>(adrp_t*, hipStream_t);
 
 #ifdef ADRP_RACE_TIMING
 ADRP_PHASE_READER(phase_read_race_f64)
+#ifdef ADRP_RACE_GJK_STATS
+ADRP_GJK_DUMP_READER(gjk_dump_read_f64)
+#endif
 ADRP_WAVE_READER(wave_read_race_f64)
 #endif

@@ -67,6 +67,10 @@ struct RaceConst {
         init_pqr[ADRP_MAX_DRONES][3];
     Real race_mass, race_inertia[3];
     float lpf[5];   // gyro lpf2p b0, b1, b2, a1, a2 (host float, as the firmware's filter.c computes them)
+    // nominal (loadURDF) attitude of every drone: quat_from_euler_fast(init_rpy * d2r) and its
+    // euler_xyz_fast, written on the device by race_const_init_kernel after each upload (the
+    // kernels' own transcendentals, so every reset / command init reads the same bits)
+    Real nom_q[ADRP_MAX_DRONES][4], nom_rpy[ADRP_MAX_DRONES][3];
 };
 
 template <typename Real>
@@ -92,6 +96,27 @@ struct RaceArgs {
     int64_t env_offset;
     int E;
 };
+
+// nominal attitude of drone k (RaceConst::nom_q / nom_rpy)
+template <typename Real>
+__device__ __forceinline__ Q4<Real> nominal_q(const RaceConst<Real>& C, int k) {
+    return {C.nom_q[k][0], C.nom_q[k][1], C.nom_q[k][2], C.nom_q[k][3]};
+}
+template <typename Real>
+__device__ __forceinline__ V3<Real> nominal_rpy(const RaceConst<Real>& C, int k) {
+    return v3(C.nom_rpy[k][0], C.nom_rpy[k][1], C.nom_rpy[k][2]);
+}
+// fills RaceConst::nom_q / nom_rpy in the device copy of the constant block (one lane per drone)
+template <typename Real>
+__global__ void race_const_init_kernel(RaceConst<Real>* c) {
+    const int k = threadIdx.x;
+    if (k >= ADRP_MAX_DRONES) return;
+    const Real d2r = Real(0.017453292519943295);
+    const Q4<Real> q = quat_from_euler_fast(c->init_rpy[k][0] * d2r, c->init_rpy[k][1] * d2r, c->init_rpy[k][2] * d2r);
+    const V3<Real> r = euler_xyz_fast(q);
+    c->nom_q[k][0] = q.x; c->nom_q[k][1] = q.y; c->nom_q[k][2] = q.z; c->nom_q[k][3] = q.w;
+    c->nom_rpy[k][0] = r.x; c->nom_rpy[k][1] = r.y; c->nom_rpy[k][2] = r.z;
+}
 
 // ---------------------------------------------------------------------------------------
 // small helpers
@@ -245,7 +270,8 @@ __device__ __forceinline__ V3<Real> tri_closest(V3<Real> a, V3<Real> b, V3<Real>
 // Minkowski difference, so |v| >= distance, and v.w / |v| <= distance for the support point
 // w: the loop stops as soon as either bound decides against `cut`, else on convergence.
 template <typename Real>
-__device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Real>& B0, Real cut) {
+__device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
+                                                bool* undecided = nullptr) {
     // in A's centre frame: support points stay O(shape size), so the fp32 termination test
     // is not swamped by rounding of world coordinates (which stalled convergence)
     Shape<Real> A = A0, B = B0;
@@ -258,9 +284,21 @@ __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Re
     V3<Real> v = A.c - B.c;
     const Real cut2 = cut * cut;
     if (dot(v, v) < Real(1e-20)) v = v3(Real(1), Real(0), Real(0));
+    Real vv_prev = Real(3.0e38);
     for (int it = 0; it < 48; ++it) {
         const V3<Real> w = support(A, Real(-1) * v) - support(B, v);
         const Real vv = dot(v, v), vw = dot(v, w);
+        // cycling: the same |v| twice in a row is the same simplex again (fp32 near contact: a support
+        // point equal to a simplex vertex up to rounding, far above the 1e-10 m duplicate test, brings
+        // back the same triangle every iteration; tools/gjk_replay.py).  The 48-iteration cap then
+        // returned this same |v|'s answer.  (|v| may grow once: from the centre difference to the
+        // first support point, and out of a flat tetrahedron, so only equality is a cycle.)
+        if (vv == vv_prev) {
+            GJK_STAT(it + 1);
+            if (undecided) *undecided = true;
+            return vv < cut2;
+        }
+        vv_prev = vv;
         if (vw > Real(0) && vw * vw >= cut2 * vv) { GJK_STAT(it + 1); return false; }   // lower bound
         if (vv - vw <= eps * vv) { GJK_STAT(it + 1); return vv < cut2; }
         // absolute gap: the distance is known to within tol (|v| - vw/|v| <= tol).  Near contact
@@ -321,7 +359,58 @@ __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Re
         if (dot(v, v) < cut2) { GJK_STAT(it + 1); return true; }   // upper bound
     }
     GJK_STAT(48);
+    if (undecided) *undecided = true;
+#if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
+    {
+        const unsigned int k = atomicAdd(&g_gjk_dump_n, 1u);
+        if (k < unsigned(kGjkDumps)) {
+            double* o = g_gjk_dump + size_t(k) * kGjkDumpF;
+            const Shape<Real>* sh[2] = {&A0, &B0};
+            for (int j = 0; j < 2; ++j) {
+                const Shape<Real>& q = *sh[j];
+                double* p = o + 17 * j;
+                p[0] = q.c.x; p[1] = q.c.y; p[2] = q.c.z;
+                p[3] = q.R.a00; p[4] = q.R.a01; p[5] = q.R.a02; p[6] = q.R.a10; p[7] = q.R.a11; p[8] = q.R.a12;
+                p[9] = q.R.a20; p[10] = q.R.a21; p[11] = q.R.a22;
+                p[12] = q.h.x; p[13] = q.h.y; p[14] = q.h.z; p[15] = q.r; p[16] = q.cyl;
+            }
+            o[34] = cut; o[35] = dot(v, v); o[36] = double(sizeof(Real));
+        }
+    }
+#endif
     return dot(v, v) < cut2;
+}
+
+template <typename Real>
+__device__ __forceinline__ Shape<double> shape_f64(const Shape<Real>& s) {
+    Shape<double> d;
+    d.c = v3(double(s.c.x), double(s.c.y), double(s.c.z));
+    d.R = {double(s.R.a00), double(s.R.a01), double(s.R.a02), double(s.R.a10), double(s.R.a11), double(s.R.a12),
+           double(s.R.a20), double(s.R.a21), double(s.R.a22)};
+    d.h = v3(double(s.h.x), double(s.h.y), double(s.h.z));
+    d.r = double(s.r);
+    d.cyl = s.cyl;
+    return d;
+}
+
+// "distance(A, B) < cut".  A contact query (cut 1 um) that the fp32 iteration leaves undecided is
+// run again by the float64 GJK on the same float shapes: near contact the float iteration can not
+// resolve |v| against the O(0.1 m) support points and cycles one triangle (|v| 1e-6 .. 4e-4 m where
+// the oracle's distance was 0 .. 2e-4 m; tools/gjk_capped.py, tools/gjk_replay.py), so those
+// queries are decided as the oracle decides them.  Decided queries (the lower bound, the enclosed
+// origin, the upper bound, convergence) keep the float answer, and range queries (0.45 m) stay
+// float.
+template <typename Real>
+__device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Real>& B0, Real cut) {
+    if constexpr (sizeof(Real) == 4) {
+        if (cut < Real(1e-3)) {
+            bool undecided = false;
+            const bool r = gjk_within_impl<Real>(A0, B0, cut, &undecided);
+            if (__builtin_expect(!undecided, 1)) return r;
+            return gjk_within_impl<double>(shape_f64(A0), shape_f64(B0), double(cut));
+        }
+    }
+    return gjk_within_impl<Real>(A0, B0, cut);
 }
 
 // entry fraction of the segment p0 -> p1 into a cylinder, > 1 on a miss
@@ -1256,9 +1345,8 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
         st(f, RF_OBST + 3 * k + 2, EN, slot, C.obst_nom[k][2]);
     }
     // initial obs at the nominal (loadURDF) poses, at rest
-    const Real d2r = Real(0.017453292519943295);
     const V3<Real> npos = v3(C.init_pos[dn][0], C.init_pos[dn][1], C.init_pos[dn][2]);
-    const Q4<Real> nq = quat_from_euler_fast(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
+    const Q4<Real> nq = nominal_q(C, dn);
     Real row0[15];
     const V3<Real> zero = v3(Real(0), Real(0), Real(0));
     uint32_t gin, oin;
@@ -1269,14 +1357,14 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
         int idx = 0;
         for (int k = 0; k < C.N; ++k) {
             if (k == dn) continue;
-            const V3<Real> orpy = euler_xyz_fast(quat_from_euler_fast(C.init_rpy[k][0] * d2r, C.init_rpy[k][1] * d2r, C.init_rpy[k][2] * d2r));
+            const V3<Real> orpy = nominal_rpy(C, k);
             float* p = obs_row + 49 + 6 * idx;
             p[0] = float(C.init_pos[k][0]); p[1] = float(C.init_pos[k][1]); p[2] = float(C.init_pos[k][2]);
             p[3] = float(orpy.x); p[4] = float(orpy.y); p[5] = float(orpy.z);
             ++idx;
         }
     }
-    const V3<Real> nrpy = euler_xyz_fast(nq);
+    const V3<Real> nrpy = nominal_rpy(C, dn);
     // RewardWrapper.reset: current_target = obs[0, 12:15], previous_pos = obs[0, :3]
     for (int k = 0; k < 3; ++k) {   // per-env state, kept in drone 0's slot
         st(f, RF_WR_TARGET + k, EN, slot, dn == 0 && C.num_gates > 0 ? row0[3 + k] : Real(0));
@@ -1349,9 +1437,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_cmd_init_kernel(RaceArgs<Real
     const size_t slot = size_t(blockIdx.x) * kRaceBlock + threadIdx.x;
     if (slot >= EN) return;
     const int dn = int(slot % C.N);
-    const Real d2r = Real(0.017453292519943295);
-    const Q4<Real> nq = quat_from_euler_fast(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
-    const V3<Real> nrpy = euler_xyz_fast(nq);
+    const V3<Real> nrpy = nominal_rpy(C, dn);
     CmdState cs;
     hl_reset(cs, float(C.init_pos[dn][0]), float(C.init_pos[dn][1]), float(C.init_pos[dn][2]),
              float(nrpy.z * Real(57.29577951308232)));

@@ -6,7 +6,7 @@
 // four lanes per drone (race_quad.h): 16 drones per 64-lane block
 template <typename Real, int PH>
 static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
-    const bool draws = h->cfg.track.disturbances && h->S <= kRacePreS;
+    const bool draws = h->cfg.track.disturbances && h->S <= kRacePreS && h->race_predraw;
     const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G * 4 + kRaceBlock - 1) / kRaceBlock));
     auto go = [&](auto kernel) {
         if (h->prof_n < h->prof_cap) {

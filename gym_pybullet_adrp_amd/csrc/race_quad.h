@@ -400,9 +400,8 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
 #pragma unroll
         for (int k = 0; k < 3; ++k) T.v[RF_OBST - RF_GATE + 3 * o + k] = qbc(own.o[k], o);
     // initial obs at the nominal (loadURDF) pose, at rest; lane ql tests gate ql / obstacle ql
-    const Real d2r = Real(0.017453292519943295);
     const V3<Real> npos = v3(C.init_pos[dn][0], C.init_pos[dn][1], C.init_pos[dn][2]);
-    const Q4<Real> nq = quat_from_euler_fast(C.init_rpy[dn][0] * d2r, C.init_rpy[dn][1] * d2r, C.init_rpy[dn][2] * d2r);
+    const Q4<Real> nq = nominal_q(C, dn);
     const Shape<Real> ds = drone_shape(C, npos, nq);
     RESET_MARK(3);
     uint32_t gin, oin, amb, camb_all;
@@ -433,20 +432,8 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
     race_obs_row(C, T, npos, nq, zero, zero, 0, obs_row, owner, row0, gin, oin);
 #endif
     RESET_MARK(5);
-    // the nominal Euler angles of drone k (lane k % 4 computes drones ql, ql + 4)
-    V3<Real> nrpy_j[(G + 3) / 4];
-#pragma unroll
-    for (int j = 0; j < (G + 3) / 4; ++j) {
-        const int k = ql + 4 * j < C.N ? ql + 4 * j : 0;
-        nrpy_j[j] = euler_xyz_fast(quat_from_euler_fast(C.init_rpy[k][0] * d2r, C.init_rpy[k][1] * d2r, C.init_rpy[k][2] * d2r));
-    }
-    V3<Real> nrpy_k[G];
-#pragma unroll
-    for (int k = 0; k < G; ++k)
-        nrpy_k[k] = v3(qbc(nrpy_j[k / 4].x, k % 4), qbc(nrpy_j[k / 4].y, k % 4), qbc(nrpy_j[k / 4].z, k % 4));
-    V3<Real> nrpy = nrpy_k[0];
-#pragma unroll
-    for (int k = 1; k < G; ++k) nrpy = dn == k ? nrpy_k[k] : nrpy;
+    // the nominal Euler angles (RaceConst::nom_rpy, race_const_init_kernel)
+    const V3<Real> nrpy = nominal_rpy(C, dn);
     if (C.compete && owner) {   // other drones' nominal pos + rpy
         int idx = 0;
 #pragma unroll
@@ -454,7 +441,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
             if (k < C.N && k != dn) {
                 float* p = obs_row + 49 + 6 * idx;
                 p[0] = C.init_pos[k][0]; p[1] = C.init_pos[k][1]; p[2] = C.init_pos[k][2];
-                p[3] = nrpy_k[k].x; p[4] = nrpy_k[k].y; p[5] = nrpy_k[k].z;
+                p[3] = C.nom_rpy[k][0]; p[4] = C.nom_rpy[k][1]; p[5] = C.nom_rpy[k][2];
                 ++idx;
             }
         }

@@ -219,6 +219,14 @@ def test_commands_after_ndarray_steps(obs_wrapper):
     env.close()
 
 
+# The scripted flight hovers for seconds (take-off, delay), where the body rates are ~1e-4 rad/s.
+# A one-unit flip of the float firmware's int16 moment truncation between the kernel and the oracle
+# (hardware vs libm float transcendentals; both precisions run the firmware in float) moves the rates
+# by ~2e-5 rad/s within the step (measured: omega_y 2.3e-5 rad/s apart with all four RPMs identical
+# at the end of the step, fp64).  So the rates are compared relative to max(|omega|, 0.05 rad/s).
+OMEGA_FLOOR = 0.05
+
+
 @pytest.mark.parametrize("precision", ["fp32", "fp64"])
 def test_hardcoded_controller_teacher_forced(precision):
     """the reference's HardCodedController command stream (tests/golden/
@@ -243,15 +251,18 @@ def test_hardcoded_controller_teacher_forced(precision):
         codes, args = hc.predict(k / f)
         want_c, want_a = fixture_commands(k, E)
         np.testing.assert_array_equal(codes.cpu().numpy(), want_c)
-        np.testing.assert_allclose(args.cpu().numpy(), want_a, atol=1e-12)
+        # planned from the env's float32 reset obs (the reference plans from float64): 1e-8 m apart
+        np.testing.assert_allclose(args.cpu().numpy(), want_a, rtol=0, atol=1e-6)
         orc.command(want_c, want_a)
         obs_o, _, te_o, tr_o, _ = orc.step(None)
         obs_g, _, te_g, tr_g, _ = env.step((codes, args))
-        if k % 10 == 0 or te_o.any():
+        try:
             cmd_errors(env, orc, worst)
             check_cmd(env, orc, rtol)
-            for g, v in check_state(env, orc, rtol).items():
+            for g, v in check_state(env, orc, rtol, floors={"omega": OMEGA_FLOOR}).items():
                 worst_s[g] = max(worst_s.get(g, 0.0), v)
+        except AssertionError as e:
+            raise AssertionError(f"step {k} (commands {want_c[0].tolist()}): {e}") from None
         np.testing.assert_array_equal(te_g.cpu().numpy(), te_o, err_msg=f"step {k}")
         if te_o.all():
             break

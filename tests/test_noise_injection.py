@@ -121,7 +121,7 @@ def test_kernels_replay_injected_reference_draws(precision):
     torch = pytest.importorskip("torch")
     from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary
     from gym_pybullet_adrp_amd.utils.enums import Physics, RaceMode
-    from test_race_gpu import check_state, sync
+    from test_race_gpu import check_state, dw_crossing, sync
     E, N = 64, 4
     env = MultiRaceAviary("level3", num_drones=N, physics=Physics.PYB_DW, racemode=RaceMode.COMPETE, num_envs=E,
                           seed=77, autoreset=False, precision=precision)
@@ -135,14 +135,19 @@ def test_kernels_replay_injected_reference_draws(precision):
         orc.step(act)
     rngs = gym_rngs(E, 1234)
     at = torch.from_numpy(act).to(env.device)
+    names = orc.field_names()[0]
     for k in range(4):
         sync(env, orc)
+        f_before = orc.get_state()[0]
         an, fn = reference_draws(rngs, E, N, 20, env.cfg.track)
         orc.set_noise(an, fn)
         env.set_noise(an, fn)
         orc.step(act)
         env.step(at)
-        check_state(env, orc, 2e-3)
+        # float32: drones whose height crossed a partner's in this step are ill-conditioned under the
+        # reference's downwash (test_race_gpu.dw_crossing); float64 is compared everywhere
+        ex = dw_crossing(f_before, orc.get_state()[0], names, E, N) if precision == "fp32" else None
+        check_state(env, orc, 2e-3, exclude=ex)
     # the draws are really the injected ones: Philox instead changes the step
     sync(env, orc)
     f0, i0 = env.get_state()

@@ -95,7 +95,42 @@ def contact_margin(cfg, fo, names, slot):
     return best
 
 
-def check_state(env, orc, rtol=1e-4):
+def dw_crossing(f_before, f_after, names, E, N, dz_err=1e-7, force_err=1e-5):
+    """drones whose downwash is ill-conditioned in this step.  The reference's downwash
+    (BaseAviary._downwash) pushes drone i down by C1 (r / 4 dz)^2 exp(-(dxy / (C2 dz + C3))^2 / 2)
+    for every partner dz > 0 above it: singular at dz -> 0+.  A drone is flagged when a partner's
+    height crossed its own during the step (the force passed through the singularity at a sub-step
+    whose dz no finite precision reproduces), or when at either end a dz rounding of `dz_err` m
+    changes that force by more than `force_err` N.  Used for float32 closed-loop comparisons of the
+    DW physics modes only."""
+    idx = {n: k for k, n in enumerate(names)}
+    C1, C2, C3, r = 2267.18, 0.16, -0.11, 0.0231348
+
+    def sens(p, i, j):
+        dz = p[:, j, 2] - p[:, i, 2]
+        dxy = np.hypot(p[:, j, 0] - p[:, i, 0], p[:, j, 1] - p[:, i, 1])
+        with np.errstate(divide="ignore", over="ignore", invalid="ignore"):
+            f = C1 * (r / (4 * dz)) ** 2 * np.exp(-0.5 * (dxy / (C2 * dz + C3)) ** 2)
+            return np.where(dz > 0, 2 * f / dz * dz_err, 0.0), dz, dxy
+
+    pb = np.stack([f_before[idx[f"pos_{a}"]] for a in "xyz"], -1).reshape(E, N, 3)
+    pa = np.stack([f_after[idx[f"pos_{a}"]] for a in "xyz"], -1).reshape(E, N, 3)
+    out = np.zeros((E, N), bool)
+    for i in range(N):
+        for j in range(N):
+            if i != j:
+                sb, db, xb = sens(pb, i, j)
+                sa, da, xa = sens(pa, i, j)
+                crossed = (np.sign(db) != np.sign(da)) & (np.minimum(xb, xa) < 5.0)
+                out[:, i] |= crossed | (sb > force_err) | (sa > force_err)
+    return out.reshape(-1)
+
+
+def check_state(env, orc, rtol=1e-4, floors=None, exclude=None):
+    """GPU state vs the oracle's, per field group: |d| / max(|oracle|, floor) <= rtol.  `floors`
+    overrides FLOORS per group; `exclude` is a boolean mask of drone slots left out of the
+    continuous groups (documented ill-conditioned cases only)."""
+    floors = {**FLOORS, **(floors or {})}
     fg, ig = env.get_state()
     fg, ig = fg.double().cpu().numpy(), ig.cpu().numpy()
     fo, io = orc.get_state()
@@ -106,9 +141,16 @@ def check_state(env, orc, rtol=1e-4):
     for g, fields in GROUPS.items():
         rows = [idx[n] for n in fields]
         d = np.linalg.norm(fg[rows] - fo[rows], axis=0)
-        err = d / np.maximum(np.linalg.norm(fo[rows], axis=0), FLOORS[g])
+        err = d / np.maximum(np.linalg.norm(fo[rows], axis=0), floors[g])
+        if exclude is not None:
+            err = np.where(exclude, 0.0, err)
         worst[g] = float(err.max())
-        assert err.max() <= rtol, f"{g}: max rel err {err.max():.3e} at slot {err.argmax()}"
+        if err.max() > rtol:
+            s = int(err.argmax())
+            show = ("pos_z", "vel_x", "vel_y", "vel_z", "omega_x", "omega_y", "omega_z", "rpm_0", "rpm_1", "rpm_2", "rpm_3")
+            detail = {n: (round(float(fg[idx[n], s]), 7), round(float(fo[idx[n], s]), 7)) for n in show}
+            ints = {n: (int(ig[inames.index(n), s]), int(io[inames.index(n), s])) for n in ("flags", "tumble", "tick")}
+            raise AssertionError(f"{g}: max rel err {err.max():.3e} at slot {s} (gpu, cpu): {detail} {ints}")
     for k in ("step_counter", "episode", "gate", "wr_gate", "tick", "last_att_tick", "last_pos_tick"):
         np.testing.assert_array_equal(ig[inames.index(k)], io[inames.index(k)], err_msg=k)
     # elimination may differ only for a grazing contact (|distance| < 1e-4 m at the oracle state)

@@ -65,7 +65,7 @@ for level, n, phys, mode, E in CONFIGS:
         G = 1 if n <= 1 else 2 if n <= 2 else 4 if n <= 4 else 8
         nb = (E * G * 4 + 63) // 64
         wbuf = (ctypes.c_ulonglong * (nb * 8))()
-        means, maxs = [], []
+        means, maxs, slowest, pct = [], [], [], []
         done = 0.0
         env.h.profile_begin(nk)
         for k in range(nk):
@@ -76,6 +76,8 @@ for level, n, phys, mode, E in CONFIGS:
             w = np.array(list(wbuf), dtype=np.float64).reshape(nb, 8)
             means.append(w.mean(0))
             maxs.append(w.max(0))
+            slowest.append(w[int(w[:, 7].argmax())])
+            pct.append(np.percentile(w[:, 7], [50, 90, 99, 100]))
         ms = env.h.profile_end(nk)
         lib.adrp_race_phase_read(buf, 1)   # GJK counters (timing build with -DADRP_RACE_GJK_STATS)
         gv = np.array(list(buf), dtype=np.float64)
@@ -87,7 +89,9 @@ for level, n, phys, mode, E in CONFIGS:
                           "kernel_us_median": float(np.median(ms)) * 1e3,
                           "reset_env_fraction_per_step": done / nk,
                           "mean_cycles_per_wave": {p: round(x) for p, x in zip(PHASES, np.mean(means, 0))},
-                          "max_cycles_per_launch": {p: round(x) for p, x in zip(PHASES, np.mean(maxs, 0))}}),
+                          "max_cycles_per_launch": {p: round(x) for p, x in zip(PHASES, np.mean(maxs, 0))},
+                          "slowest_wave_phases": {p: round(x) for p, x in zip(PHASES, np.mean(slowest, 0))},
+                          "wave_total_p50_p90_p99_max": [round(x) for x in np.mean(pct, 0)]}),
               flush=True)
         env.close()
         continue

@@ -1,0 +1,44 @@
+"""What the auto-reset costs the race step kernel: per-launch kernel time (HIP events) with
+autoreset on vs off, same workload (bench.py's race protocol: start pose + U(+-0.3) m targets).
+
+usage: python tools/reset_ab.py [LEVEL DRONES PHYSICS MODE E PRECISION]
+"""
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary  # noqa: E402
+from gym_pybullet_adrp_amd.utils.enums import Physics, RaceMode  # noqa: E402
+
+a = sys.argv[1:] + [None] * 6
+level, n, phys, mode = a[0] or "level3", int(a[1] or 4), a[2] or "PYB_DW", a[3] or "COMPETE"
+E, prec = int(a[4] or 4096), a[5] or "fp32"
+out = {"config": f"{level} N={n} {phys} {mode} E={E} {prec}"}
+for autoreset in (True, False):
+    env = MultiRaceAviary(level, num_drones=n, physics=Physics[phys], racemode=RaceMode[mode], num_envs=E, seed=7,
+                          precision=prec, autoreset=autoreset)
+    obs0, _ = env.reset()
+    gen = torch.Generator(device=env.device)
+    gen.manual_seed(3)
+    off = torch.rand((16, E, n, 3), generator=gen, device=env.device) * 0.6 - 0.3
+    tgt = obs0[..., :3].unsqueeze(0) + off
+    tgt[..., 2] = tgt[..., 2].clamp(0.2, 1.5)
+    acts = torch.cat([tgt, torch.zeros((16, E, n, 1), device=env.device)], -1).contiguous()
+    for k in range(60):
+        env.step(acts[k % 16])
+    torch.cuda.synchronize()
+    nk = 300
+    env.h.profile_begin(nk)
+    done = 0
+    for k in range(nk):
+        _, _, te, tr, _ = env.step(acts[k % 16])
+        done += int((te | tr).sum())
+    ms = np.asarray(env.h.profile_end(nk)) * 1e3
+    out["autoreset" if autoreset else "no_autoreset"] = {
+        "kernel_us_mean": float(ms.mean()), "median": float(np.median(ms)), "p90": float(np.percentile(ms, 90)),
+        "min": float(ms.min()), "max": float(ms.max()), "done_envs_per_step": done / nk, "kernel": env.kernel_name}
+    env.close()
+print(json.dumps(out), flush=True)
