@@ -640,6 +640,8 @@ def main():
                                            graph_only=go)
             cf["config3_policy"] = bench_race("level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2,
                                               policy_spec="example", graph_only=go)
+            cf["config3_policy_f32"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
+                                                  policy_spec="example", graph_only=go)
             other = "fp32" if args.precision == "fp64" else "fp64"
             r2, _ = bench_hover(args, other, E, min(K, 1000), min(W, 100), 1, 0, local)
             r2.update({"workload": f"the `value` workload with the {other} kernel", "unit": "env-steps/s",

@@ -262,10 +262,19 @@ static RaceConst<Real> race_const(const adrp_config& c) {
     return k;
 }
 
+// the race drone's physical constants are race_cf2x_phys' bit for bit (the four-lane kernel's literals)
+template <typename Real>
+static bool race_is_cf2x(const RaceConst<Real>& rt) {
+    RaceConst<Real> ct = rt;
+    race_cf2x_phys(ct);
+    return memcmp(&rt, &ct, sizeof rt) == 0;
+}
+
 template <typename Real>
 static int upload_race_const(adrp_t* h) {
     RaceConst<Real> k = race_const<Real>(h->cfg);
     k.refine = h->race_refine ? 1 : 0;
+    h->race_cf2x = race_is_cf2x(k);
     // [RaceConst | tick-schedule tables (att, pos)] (race_args)
     std::vector<uint32_t> ticks(2 * kTickWords);
     race_tick_tables(ticks.data(), ticks.data() + kTickWords);
@@ -288,7 +297,8 @@ extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
     const int p = cfg->physics >= 0 && cfg->physics <= 5 ? cfg->physics : 0;
     if (cfg->task == ADRP_TASK_RACE) {
         const char* q = getenv("ADRP_RACE_QUAD");
-        const bool quad = !(q && atoi(q) == 0);
+        const bool cf2x = cfg->precision ? race_is_cf2x(race_const<double>(*cfg)) : race_is_cf2x(race_const<float>(*cfg));
+        const bool quad = !(q && atoi(q) == 0) && (cf2x || !cfg->precision);
         snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s>", cfg->precision ? "f64" : "f32", ph[p],
                  race_group(cfg->num_drones), quad ? ",Q4" : "");
         return buf;
@@ -316,7 +326,7 @@ extern "C" const char* adrp_handle_kernel_name(const adrp_t* h) {
     const char* prec = h->real_size == 8 ? "f64" : "f32";
     if (h->cmdf) snprintf(buf, sizeof buf, "race_step<%s,%s,G8,CMD>", prec, ph[p]);
     else snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s>", prec, ph[p], race_group(h->N),
-                  h->race_quad ? ",Q4" : "");
+                  h->race_quad && (h->race_cf2x || h->real_size == 4) ? ",Q4" : "");
     return buf;
 }
 

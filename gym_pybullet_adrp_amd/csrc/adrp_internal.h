@@ -38,6 +38,7 @@ struct adrp_handle {
     bool race_helpers = true;     // race fp32: helper waves (track copy, draws) (ADRP_RACE_HELPERS=0)
     bool race_quad = true;        // race: four lanes per drone (race_quad.h) (ADRP_RACE_QUAD=0: one lane)
     bool race_refine = true;      // race: support-function bounds before GJK (ADRP_RACE_REFINE=0: centre bounds only)
+    bool race_cf2x = false;       // race: the physical constants are race_cf2x_phys' (the quad kernel's literals)
     bool race_predraw = true;     // race quad: sub-step draws up front into LDS (ADRP_RACE_PREDRAW=0: in the loop)
     float* cmdf = nullptr;        // race command mode (adrp_enable_commands): [ADRP_CMD_NF][E*N]
     int32_t* cmdi = nullptr;      // [ADRP_CMD_NI][E*N]

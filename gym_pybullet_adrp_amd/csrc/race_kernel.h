@@ -29,7 +29,10 @@ constexpr int kRacePreS = 32;       // sub-steps per env.step whose draws fit th
 // GJK call counts (global atomics from every lane that runs a GJK: they inflate the phase times, so
 // they are a separate opt-in of the timing build)
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
-#define GJK_STAT(n) do { atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
+// this workgroup's GJK iterations (the four-lane kernel reports them in its "contacts" wave slot)
+__shared__ unsigned int g_gjk_wave_iters;
+#define GJK_STAT(n) do { atomicAdd(&g_gjk_wave_iters, (unsigned int)(n)); \
+        atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
         atomicMax(&g_race_phase[19], (unsigned long long)(n)); \
         if (cut < Real(1e-3)) { atomicAdd(&g_race_phase[20], 1ull); atomicMax(&g_race_phase[21], (unsigned long long)(n)); } \
         if ((n) >= 48) atomicAdd(&g_race_phase[22], 1ull); } while (0)
@@ -96,6 +99,27 @@ struct RaceArgs {
     int64_t env_offset;
     int E;
 };
+
+// The physical constants of the reference's race drone (cf2x.urdf at PYB_FREQ 500, BaseAviary.py:
+// 117-128, 792-818): the float64 results of the host's race_const for that drone, so the host can
+// check its runtime block against them bit for bit (race_is_cf2x, adrp.hip) and the four-lane
+// kernel then compiles them in as literals (no SGPRs held or spilled across the sub-step loop).
+template <typename Real>
+__host__ __device__ constexpr void race_cf2x_phys(RaceConst<Real>& k) {
+    k.dt = Real(1.0 / 500); k.gravity = Real(9.8); k.kf = Real(3.16e-10); k.km = Real(7.94e-12);
+    k.px[0] = Real(0.028); k.px[1] = Real(-0.028); k.px[2] = Real(-0.028); k.px[3] = Real(0.028);
+    k.py[0] = Real(0.028); k.py[1] = Real(0.028); k.py[2] = Real(-0.028); k.py[3] = Real(-0.028);
+    k.pz[0] = Real(0); k.pz[1] = Real(0); k.pz[2] = Real(0); k.pz[3] = Real(0);
+    k.gnd_kf = Real(3.16e-10 * 11.36859); k.prop_r4 = Real(0.0231348 / 4); k.gnd_clip = Real(0.03776371349209501);
+    k.drag[0] = Real(9.1785e-7); k.drag[1] = Real(9.1785e-7); k.drag[2] = Real(1.0311e-6);
+    k.dw1 = Real(2267.18); k.dw2 = Real(0.16); k.dw3 = Real(-0.11); k.prop_r = Real(0.0231348);
+    k.dyn_mass = Real(0.03454); k.dyn_inv_mass = Real(1.0 / 0.03454);
+    k.dyn_i[0] = Real(1.4e-5); k.dyn_i[1] = Real(1.4e-5); k.dyn_i[2] = Real(2.17e-5);
+    k.dyn_inv_i[0] = Real(1.0 / 1.4e-5); k.dyn_inv_i[1] = Real(1.0 / 1.4e-5); k.dyn_inv_i[2] = Real(1.0 / 2.17e-5);
+    k.dyn_arm = Real(0.028072139213105935);
+    k.coll_hh = Real(0.5 * 0.025); k.coll_r = Real(0.06); k.coll_zoff = Real(0);
+    k.ang_max = Real(0.5 * (3.14159265358979323846 / 2) * 500);
+}
 
 // nominal attitude of drone k (RaceConst::nom_q / nom_rpy)
 template <typename Real>
@@ -400,6 +424,12 @@ __device__ __forceinline__ Shape<double> shape_f64(const Shape<Real>& s) {
 // queries are decided as the oracle decides them.  Decided queries (the lower bound, the enclosed
 // origin, the upper bound, convergence) keep the float answer, and range queries (0.45 m) stay
 // float.
+// out of line: one copy per code object for the rare rerun (inlined at the three query sites it
+// grew the fp32 kernels by ~10 % of code and made them no faster; tools/gpu_r3_t16.sh)
+__device__ __noinline__ bool gjk_within_f64_call(Shape<double> A, Shape<double> B, double cut) {
+    return gjk_within_impl<double>(A, B, cut);
+}
+
 template <typename Real>
 __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Real>& B0, Real cut) {
     if constexpr (sizeof(Real) == 4) {
@@ -407,7 +437,7 @@ __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Re
             bool undecided = false;
             const bool r = gjk_within_impl<Real>(A0, B0, cut, &undecided);
             if (__builtin_expect(!undecided, 1)) return r;
-            return gjk_within_impl<double>(shape_f64(A0), shape_f64(B0), double(cut));
+            return gjk_within_f64_call(shape_f64(A0), shape_f64(B0), double(cut));
         }
     }
     return gjk_within_impl<Real>(A0, B0, cut);

@@ -3,6 +3,11 @@
 
 #include "adrp_internal.h"
 
+// the quad kernel's physical constants are compiled in (race_cf2x_phys) for fp64, where that took
+// config 4 from 98.2 to 95.5 us; for fp32 it measured 0.5 us slower (tools/gpu_r3_t17.sh)
+template <typename Real>
+constexpr bool kQuadDef = sizeof(Real) == 8;
+
 // four lanes per drone (race_quad.h): 16 drones per 64-lane block
 template <typename Real, int PH>
 static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
@@ -20,11 +25,11 @@ static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t
         constexpr bool D = decltype(dr)::value;
         switch (G) {
 #ifndef ADRP_DEV_FAST
-            case 1: go(race_step_q4<Real, PH, 1, D>); break;
-            case 8: go(race_step_q4<Real, PH, 8, D>); break;
+            case 1: go(race_step_q4<Real, PH, 1, D, kQuadDef<Real>>); break;
+            case 8: go(race_step_q4<Real, PH, 8, D, kQuadDef<Real>>); break;
 #endif
-            case 2: go(race_step_q4<Real, PH, 2, D>); break;
-            default: go(race_step_q4<Real, PH, 4, D>); break;
+            case 2: go(race_step_q4<Real, PH, 2, D, kQuadDef<Real>>); break;
+            default: go(race_step_q4<Real, PH, 4, D, kQuadDef<Real>>); break;
         }
     };
     if (draws) by_g(std::true_type{});
@@ -49,7 +54,9 @@ static void launch_race_cmd(const RaceArgs<Real>& a, hipStream_t s, adrp_t* h) {
 template <typename Real, int PH>
 static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
     if (h->cmdf) return launch_race_cmd<Real, PH>(a, s, h);
-    if (h->race_quad) return launch_race_q4<Real, PH>(a, G, s, h);
+    // the fp64 four-lane kernel has the reference drone's physical constants compiled in: another
+    // drone (or PYB_FREQ) runs the one-lane kernel there
+    if (h->race_quad && (h->race_cf2x || !kQuadDef<Real>)) return launch_race_q4<Real, PH>(a, G, s, h);
     // kRaceBlock drone lanes, + kRaceHelpers helper waves per block in the fp32 kernel (the track
     // copy into LDS, and the sub-step draws with disturbances on; race_kernel.h)
     const int helpers = sizeof(Real) != 4 || !h->race_helpers ? 0

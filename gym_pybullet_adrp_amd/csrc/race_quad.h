@@ -540,7 +540,7 @@ __device__ __forceinline__ void quad_draws(const RaceConst<Real>& H, float* pre_
 // Block = 64 lanes = 16 drones (kQuadDrones); one wave.  DRAWS: the disturbance draws of the
 // step's S <= kRacePreS sub-steps go through LDS (disturbances on); else none are needed, or (S
 // larger) each lane draws in the loop.
-template <typename Real, int PH, int G, bool DRAWS>
+template <typename Real, int PH, int G, bool DRAWS, bool DEF>
 __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     constexpr bool F32 = sizeof(Real) == 4;
     RACE_MARK(t0);
@@ -569,19 +569,22 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     const int cax = ql < 3 ? ql : 2;                     // this lane's Euler axis
     RaceConst<Real> H;
     H.S = CG.S; H.link_lag = CG.link_lag; H.disturbances = CG.disturbances;
-    H.dt = CG.dt; H.gravity = CG.gravity; H.kf = CG.kf; H.km = CG.km;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { H.px[i] = CG.px[i]; H.py[i] = CG.py[i]; H.pz[i] = CG.pz[i]; }
-    H.gnd_kf = CG.gnd_kf; H.prop_r4 = CG.prop_r4; H.gnd_clip = CG.gnd_clip;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        H.drag[i] = CG.drag[i]; H.dist_lo[i] = CG.dist_lo[i]; H.dist_hi[i] = CG.dist_hi[i];
-        H.dyn_i[i] = CG.dyn_i[i]; H.dyn_inv_i[i] = CG.dyn_inv_i[i];
-    }
-    H.dw1 = CG.dw1; H.dw2 = CG.dw2; H.dw3 = CG.dw3; H.prop_r = CG.prop_r;
-    H.dyn_mass = CG.dyn_mass; H.dyn_inv_mass = CG.dyn_inv_mass; H.dyn_arm = CG.dyn_arm;
-    H.coll_hh = CG.coll_hh; H.coll_r = CG.coll_r; H.coll_zoff = CG.coll_zoff; H.ang_max = CG.ang_max;
+    for (int i = 0; i < 3; ++i) { H.dist_lo[i] = CG.dist_lo[i]; H.dist_hi[i] = CG.dist_hi[i]; }
     H.noise_std = CG.noise_std;
+    if constexpr (DEF) {   // the reference's race drone: the physical constants as literals
+        race_cf2x_phys(H);
+    } else {
+        H.dt = CG.dt; H.gravity = CG.gravity; H.kf = CG.kf; H.km = CG.km;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { H.px[i] = CG.px[i]; H.py[i] = CG.py[i]; H.pz[i] = CG.pz[i]; }
+        H.gnd_kf = CG.gnd_kf; H.prop_r4 = CG.prop_r4; H.gnd_clip = CG.gnd_clip;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { H.drag[i] = CG.drag[i]; H.dyn_i[i] = CG.dyn_i[i]; H.dyn_inv_i[i] = CG.dyn_inv_i[i]; }
+        H.dw1 = CG.dw1; H.dw2 = CG.dw2; H.dw3 = CG.dw3; H.prop_r = CG.prop_r;
+        H.dyn_mass = CG.dyn_mass; H.dyn_inv_mass = CG.dyn_inv_mass; H.dyn_arm = CG.dyn_arm;
+        H.coll_hh = CG.coll_hh; H.coll_r = CG.coll_r; H.coll_zoff = CG.coll_zoff; H.ang_max = CG.ang_max;
+    }
     const int lb = xcd_block(blockIdx.x, gridDim.x);     // logical block (XCD-aware order)
     const int dl = lb * kQuadDrones + qd;                // drone lane of the one-lane layout
     const int e_raw = dl / G, d_raw = dl % G;
@@ -627,6 +630,9 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     }
     const Lpf lpf = {CG.lpf[0], CG.lpf[1], CG.lpf[2], CG.lpf[3], CG.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
     const bool inj = a.inj_force != nullptr;   // parity mode: the caller's draws, read in the loop
+#if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
+    if (threadIdx.x == 0) g_gjk_wave_iters = 0;
+#endif
     if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
         if (!inj) quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
         __syncthreads();
@@ -800,11 +806,23 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     uint32_t gin, oin;
     uint32_t amb, camb_all;
     bool ccert;
+#ifdef ADRP_OBS_PHASES
+    RACE_MARK(o0);
+#endif
     track_bounds_q4(C, T, ds, Real(0.45), Real(1e-6), ql, !(d.flags & 1), gin, oin, amb, camb_all, ccert);
+#ifdef ADRP_OBS_PHASES
+    RACE_MARK(o1);
+#endif
     bool crashed = track_gjk_pool<Real, TrackSrcQ<Real>, 2>(C, T, ds, owner, Real(0.45), Real(1e-6), gin, oin, amb, camb_all,
                                                      tjobs, tl, G, N, a.E) || ccert;
+#ifdef ADRP_OBS_PHASES
+    RACE_MARK(o2);
+#endif
     V3<Real> rpy;
     race_obs_row(C, T, d.pos, d.q, d.vel, wv, d.gate, row, owner, row0, gin, oin, &rpy);
+#ifdef ADRP_OBS_PHASES
+    RACE_MARK(o3);
+#endif
     if (C.compete) {   // other drones' pos + rpy (653-659): the rpy of their own obs rows
         V3<Real> grpy[ADRP_MAX_DRONES];
 #pragma unroll
@@ -910,7 +928,14 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         for (int k = 0; k < 8; ++k) RACE_WAVE(k, reset ? g_reset_mark[k + 1] - g_reset_mark[k] : 0);
 #else
         RACE_WAVE(0, t1 - t0); RACE_WAVE(1, acc_phys); RACE_WAVE(2, (t2 - t1) - acc_phys); RACE_WAVE(3, t3 - t2);
+#if defined(ADRP_OBS_PHASES)   // measurement-only: the obs phase split (bounds, GJK pool, row, compete rows)
+        RACE_WAVE(0, o1 - o0); RACE_WAVE(1, o2 - o1); RACE_WAVE(2, o3 - o2); RACE_WAVE(3, t4 - o3);
         RACE_WAVE(4, t4 - t3); RACE_WAVE(5, t5 - t4); RACE_WAVE(6, t6 - t5); RACE_WAVE(7, t6 - t0);
+#elif defined(ADRP_RACE_GJK_STATS)   // the "contacts" slot: this workgroup's GJK iterations
+        RACE_WAVE(4, t4 - t3); RACE_WAVE(5, g_gjk_wave_iters); RACE_WAVE(6, t6 - t5); RACE_WAVE(7, t6 - t0);
+#else
+        RACE_WAVE(4, t4 - t3); RACE_WAVE(5, t5 - t4); RACE_WAVE(6, t6 - t5); RACE_WAVE(7, t6 - t0);
+#endif
 #endif
     }
 #endif

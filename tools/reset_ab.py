@@ -2,7 +2,10 @@
 autoreset on vs off, same workload (bench.py's race protocol: start pose + U(+-0.3) m targets).
 
 usage: python tools/reset_ab.py [LEVEL DRONES PHYSICS MODE E PRECISION]
+       RACE_POLICY=example: closed loop with the on-device PPO actor instead of fixed targets;
+       AB_ONLY=autoreset: only the auto-reset leg (library A/B: ADRP_LIB=...)
 """
+import os
 import json
 import sys
 
@@ -16,8 +19,11 @@ from gym_pybullet_adrp_amd.utils.enums import Physics, RaceMode  # noqa: E402
 a = sys.argv[1:] + [None] * 6
 level, n, phys, mode = a[0] or "level3", int(a[1] or 4), a[2] or "PYB_DW", a[3] or "COMPETE"
 E, prec = int(a[4] or 4096), a[5] or "fp32"
-out = {"config": f"{level} N={n} {phys} {mode} E={E} {prec}"}
-for autoreset in (True, False):
+out = {"config": f"{level} N={n} {phys} {mode} E={E} {prec}" + (" actor" if os.environ.get("RACE_POLICY") else "")}
+legs = (True,) if os.environ.get("AB_ONLY") == "autoreset" else (True, False)
+out["lib"] = os.path.basename(os.environ.get("ADRP_LIB", "libadrp.so"))
+pol = os.environ.get("RACE_POLICY")
+for autoreset in legs:
     env = MultiRaceAviary(level, num_drones=n, physics=Physics[phys], racemode=RaceMode[mode], num_envs=E, seed=7,
                           precision=prec, autoreset=autoreset)
     obs0, _ = env.reset()
@@ -27,14 +33,25 @@ for autoreset in (True, False):
     tgt = obs0[..., :3].unsqueeze(0) + off
     tgt[..., 2] = tgt[..., 2].clamp(0.2, 1.5)
     acts = torch.cat([tgt, torch.zeros((16, E, n, 1), device=env.device)], -1).contiguous()
+    if pol:
+        from bench import make_policy
+        policy = make_policy(pol, env.device.index or 0)
+        pact = torch.empty((E, n, 4), device=env.device)
+
+        def step(k):
+            policy.act(env._obs, out=pact)
+            return env.step(pact)
+    else:
+        def step(k):
+            return env.step(acts[k % 16])
     for k in range(60):
-        env.step(acts[k % 16])
+        step(k)
     torch.cuda.synchronize()
     nk = 300
     env.h.profile_begin(nk)
     done = 0
     for k in range(nk):
-        _, _, te, tr, _ = env.step(acts[k % 16])
+        _, _, te, tr, _ = step(k)
         done += int((te | tr).sum())
     ms = np.asarray(env.h.profile_end(nk)) * 1e3
     out["autoreset" if autoreset else "no_autoreset"] = {
