@@ -575,6 +575,41 @@ __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, s
     for (int k = 0; k < 3; ++k) d.inv_i[k] = Real(1) / d.inertia[k];
 }
 
+// store_drone split in two for the four-lane kernel: everything the sub-step loop leaves final
+// (stored right after the loop, so those registers are free for the post-loop queries), then the
+// gate / flags the post-loop phases still change
+template <typename Real>
+__device__ __forceinline__ void store_drone_body(const RaceArgs<Real>& a, size_t EN, size_t slot, const RDrone<Real>& d) {
+    Real* f = a.f;
+#define S_(k, v) st(f, (k), EN, slot, Real(v))
+    S_(RF_POS, d.pos.x); S_(RF_POS + 1, d.pos.y); S_(RF_POS + 2, d.pos.z);
+    S_(RF_QUAT, d.q.x); S_(RF_QUAT + 1, d.q.y); S_(RF_QUAT + 2, d.q.z); S_(RF_QUAT + 3, d.q.w);
+    S_(RF_VEL, d.vel.x); S_(RF_VEL + 1, d.vel.y); S_(RF_VEL + 2, d.vel.z);
+    S_(RF_OMEGA, d.w.x); S_(RF_OMEGA + 1, d.w.y); S_(RF_OMEGA + 2, d.w.z);
+    S_(RF_ANGV, d.angv.x); S_(RF_ANGV + 1, d.angv.y); S_(RF_ANGV + 2, d.angv.z);
+    S_(RF_LINK_QUAT, d.ql.x); S_(RF_LINK_QUAT + 1, d.ql.y); S_(RF_LINK_QUAT + 2, d.ql.z); S_(RF_LINK_QUAT + 3, d.ql.w);
+    S_(RF_LINK_POS, d.lpos.x); S_(RF_LINK_POS + 1, d.lpos.y); S_(RF_LINK_POS + 2, d.lpos.z);
+    S_(RF_KIN_POS, d.kpos.x); S_(RF_KIN_POS + 1, d.kpos.y); S_(RF_KIN_POS + 2, d.kpos.z);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { S_(RF_RPM + k, d.rpm[k]); S_(RF_PREV_RPM + k, d.prev[k]); S_(RF_CTL + k, d.ctl[k]); }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        S_(RF_PREV_RPY + k, d.prev_rpy[k]); S_(RF_PREV_VEL + k, d.prev_vel[k]);
+        S_(RF_LPF_D1 + k, d.lpf1[k]); S_(RF_LPF_D2 + k, d.lpf2[k]);
+        S_(RF_I_ERR + k, d.ierr[k]); S_(RF_I_ERR_M + k, d.ierrm[k]);
+    }
+    S_(RF_PREV_OMEGA_ROLL, d.pw_roll); S_(RF_PREV_OMEGA_PITCH, d.pw_pitch);
+    S_(RF_PREV_SP_ROLL, d.psp_roll); S_(RF_PREV_SP_PITCH, d.psp_pitch);
+#undef S_
+    int32_t* ist = a.ist;
+    ist[RI_TICK * EN + slot] = d.tick; ist[RI_LAST_ATT * EN + slot] = d.last_att;
+    ist[RI_LAST_POS * EN + slot] = d.last_pos; ist[RI_TUMBLE * EN + slot] = d.tumble;
+}
+template <typename Real>
+__device__ __forceinline__ void store_drone_flags(const RaceArgs<Real>& a, size_t EN, size_t slot, const RDrone<Real>& d) {
+    a.ist[RI_GATE * EN + slot] = d.gate; a.ist[RI_FLAGS * EN + slot] = d.flags;
+}
+
 template <typename Real>
 __device__ __forceinline__ void store_drone(const RaceArgs<Real>& a, size_t EN, size_t slot, const RDrone<Real>& d,
                                             bool params) {

@@ -670,6 +670,8 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
 #pragma unroll
                 for (int j = 0; j < (G + 3) / 4; ++j) {
                     const int k = ql + 4 * j;
+                    // ds_bpermute: DPP row broadcasts of the four partners' positions (row_newbcast +
+                    // selects) measured 2.5-3 us slower on config 4 (tools/gpu_r3_t20.sh)
                     const int src = (tl & ~(4 * G - 1)) + 4 * (k < G ? k : 0);
                     const Real ox = __shfl(d.pos.x, src), oy = __shfl(d.pos.y, src), oz = __shfl(d.pos.z, src);
                     const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
@@ -745,6 +747,12 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         d.lpf1[k] = qbc(l1, k);
         d.lpf2[k] = qbc(l2, k);
     }
+    // the state the post-loop phases do not change goes out now, so its registers are free for the
+    // track queries (the GJK path spilled to scratch under the live drone state); a done env's
+    // auto-reset overwrites it below
+#ifndef ADRP_EXP_LATE_STORE   // measurement-only: the round-2 single store at the end
+    if (owner) store_drone_body(a, EN, slot, d);
+#endif
 #pragma unroll
     for (int i = 0; i < (kTrackFields + 3) / 4; ++i) {
         const int k = ql + 4 * i;
@@ -910,15 +918,21 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
             a.term[e] = te;
             a.trunc[e] = tr;
         }
-        if (reset && a.tobs) {
-            float* trow = a.tobs + slot * size_t(C.D);
-            for (int k = 0; k < C.D; ++k) trow[k] = row[k];
-        }
         if (!reset) {
-            store_drone(a, EN, slot, d, false);
+#ifdef ADRP_EXP_LATE_STORE
+            store_drone_body(a, EN, slot, d);
+#endif
+            store_drone_flags(a, EN, slot, d);
             a.ist[RI_STEP * EN + slot] = sc0 + C.S;
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
         }
+    }
+    if (reset && a.tobs && e_raw < a.E) {   // terminal obs: the env's N rows, copied by its 4G lanes
+        const int nl = 4 * G, li = tl & (nl - 1);
+        const float* src = rows + (qd / G) * N * C.D;
+        float* dst = a.tobs + size_t(e) * N * C.D;
+        const int n = N * C.D;
+        for (int k = li; k < n; k += nl) dst[k] = src[k];
     }
     if (reset) race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, row, ResetToHBM<Real>{&a});
 #ifdef ADRP_RACE_TIMING
