@@ -571,6 +571,15 @@ def bench_sb3_loop(args, dev, E=ENVS_PER_GPU, K=200, W=20):
     return rec
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """one stderr line per finished part (a long default run shows it is alive; stdout stays the one
+    JSON line)"""
+    print(f"[bench {time.perf_counter() - _T0:6.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -619,6 +628,7 @@ def main():
                                   "global_envs": E * world, "drones_per_env": 1,
                                   "parallelism": f"env-sharded dp{world}"}})
         result.update(rec)
+    progress("main line")
 
     if not args.no_configs and args.task == "hover":
         cf = {}
@@ -628,28 +638,39 @@ def main():
         # `strong`: the 32,768 envs of config 5 in total over the N GPUs
         cf["config5"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp64", 4096, RK, RW, world, rank, local, 4,
                                    sharded_gather=gather, graph_only=go)
+        progress("config5")
         cf["config5"]["strong"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp64", None, RK, RW, world, rank,
                                              local, 4, graph_only=go, global_envs=8 * 4096)
+        progress("config5 strong")
         cf["config5_f32"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp32", 4096, RK, RW, world, rank, local, 4,
                                        sharded_gather=gather, graph_only=go)
         if world == 1:
+            progress("config5_f32")
             cf["config4_gnd_drag_dw"] = bench_race("level3", 4, "PYB_GND_DRAG_DW", "COMPETE", "fp64", 4096, RK, RW, 1,
                                                    0, local, 4, graph_only=go)
+            progress("config4_gnd_drag_dw")
             cf["config3"] = bench_race("level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2, graph_only=go)
+            progress("config3")
             cf["config3_f32"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
                                            graph_only=go)
+            progress("config3_f32")
             cf["config3_policy"] = bench_race("level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2,
                                               policy_spec="example", graph_only=go)
+            progress("config3_policy")
             cf["config3_policy_f32"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
                                                   policy_spec="example", graph_only=go)
+            progress("config3_policy_f32")
             other = "fp32" if args.precision == "fp64" else "fp64"
             r2, _ = bench_hover(args, other, E, min(K, 1000), min(W, 100), 1, 0, local)
             r2.update({"workload": f"the `value` workload with the {other} kernel", "unit": "env-steps/s",
                        "dtype": "f32" if other == "fp32" else "f64"})
             cf[f"config2_{'f32' if other == 'fp32' else 'f64'}"] = r2
+            progress("config2 other precision")
             if not go:
                 cf["config1"] = bench_config1(args, local, args.cpu_seconds, not args.no_cpu_baseline)
+                progress("config1")
                 cf["config2_sb3_vecenv"] = bench_sb3_loop(args, local)
+                progress("config2_sb3_vecenv")
         result["configs"] = cf
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -657,6 +678,7 @@ def main():
             result["cpu_baseline"] = cpu_baseline(race_cfg_of(args), args.cpu_seconds, race=True)
         else:
             result["cpu_baseline"] = cpu_baseline(hover_cfg, args.cpu_seconds)
+            progress("cpu baseline")
             if "configs" in result:
                 from gym_pybullet_adrp_amd.envs.race import race_config
                 for name, lv, n, ph, md in (("config5", "level3", 4, "PYB_DW", "COMPETE"),
@@ -664,6 +686,7 @@ def main():
                                             ("config4_gnd_drag_dw", "level3", 4, "PYB_GND_DRAG_DW", "COMPETE")):
                     c = race_config(lv, n, ph, md)
                     result["configs"][name]["cpu_baseline"] = cpu_baseline(c, args.cpu_seconds / 2, race=True)
+                    progress(f"cpu baseline {name}")
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:

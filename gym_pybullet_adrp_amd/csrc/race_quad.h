@@ -748,11 +748,13 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         d.lpf2[k] = qbc(l2, k);
     }
     // the state the post-loop phases do not change goes out now, so its registers are free for the
-    // track queries (the GJK path spilled to scratch under the live drone state); a done env's
-    // auto-reset overwrites it below
-#ifndef ADRP_EXP_LATE_STORE   // measurement-only: the round-2 single store at the end
-    if (owner) store_drone_body(a, EN, slot, d);
-#endif
+    // track queries and the reset (a done env's auto-reset overwrites it below)
+    // fp64: config 4 95 -> 80.5 us; fp32 keeps the store at the end (0.5 us faster there;
+    // tools/gpu_r3_t21.sh)
+    constexpr bool kEarlyStore = !F32;
+    if constexpr (kEarlyStore) {
+        if (owner) store_drone_body(a, EN, slot, d);
+    }
 #pragma unroll
     for (int i = 0; i < (kTrackFields + 3) / 4; ++i) {
         const int k = ql + 4 * i;
@@ -919,9 +921,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
             a.trunc[e] = tr;
         }
         if (!reset) {
-#ifdef ADRP_EXP_LATE_STORE
-            store_drone_body(a, EN, slot, d);
-#endif
+            if constexpr (!kEarlyStore) store_drone_body(a, EN, slot, d);
             store_drone_flags(a, EN, slot, d);
             a.ist[RI_STEP * EN + slot] = sc0 + C.S;
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;

@@ -60,7 +60,8 @@ def valu(out_path, rest):
                     + c["SQ_INSTS_VALU_TRANS_F32"])
         # GRBM_GUI_ACTIVE is summed over the 8 XCDs in the per-dispatch record: per-XCD cycles = / 8
         busy = c["SQ_ACTIVE_INST_VALU"] / (CUS * c["GRBM_GUI_ACTIVE"] / 8) if c["GRBM_GUI_ACTIVE"] else None
-        rec[key] = {"kernel": kernel, "flops_per_launch": flops, "flops_instruction_mix_estimate": mix,
+        keep = {k: v for k, v in rec.get(key, {}).items() if k.startswith("algorithmic_")}   # the flop model
+        rec[key] = {**keep, "kernel": kernel, "flops_per_launch": flops, "flops_instruction_mix_estimate": mix,
                     "valu_insts_per_launch": c["SQ_INSTS_VALU"], "valu_busy": busy, "counters": c,
                     "method": "rocprofv3 --pmc, two passes (FLOPS counters; instruction mix + busy); median over "
                               "dispatches after the first 8"}
