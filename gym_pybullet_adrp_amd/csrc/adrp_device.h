@@ -129,6 +129,24 @@ __device__ __forceinline__ double rsq(double x) {
     }
     return __builtin_isfinite(y) ? y : y0;
 }
+// rcp / rsq without the non-finite fix-up (3 ops each), for arguments known finite and non-zero on
+// the lanes that use the result (the quaternion norm ~1; 1/|w| under an |w| >= 0.001 select)
+__device__ __forceinline__ double rcp_nc(double x) {
+    const double y0 = __builtin_amdgcn_rcp(x);
+    double e = fma_(-x, y0, 1.0);
+    double y = fma_(y0, e, y0);
+    e = fma_(-x, y, 1.0);
+    return fma_(y, e, y);
+}
+__device__ __forceinline__ double rsq_nc(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double e = fma_(-x * y, y, 1.0);
+        y = fma_(0.5 * y, e, y);
+    }
+    return y;
+}
 // sqrt(x), x >= 0: Goldschmidt on v_rsq_f64 (g -> sqrt x, h -> 1/(2 sqrt x)) + a final residual step
 __device__ __forceinline__ double sqrt(double x) {
     const double y = __builtin_amdgcn_rsq(x);
@@ -142,6 +160,21 @@ __device__ __forceinline__ double sqrt(double x) {
     const double d = fma_(-g, g, x);
     g = fma_(d, h, g);
     return x > 0.0 ? g : (x == 0.0 ? x : __builtin_nan(""));
+}
+// sqrt of a sum of squares (x >= 0 or NaN): the same iteration on rsq(max(x, 1e-300)), so x = 0
+// gives 0 (0 * 1e150) without the zero / negative selects of sqrt (6 fewer ops on the chain); NaN
+// stays NaN through x * y.  Differs from sqrt only below x = 1e-300.
+__device__ __forceinline__ double sqrt_nn(double x) {
+    const double y = __builtin_amdgcn_rsq(__builtin_fmax(x, 1e-300));
+    double g = x * y, h = 0.5 * y;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double r = fma_(-g, h, 0.5);
+        g = fma_(g, r, g);
+        h = fma_(h, r, h);
+    }
+    const double d = fma_(-g, g, x);
+    return fma_(d, h, g);
 }
 // sin / cos for |x| <= pi/8: Taylor to x^13 / x^14 (relative error <= 1.7e-16 before rounding)
 __device__ __forceinline__ void sincos_small(double x, double* s, double* c) {
@@ -236,6 +269,14 @@ __device__ __forceinline__ float rcp_(float x) { return __builtin_amdgcn_rcpf(x)
 __device__ __forceinline__ double rcp_(double x) { return f64::rcp(x); }
 __device__ __forceinline__ float hsqrt_(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ double hsqrt_(double x) { return f64::sqrt(x); }
+// rcp_ / hrsqrt_ of arguments known finite and non-zero where the result is used
+__device__ __forceinline__ float rcp_nc_(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ double rcp_nc_(double x) { return f64::rcp_nc(x); }
+__device__ __forceinline__ float hrsqrt_nc_(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ double hrsqrt_nc_(double x) { return f64::rsq_nc(x); }
+// hsqrt_ of a sum of squares (argument >= 0 or NaN)
+__device__ __forceinline__ float hsqrt_nn_(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ double hsqrt_nn_(double x) { return f64::sqrt_nn(x); }
 __device__ __forceinline__ float hrsqrt_(float x) { return __builtin_amdgcn_rsqf(x); }
 __device__ __forceinline__ double hrsqrt_(double x) { return f64::rsq(x); }
 
@@ -275,6 +316,27 @@ __device__ __forceinline__ float fasin_(float s) { return fatan2_(s, __builtin_a
 __device__ __forceinline__ double fasin_(double s) { return f64::asin(s); }
 __device__ __forceinline__ float fexp_(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ double fexp_(double x) { return f64::exp(x); }
+
+// btClamp(x, -100, 100) of the six coordinate velocities (btMultiBody m_maxCoordinateVelocity) after
+// the semi-implicit Euler update.  fp32: one v_med3 each.  fp64 has no med3, and the select form
+// (x < -100 ? -100 : x > 100 ? 100 : x) is 2 compares + 4 32-bit selects per component on every
+// sub-step of the dependent chain; the clamp is the identity unless a component exceeds 100 in
+// magnitude, so a wave-uniform test guards the exact select form (NaN passes through as in btClamp).
+__device__ __forceinline__ void clamp100_wv(V3<float>& w, V3<float>& v) {
+    w = {__builtin_amdgcn_fmed3f(w.x, -100.0f, 100.0f), __builtin_amdgcn_fmed3f(w.y, -100.0f, 100.0f),
+         __builtin_amdgcn_fmed3f(w.z, -100.0f, 100.0f)};
+    v = {__builtin_amdgcn_fmed3f(v.x, -100.0f, 100.0f), __builtin_amdgcn_fmed3f(v.y, -100.0f, 100.0f),
+         __builtin_amdgcn_fmed3f(v.z, -100.0f, 100.0f)};
+}
+__device__ __forceinline__ double clamp100_sel(double x) { return x < -100.0 ? -100.0 : (x > 100.0 ? 100.0 : x); }
+__device__ __forceinline__ void clamp100_wv(V3<double>& w, V3<double>& v) {
+    const bool big = (__builtin_fabs(w.x) > 100.0) | (__builtin_fabs(w.y) > 100.0) | (__builtin_fabs(w.z) > 100.0) |
+                     (__builtin_fabs(v.x) > 100.0) | (__builtin_fabs(v.y) > 100.0) | (__builtin_fabs(v.z) > 100.0);
+    if (__builtin_expect(__any(big), 0)) {
+        w = {clamp100_sel(w.x), clamp100_sel(w.y), clamp100_sel(w.z)};
+        v = {clamp100_sel(v.x), clamp100_sel(v.y), clamp100_sel(v.z)};
+    }
+}
 
 // rotation matrix of a unit quaternion (body->world)
 template <typename Real>

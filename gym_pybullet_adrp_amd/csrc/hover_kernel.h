@@ -135,10 +135,6 @@ __device__ __forceinline__ float rpm_gain(float a) {
     return 1.0f + m;
 }
 
-// btClamp(x, -m_maxCoordinateVelocity, m_maxCoordinateVelocity): one v_med3_f32
-__device__ __forceinline__ float clamp100(float x) { return __builtin_amdgcn_fmed3f(x, -100.0f, 100.0f); }
-__device__ __forceinline__ double clamp100(double x) { return x < -100.0 ? -100.0 : (x > 100.0 ? 100.0 : x); }
-
 // One Bullet stepSimulation of one drone after the reference's force calls.
 // R = rot(b.q) on entry; Rs = rotation of the cached link basis.  On exit R/Rs are the
 // matrices the next sub-step needs.  Returns true if the plane contact model acted.
@@ -189,28 +185,29 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     // ---- Bullet: forwardKinematics, ABA of the floating base, semi-implicit Euler ----
     const V3<Real> wb = mulT(R, b.w);
     const V3<Real> Iw = v3(a.ixx * wb.x, a.iyy * wb.y, a.izz * wb.z);
-    const Real kw = Real(0.04) + Real(0.04) * hsqrt_(dot(wb, wb));
+    const Real kw = Real(0.04) + Real(0.04) * hsqrt_nn_(dot(wb, wb));
     const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
     const V3<Real> wdot = mul(R, v3(rhs.x * a.inv_ixx, rhs.y * a.inv_iyy, rhs.z * a.inv_izz));
-    const Real kv = Real(0.04) + Real(0.04) * hsqrt_(dot(b.vel, b.vel));
+    const Real kv = Real(0.04) + Real(0.04) * hsqrt_nn_(dot(b.vel, b.vel));
     const V3<Real> acc = a.inv_mass * Fw - kv * b.vel;
-    b.w = v3(clamp100(b.w.x + a.dt * wdot.x), clamp100(b.w.y + a.dt * wdot.y), clamp100(b.w.z + a.dt * wdot.z));
-    b.vel = v3(clamp100(b.vel.x + a.dt * acc.x), clamp100(b.vel.y + a.dt * acc.y), clamp100(b.vel.z + a.dt * acc.z));
+    b.w = v3(b.w.x + a.dt * wdot.x, b.w.y + a.dt * wdot.y, b.w.z + a.dt * wdot.z);
+    b.vel = v3(b.vel.x + a.dt * acc.x, b.vel.y + a.dt * acc.y, b.vel.z + a.dt * acc.z);
+    clamp100_wv(b.w, b.vel);
     b.pos = b.pos + a.dt * b.vel;
     // exp-map quaternion update (btMultiBody::stepPositionsMultiDof)
-    Real ang = hsqrt_(dot(b.w, b.w));
+    Real ang = hsqrt_nn_(dot(b.w, b.w));
     if (ang > a.ang_max) ang = a.ang_max;          // |w| dt > ANGULAR_MOTION_THRESHOLD
     Real sh, ch;
     small_sincos(Real(0.5) * ang * a.dt, &sh, &ch);
     const Real sc = ang < Real(0.001) ? Real(0.5) * a.dt - (a.dt * a.dt * a.dt) * Real(0.020833333333) * ang * ang
-                                      : sh * rcp_(ang);
+                                      : sh * rcp_nc_(ang);
     const V3<Real> ax = sc * b.w;
     const Q4<Real> q0 = b.q;
     const Q4<Real> q1 = {ch * q0.x + ax.x * q0.w + ax.y * q0.z - ax.z * q0.y,
                          ch * q0.y + ax.y * q0.w + ax.z * q0.x - ax.x * q0.z,
                          ch * q0.z + ax.z * q0.w + ax.x * q0.y - ax.y * q0.x,
                          ch * q0.w - ax.x * q0.x - ax.y * q0.y - ax.z * q0.z};
-    const Real inv = hrsqrt_(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
+    const Real inv = hrsqrt_nc_(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
     // the basis cached by this step's forwardKinematics is the pre-integration pose
     if (a.link_lag) {
         b.ql = b.q;
@@ -221,7 +218,7 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     if (!a.link_lag) Rs = R;
     // plane contact model: non-penetration, no inward velocity.
     // lowest point of the body cylinder: cos(tilt) = R22, sin(tilt) = |(R02, R12)|
-    const Real low = b.pos.z + a.coll_zoff - a.coll_hh * fabs_(R.a22) - a.coll_r * hsqrt_(R.a02 * R.a02 + R.a12 * R.a12);
+    const Real low = b.pos.z + a.coll_zoff - a.coll_hh * fabs_(R.a22) - a.coll_r * hsqrt_nn_(R.a02 * R.a02 + R.a12 * R.a12);
     if (low < Real(0)) {
         b.pos.z -= low;
         if (b.vel.z < Real(0)) b.vel.z = Real(0);

@@ -869,9 +869,6 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
 // ---------------------------------------------------------------------------------------
 // one physics sub-step of one drone (Bullet floating-base step after the force calls)
 // ---------------------------------------------------------------------------------------
-template <typename Real>
-__device__ __forceinline__ Real clamp100r(Real x) { return clampr_(x, Real(-100), Real(100)); }
-
 // Rq = rot(d.q), Rl = rot(d.ql) on entry; on return Rq = rot(new q), Rl = rot(new ql) (= the entry
 // Rq): a caller that carries both across sub-steps computes one rotation matrix per sub-step
 template <typename Real, int PH>
@@ -931,33 +928,37 @@ __device__ __forceinline__ void race_pyb_substep_r(const RaceConst<Real>& C, RDr
     (void)0;
     const V3<Real> wb = mulT(R, d.w);
     const V3<Real> Iw = v3(ixx * wb.x, iyy * wb.y, izz * wb.z);
-    const Real kw = Real(0.04) + Real(0.04) * hsqrt_(dot(wb, wb));
+    const Real kw = Real(0.04) + Real(0.04) * hsqrt_nn_(dot(wb, wb));
     const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
     const V3<Real> wdot = mul(R, v3(rhs.x * d.inv_i[0], rhs.y * d.inv_i[1], rhs.z * d.inv_i[2]));
-    const Real kv = Real(0.04) + Real(0.04) * hsqrt_(dot(d.vel, d.vel));
+    const Real kv = Real(0.04) + Real(0.04) * hsqrt_nn_(dot(d.vel, d.vel));
     const V3<Real> acc = d.inv_mass * Fw - kv * d.vel;
-    d.w = v3(clamp100r(d.w.x + C.dt * wdot.x), clamp100r(d.w.y + C.dt * wdot.y), clamp100r(d.w.z + C.dt * wdot.z));
-    d.vel = v3(clamp100r(d.vel.x + C.dt * acc.x), clamp100r(d.vel.y + C.dt * acc.y), clamp100r(d.vel.z + C.dt * acc.z));
+    d.w = v3(d.w.x + C.dt * wdot.x, d.w.y + C.dt * wdot.y, d.w.z + C.dt * wdot.z);
+    d.vel = v3(d.vel.x + C.dt * acc.x, d.vel.y + C.dt * acc.y, d.vel.z + C.dt * acc.z);
+    clamp100_wv(d.w, d.vel);
     // forwardKinematics of this step caches the pre-integration pose
     d.ql = d.q;
     d.lpos = d.pos;
     d.pos = d.pos + C.dt * d.vel;
-    Real ang = hsqrt_(dot(d.w, d.w));
+    Real ang = hsqrt_nn_(dot(d.w, d.w));
     if (ang > C.ang_max) ang = C.ang_max;
     Real sh, ch;
     small_sincos(Real(0.5) * ang * C.dt, &sh, &ch);   // argument <= ANGULAR_MOTION_THRESHOLD / 2 = pi / 8
     const Real sc = ang < Real(0.001) ? Real(0.5) * C.dt - (C.dt * C.dt * C.dt) * Real(0.020833333333) * ang * ang
-                                      : sh * rcp_(ang);
+                                      : sh * rcp_nc_(ang);
     const V3<Real> ax = sc * d.w;
     const Q4<Real> q0 = d.q;
     const Q4<Real> q1 = {ch * q0.x + ax.x * q0.w + ax.y * q0.z - ax.z * q0.y,
                          ch * q0.y + ax.y * q0.w + ax.z * q0.x - ax.x * q0.z,
                          ch * q0.z + ax.z * q0.w + ax.x * q0.y - ax.y * q0.x,
                          ch * q0.w - ax.x * q0.x - ax.y * q0.y - ax.z * q0.z};
-    const Real inv = rsqrt_(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
+    // fp64: the refined v_rsq_f64 (<= 2 ulp) instead of 1 / IEEE sqrt (two correctly rounded
+    // sequences on the chain); fp32 keeps the correctly rounded form
+    const Real nq2 = q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w;
+    const Real inv = sizeof(Real) == 8 ? hrsqrt_nc_(nq2) : rsqrt_(nq2);
     d.q = {q1.x * inv, q1.y * inv, q1.z * inv, q1.w * inv};
     const M3<Real> Rn = rot(d.q);
-    const Real low = d.pos.z + C.coll_zoff - C.coll_hh * fabs_(Rn.a22) - C.coll_r * hsqrt_(Rn.a02 * Rn.a02 + Rn.a12 * Rn.a12);
+    const Real low = d.pos.z + C.coll_zoff - C.coll_hh * fabs_(Rn.a22) - C.coll_r * hsqrt_nn_(Rn.a02 * Rn.a02 + Rn.a12 * Rn.a12);
     if (low < Real(0)) {
         d.pos.z -= low;
         if (d.vel.z < Real(0)) d.vel.z = Real(0);

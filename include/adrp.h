@@ -331,6 +331,9 @@ int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_d
 #define ADRP_MATH_ATAN2 5
 #define ADRP_MATH_ASIN 6           /* |x| < 1 */
 #define ADRP_MATH_EXP 7            /* x <= 0 in the kernels */
+#define ADRP_MATH_SQRT_NN 8        /* sums of squares: x >= 0 or NaN (Bullet step norms) */
+#define ADRP_MATH_RCP_NC 9         /* finite, non-zero x (no non-finite fix-up) */
+#define ADRP_MATH_RSQ_NC 10        /* finite, positive x (quaternion norm) */
 int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream);
 
 #ifdef __cplusplus

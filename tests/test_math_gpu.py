@@ -38,7 +38,7 @@ def rel_err(got, ref, floor=0.0):
 
 
 def test_constants_mirrored():
-    assert (abi.MATH_RCP, abi.MATH_EXP) == (0, 7)
+    assert (abi.MATH_RCP, abi.MATH_EXP, abi.MATH_RSQ_NC) == (0, 7, 10)
 
 
 def test_rcp_rsq_sqrt():
@@ -50,6 +50,19 @@ def test_rcp_rsq_sqrt():
     z = probe(abi.MATH_SQRT, np.array([0.0, -0.0, -1.0]))
     assert z[0] == 0.0 and np.isnan(z[2])
     assert np.isinf(probe(abi.MATH_RCP, np.array([0.0]))[0])
+
+
+def test_chain_variants():
+    """The Bullet-step forms: sqrt of sums of squares (0 -> 0, NaN -> NaN, bit-identical to sqrt
+    above 1e-300) and rcp / rsq without the non-finite fix-up (bit-identical to the checked forms on
+    finite non-zero arguments)."""
+    rng = np.random.default_rng(1)
+    x = np.concatenate([10.0 ** rng.uniform(-12, 12, 200000), [1.0, 2.0, 3.0, 0.1, 1e-300, 1e300]])
+    np.testing.assert_array_equal(probe(abi.MATH_SQRT_NN, x), probe(abi.MATH_SQRT, x))
+    np.testing.assert_array_equal(probe(abi.MATH_RCP_NC, x), probe(abi.MATH_RCP, x))
+    np.testing.assert_array_equal(probe(abi.MATH_RSQ_NC, x), probe(abi.MATH_RSQ, x))
+    z = probe(abi.MATH_SQRT_NN, np.array([0.0, np.nan]))
+    assert z[0] == 0.0 and np.isnan(z[1])
 
 
 def test_sincos_small():
