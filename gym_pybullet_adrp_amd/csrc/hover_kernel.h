@@ -137,10 +137,13 @@ __device__ __forceinline__ float rpm_gain(float a) {
 
 // One Bullet stepSimulation of one drone after the reference's force calls.
 // R = rot(b.q) on entry; Rs = rotation of the cached link basis.  On exit R/Rs are the
-// matrices the next sub-step needs.  Returns true if the plane contact model acted.
+// matrices the next sub-step needs.  wn = |b.w| on entry and on exit (the exp map's |w| is the
+// next sub-step's |R^T w| of the damping term: a rotation keeps the norm, so the chain takes one
+// square root per sub-step, not two; rounding-level difference).  Returns true if the plane
+// contact model acted.
 template <typename Real, int PH>
 __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real>& b, M3<Real>& R, M3<Real>& Rs,
-                                            const Real rpm[4], Real sum_f, V3<Real> P, Real tau_z) {
+                                            const Real rpm[4], Real sum_f, V3<Real> P, Real tau_z, Real& wn) {
     constexpr bool GND = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     // _physics: 4 prop forces + z torque on link 4, LINK_FRAME, cached basis
@@ -185,7 +188,7 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     // ---- Bullet: forwardKinematics, ABA of the floating base, semi-implicit Euler ----
     const V3<Real> wb = mulT(R, b.w);
     const V3<Real> Iw = v3(a.ixx * wb.x, a.iyy * wb.y, a.izz * wb.z);
-    const Real kw = Real(0.04) + Real(0.04) * hsqrt_nn_(dot(wb, wb));
+    const Real kw = Real(0.04) + Real(0.04) * wn;
     const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
     const V3<Real> wdot = mul(R, v3(rhs.x * a.inv_ixx, rhs.y * a.inv_iyy, rhs.z * a.inv_izz));
     const Real kv = Real(0.04) + Real(0.04) * hsqrt_nn_(dot(b.vel, b.vel));
@@ -196,6 +199,7 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     b.pos = b.pos + a.dt * b.vel;
     // exp-map quaternion update (btMultiBody::stepPositionsMultiDof)
     Real ang = hsqrt_nn_(dot(b.w, b.w));
+    wn = ang;
     if (ang > a.ang_max) ang = a.ang_max;          // |w| dt > ANGULAR_MOTION_THRESHOLD
     Real sh, ch;
     small_sincos(Real(0.5) * ang * a.dt, &sh, &ch);
@@ -217,12 +221,16 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     R = rot(b.q);
     if (!a.link_lag) Rs = R;
     // plane contact model: non-penetration, no inward velocity.
-    // lowest point of the body cylinder: cos(tilt) = R22, sin(tilt) = |(R02, R12)|
-    const Real low = b.pos.z + a.coll_zoff - a.coll_hh * fabs_(R.a22) - a.coll_r * hsqrt_nn_(R.a02 * R.a02 + R.a12 * R.a12);
-    if (low < Real(0)) {
-        b.pos.z -= low;
-        if (b.vel.z < Real(0)) b.vel.z = Real(0);
-        return true;
+    // lowest point of the body cylinder: cos(tilt) = R22, sin(tilt) = |(R02, R12)|.  It is at
+    // least z + zoff - hh - r below the centre, so a wave whose drones are all higher than that
+    // skips the exact test (same result)
+    if (__builtin_expect(__any(b.pos.z + a.coll_zoff <= a.coll_hh + a.coll_r + Real(1e-6)), 0)) {
+        const Real low = b.pos.z + a.coll_zoff - a.coll_hh * fabs_(R.a22) - a.coll_r * hsqrt_nn_(R.a02 * R.a02 + R.a12 * R.a12);
+        if (low < Real(0)) {
+            b.pos.z -= low;
+            if (b.vel.z < Real(0)) b.vel.z = Real(0);
+            return true;
+        }
     }
     return false;
 }
@@ -673,8 +681,9 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         const Real tau_z = t2 * C.km;    // KM*(rpm0^2 - rpm1^2 + rpm2^2 - rpm3^2), IROS sign
         M3<Real> R = rot(b.q);
         M3<Real> Rs = lag ? rot(b.ql) : R;
+        Real wn = hsqrt_nn_(dot(b.w, b.w));
         auto substep = [&]() {
-            touched |= pyb_substep<Real, PH>(C, b, R, Rs, rpm, sum_f, P, tau_z);
+            touched |= pyb_substep<Real, PH>(C, b, R, Rs, rpm, sum_f, P, tau_z, wn);
 #pragma unroll
             for (int i = 0; i < 4; ++i) b.prev_rpm[i] = rpm[i];  // last_clipped_action
         };

@@ -958,10 +958,14 @@ __device__ __forceinline__ void race_pyb_substep_r(const RaceConst<Real>& C, RDr
     const Real inv = sizeof(Real) == 8 ? hrsqrt_nc_(nq2) : rsqrt_(nq2);
     d.q = {q1.x * inv, q1.y * inv, q1.z * inv, q1.w * inv};
     const M3<Real> Rn = rot(d.q);
-    const Real low = d.pos.z + C.coll_zoff - C.coll_hh * fabs_(Rn.a22) - C.coll_r * hsqrt_nn_(Rn.a02 * Rn.a02 + Rn.a12 * Rn.a12);
-    if (low < Real(0)) {
-        d.pos.z -= low;
-        if (d.vel.z < Real(0)) d.vel.z = Real(0);
+    // plane contact: the cylinder's lowest point is at least zoff - hh - r from the centre, so a wave
+    // whose drones are all higher than that skips the exact test (same result)
+    if (__builtin_expect(__any(d.pos.z + C.coll_zoff <= C.coll_hh + C.coll_r + Real(1e-6)), 0)) {
+        const Real low = d.pos.z + C.coll_zoff - C.coll_hh * fabs_(Rn.a22) - C.coll_r * hsqrt_nn_(Rn.a02 * Rn.a02 + Rn.a12 * Rn.a12);
+        if (low < Real(0)) {
+            d.pos.z -= low;
+            if (d.vel.z < Real(0)) d.vel.z = Real(0);
+        }
     }
     Rl = R;
     Rq = Rn;
