@@ -195,6 +195,20 @@ __device__ __forceinline__ void sincos_small(double x, double* s, double* c) {
     *s = fma_(x * x2, ps, x);
     *c = fma_(x2, pc, 1.0);
 }
+// sin / cos for |x| <= 0.03 (the exp-map half angle |w| dt / 2 below 14 rad/s at 240 Hz): Taylor to
+// x^7 / x^8; the first omitted terms are x^8/9! = 1.8e-18 and x^10/10! = 1.6e-22 relative
+__device__ __forceinline__ void sincos_tiny(double x, double* s, double* c) {
+    const double x2 = x * x;
+    double ps = -0.0001984126984126984;
+    ps = fma_(ps, x2, 0.008333333333333333);
+    ps = fma_(ps, x2, -0.16666666666666666);
+    double pc = 2.48015873015873e-05;
+    pc = fma_(pc, x2, -0.001388888888888889);
+    pc = fma_(pc, x2, 0.041666666666666664);
+    pc = fma_(pc, x2, -0.5);
+    *s = fma_(x * x2, ps, x);
+    *c = fma_(x2, pc, 1.0);
+}
 // atan2(y, x): octant reduction to a = min/max in [0, 1], then t = a or (a - 1)/(a + 1) (one
 // division either way: (min - max)/(min + max)) so |t| <= tan(pi/8), atan t = t + t^3 P(t^2)
 // with a degree-9 near-minimax P (1.7e-16 relative).  atan2(0, 0) = 0 (as the fp32 fatan2_).
@@ -288,6 +302,21 @@ __device__ __forceinline__ void small_sincos(float x, float* s, float* c) {
     *c = 1.0f + x2 * (-0.5f + x2 * (1.0f / 24.0f + x2 * (-1.0f / 720.0f + x2 * (1.0f / 40320.0f))));
 }
 __device__ __forceinline__ void small_sincos(double x, double* s, double* c) { f64::sincos_small(x, s, c); }
+// the exp-map half angle of the sub-step chains: the short series when the whole wave is within
+// |x| <= 0.03 (wave-uniform branch), else the full one (fp32: the one series)
+__device__ __forceinline__ void expmap_sincos(float x, float* s, float* c) { small_sincos(x, s, c); }
+__device__ __forceinline__ void expmap_sincos(double x, double* s, double* c) {
+    if (__builtin_expect(__all(__builtin_fabs(x) <= 0.03), 1)) f64::sincos_tiny(x, s, c);
+    else f64::sincos_small(x, s, c);
+}
+// 1/|q| of the exp-map quaternion: |q1|^2 = |q0|^2 (cos^2 + sin^2) = 1 up to rounding unless the
+// |w| dt threshold clamped the angle, so while |n2 - 1| <= 1e-9 across the wave one Newton step
+// from 1, 1 + (1 - n2) / 2 (error 3/8 (n2 - 1)^2 <= 4e-19), else the refined rsq (fp32: v_rsq)
+__device__ __forceinline__ float quat_inv_norm(float n2) { return __builtin_amdgcn_rsqf(n2); }
+__device__ __forceinline__ double quat_inv_norm(double n2) {
+    if (__builtin_expect(__all(__builtin_fabs(n2 - 1.0) <= 1e-9), 1)) return f64::fma_(0.5, 1.0 - n2, 1.0);
+    return f64::rsq_nc(n2);
+}
 
 // fast fp32 transcendentals for the latency-bound sub-step loop (fp64: the f64 forms above).
 // atan on [0,1] is an odd minimax polynomial (|err| <= 1.1e-7 rad, fitted by IRLS on

@@ -202,7 +202,7 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     wn = ang;
     if (ang > a.ang_max) ang = a.ang_max;          // |w| dt > ANGULAR_MOTION_THRESHOLD
     Real sh, ch;
-    small_sincos(Real(0.5) * ang * a.dt, &sh, &ch);
+    expmap_sincos(Real(0.5) * ang * a.dt, &sh, &ch);
     const Real sc = ang < Real(0.001) ? Real(0.5) * a.dt - (a.dt * a.dt * a.dt) * Real(0.020833333333) * ang * ang
                                       : sh * rcp_nc_(ang);
     const V3<Real> ax = sc * b.w;
@@ -211,7 +211,7 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
                          ch * q0.y + ax.y * q0.w + ax.z * q0.x - ax.x * q0.z,
                          ch * q0.z + ax.z * q0.w + ax.x * q0.y - ax.y * q0.x,
                          ch * q0.w - ax.x * q0.x - ax.y * q0.y - ax.z * q0.z};
-    const Real inv = hrsqrt_nc_(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
+    const Real inv = quat_inv_norm(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
     // the basis cached by this step's forwardKinematics is the pre-integration pose
     if (a.link_lag) {
         b.ql = b.q;

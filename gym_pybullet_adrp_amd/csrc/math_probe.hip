@@ -25,6 +25,8 @@ __global__ void __launch_bounds__(256) math_probe_kernel(int fn, const double* _
         case ADRP_MATH_SQRT_NN: r = adrp::f64::sqrt_nn(x); break;
         case ADRP_MATH_RCP_NC: r = adrp::f64::rcp_nc(x); break;
         case ADRP_MATH_RSQ_NC: r = adrp::f64::rsq_nc(x); break;
+        case ADRP_MATH_SIN_TINY: adrp::f64::sincos_tiny(x, &r, &c); break;
+        case ADRP_MATH_COS_TINY: adrp::f64::sincos_tiny(x, &c, &r); break;
         default: r = __builtin_nan(""); break;
     }
     out[i] = r;
@@ -32,7 +34,7 @@ __global__ void __launch_bounds__(256) math_probe_kernel(int fn, const double* _
 }  // namespace
 
 extern "C" int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream) {
-    if (fn < ADRP_MATH_RCP || fn > ADRP_MATH_RSQ_NC || n < 0 || (n > 0 && (!in_dev || !out_dev))) return ADRP_ERR_INVALID;
+    if (fn < ADRP_MATH_RCP || fn > ADRP_MATH_COS_TINY || n < 0 || (n > 0 && (!in_dev || !out_dev))) return ADRP_ERR_INVALID;
     if (n == 0) return ADRP_OK;
     hipLaunchKernelGGL(math_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, in_dev, out_dev, n);
     return hipGetLastError() == hipSuccess ? ADRP_OK : ADRP_ERR_DEVICE;

@@ -16,7 +16,7 @@ TASK_HOVER, TASK_RACE = 0, 1
 PHYS_PYB, PHYS_DYN, PHYS_PYB_GND, PHYS_PYB_DRAG, PHYS_PYB_DW, PHYS_PYB_GND_DRAG_DW = range(6)
 ACT_RPM, ACT_ONE_D_RPM, ACT_FULLSTATE, ACT_PID, ACT_VEL, ACT_ONE_D_PID = 0, 1, 2, 3, 4, 5
 MATH_RCP, MATH_RSQ, MATH_SQRT, MATH_SIN_SMALL, MATH_COS_SMALL, MATH_ATAN2, MATH_ASIN, MATH_EXP = range(8)   # adrp_math_probe
-MATH_SQRT_NN, MATH_RCP_NC, MATH_RSQ_NC = 8, 9, 10
+MATH_SQRT_NN, MATH_RCP_NC, MATH_RSQ_NC, MATH_SIN_TINY, MATH_COS_TINY = 8, 9, 10, 11, 12
 RACE_COMPARE, RACE_COMPETE = 0, 1
 POLICY_TANH, POLICY_RELU = 0, 1
 POLICY_RAW, POLICY_RELATIVE, POLICY_ABSOLUTE = 0, 1, 2

@@ -334,6 +334,8 @@ int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_d
 #define ADRP_MATH_SQRT_NN 8        /* sums of squares: x >= 0 or NaN (Bullet step norms) */
 #define ADRP_MATH_RCP_NC 9         /* finite, non-zero x (no non-finite fix-up) */
 #define ADRP_MATH_RSQ_NC 10        /* finite, positive x (quaternion norm) */
+#define ADRP_MATH_SIN_TINY 11      /* |x| <= 0.03 (exp-map half angle) */
+#define ADRP_MATH_COS_TINY 12      /* |x| <= 0.03 */
 int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream);
 
 #ifdef __cplusplus

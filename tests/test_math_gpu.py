@@ -38,7 +38,7 @@ def rel_err(got, ref, floor=0.0):
 
 
 def test_constants_mirrored():
-    assert (abi.MATH_RCP, abi.MATH_EXP, abi.MATH_RSQ_NC) == (0, 7, 10)
+    assert (abi.MATH_RCP, abi.MATH_EXP, abi.MATH_COS_TINY) == (0, 7, 12)
 
 
 def test_rcp_rsq_sqrt():
@@ -63,6 +63,14 @@ def test_chain_variants():
     np.testing.assert_array_equal(probe(abi.MATH_RSQ_NC, x), probe(abi.MATH_RSQ, x))
     z = probe(abi.MATH_SQRT_NN, np.array([0.0, np.nan]))
     assert z[0] == 0.0 and np.isnan(z[1])
+
+
+def test_sincos_tiny():
+    """The short exp-map series on |x| <= 0.03 (taken when the whole wave is there)."""
+    x = np.concatenate([np.linspace(-0.03, 0.03, 100001), [1e-300, -1e-12, 0.0]])
+    xs = x[x != 0]
+    assert rel_err(probe(abi.MATH_SIN_TINY, xs), np.sin(xs.astype(L))).max() < ULP4
+    assert rel_err(probe(abi.MATH_COS_TINY, x), np.cos(x.astype(L))).max() < ULP4
 
 
 def test_sincos_small():
