@@ -201,10 +201,11 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     Real ang = hsqrt_nn_(dot(b.w, b.w));
     wn = ang;
     if (ang > a.ang_max) ang = a.ang_max;          // |w| dt > ANGULAR_MOTION_THRESHOLD
-    Real sh, ch;
-    expmap_sincos(Real(0.5) * ang * a.dt, &sh, &ch);
-    const Real sc = ang < Real(0.001) ? Real(0.5) * a.dt - (a.dt * a.dt * a.dt) * Real(0.020833333333) * ang * ang
-                                      : sh * rcp_nc_(ang);
+    // sin(|w| dt / 2) / |w| = (dt / 2) sinc(|w| dt / 2): no reciprocal, and Bullet's small-angle
+    // form (|w| < 0.001: 0.5 dt - dt^3 |w|^2 / 48) is the same series to rounding
+    Real sinc, ch;
+    expmap_sinc_cos(Real(0.5) * ang * a.dt, &sinc, &ch);
+    const Real sc = (Real(0.5) * a.dt) * sinc;
     const V3<Real> ax = sc * b.w;
     const Q4<Real> q0 = b.q;
     const Q4<Real> q1 = {ch * q0.x + ax.x * q0.w + ax.y * q0.z - ax.z * q0.y,
