@@ -347,6 +347,27 @@ __device__ __forceinline__ void expmap_sinc_cos(double x, double* sinc, double* 
     *sinc = f64::fma_(x2, ps, 1.0);
     *c = f64::fma_(x2, pc, 1.0);
 }
+// expmap_sinc_cos with the full series and no wave-uniform branch (the race quad kernel, where the
+// branchy short forms measured slower)
+__device__ __forceinline__ void expmap_sinc_cos_full(float x, float* sinc, float* c) { expmap_sinc_cos(x, sinc, c); }
+__device__ __forceinline__ void expmap_sinc_cos_full(double x, double* sinc, double* c) {
+    const double x2 = x * x;
+    double ps = 1.6059043836821613e-10;
+    ps = f64::fma_(ps, x2, -2.505210838544172e-08);
+    ps = f64::fma_(ps, x2, 2.7557319223985893e-06);
+    ps = f64::fma_(ps, x2, -0.0001984126984126984);
+    ps = f64::fma_(ps, x2, 0.008333333333333333);
+    ps = f64::fma_(ps, x2, -0.16666666666666666);
+    double pc = -1.1470745597729725e-11;
+    pc = f64::fma_(pc, x2, 2.08767569878681e-09);
+    pc = f64::fma_(pc, x2, -2.755731922398589e-07);
+    pc = f64::fma_(pc, x2, 2.48015873015873e-05);
+    pc = f64::fma_(pc, x2, -0.001388888888888889);
+    pc = f64::fma_(pc, x2, 0.041666666666666664);
+    pc = f64::fma_(pc, x2, -0.5);
+    *sinc = f64::fma_(x2, ps, 1.0);
+    *c = f64::fma_(x2, pc, 1.0);
+}
 // 1/|q| of the exp-map quaternion: |q1|^2 = |q0|^2 (cos^2 + sin^2) = 1 up to rounding unless the
 // |w| dt threshold clamped the angle, so while |n2 - 1| <= 1e-9 across the wave one Newton step
 // from 1, 1 + (1 - n2) / 2 (error 3/8 (n2 - 1)^2 <= 4e-19), else the refined rsq (fp32: v_rsq)

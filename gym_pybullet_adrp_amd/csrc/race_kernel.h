@@ -942,10 +942,11 @@ __device__ __forceinline__ void race_pyb_substep_r(const RaceConst<Real>& C, RDr
     d.pos = d.pos + C.dt * d.vel;
     Real ang = hsqrt_nn_(dot(d.w, d.w));
     if (ang > C.ang_max) ang = C.ang_max;
-    Real sh, ch;
-    small_sincos(Real(0.5) * ang * C.dt, &sh, &ch);   // argument <= ANGULAR_MOTION_THRESHOLD / 2 = pi / 8
-    const Real sc = ang < Real(0.001) ? Real(0.5) * C.dt - (C.dt * C.dt * C.dt) * Real(0.020833333333) * ang * ang
-                                      : sh * rcp_nc_(ang);
+    // sin(|w| dt / 2) / |w| = (dt / 2) sinc(|w| dt / 2) (argument <= ANGULAR_MOTION_THRESHOLD / 2 = pi / 8):
+    // no reciprocal, and Bullet's |w| < 0.001 form is the same series to rounding
+    Real sinc, ch;
+    expmap_sinc_cos_full(Real(0.5) * ang * C.dt, &sinc, &ch);
+    const Real sc = (Real(0.5) * C.dt) * sinc;
     const V3<Real> ax = sc * d.w;
     const Q4<Real> q0 = d.q;
     const Q4<Real> q1 = {ch * q0.x + ax.x * q0.w + ax.y * q0.z - ax.z * q0.y,
