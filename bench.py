@@ -349,18 +349,20 @@ def race_key(level, drones, physics, precision, E):
 # ----------------------------------------------------------------------------------------------
 # workloads
 # ----------------------------------------------------------------------------------------------
-def _gather_record(sharded, acts, K, W, world, dev, E_rank, row_floats):
+def _gather_record(sharded, acts, K, W, world, dev, E_rank, row_floats, refuse_capture=False):
     """step + packed all-gather (sharding.ShardedAviary(packed=True).step_gather): env.step and one
     all_gather_into_tensor of the preallocated send buffer, captured together in the HIP graph;
-    eager (one launch + one collective per step) if the capture is refused"""
+    eager (one launch + one collective per step) if the capture is refused (refuse_capture: act as if
+    it were, tests/test_sharding_gpu.py)"""
 
     class _SG:
         def step(self, a):
             return sharded.step_gather(a)
-    rec = {"collective": "all_gather_into_tensor (RCCL over xGMI) of the packed obs/reward/flags send buffer "
-                         "(preallocated; the env writes its outputs into it)",
+    rec = {"collective": "all_gather_into_tensor (RCCL) of the packed obs/reward/flags send buffer",
            "bytes_per_rank_per_step": sharded._seg, "obs_floats_per_env": row_floats}
     try:
+        if refuse_capture:
+            raise RuntimeError("capture refused (forced)")
         el, G = time_graph(_SG(), acts, K, W, world, dev)
         rec["timed_region"] = f"{K // G} replays of a {G}-step HIP graph (step kernel + RCCL all-gather per step)"
     except Exception as exc:   # capture of the collective refused: time it eagerly instead
@@ -381,6 +383,32 @@ def _gather_record(sharded, acts, K, W, world, dev, E_rank, row_floats):
         rec["timed_region"] = f"{K} eager steps (step kernel + RCCL all-gather each)"
     rec.update({"value": E_rank * world * K / el, "unit": "env-steps/s", "ms_per_step": el / K * 1e3, "steps": K})
     return rec
+
+
+def gather_record_world1(dev, K, W, precision="fp64", E=ENVS_PER_GPU, refuse_capture=False, seed=4):
+    """config 5's step + RCCL all-gather at N = 1: a world-1 "nccl" (RCCL) group (created here unless
+    one is already initialised), ShardedAviary(packed=True) over the config-5 per-GPU workload,
+    step_gather captured in the HIP graph (the path every rank of an N-GPU job runs)"""
+    from gym_pybullet_adrp_amd.sharding import ShardedAviary
+    own = not dist.is_initialized()
+    if own:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ["MASTER_PORT"] = str(_free_port())
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", dev))
+    sharded = None
+    try:
+        sharded = ShardedAviary(E, race_make("level3", 4, "PYB_DW", "COMPETE", precision, dev), packed=True)
+        obs0, _ = sharded.env.reset()
+        acts = race_actions(obs0.clone(), dev, seed)
+        rec = _gather_record(sharded, acts, K, W, 1, dev, E, 4 * sharded.env.h.D, refuse_capture=refuse_capture)
+        rec.update({"world": dist.get_world_size(), "backend": dist.get_backend(), "precision": precision,
+                    "envs_per_gpu": E, "kernel": sharded.env.kernel_name})
+        return rec
+    finally:
+        if sharded is not None:
+            sharded.close()
+        if own:
+            dist.destroy_process_group()
 
 
 def bench_race(level, drones, physics, racemode, precision, E, K, W, world, rank, dev, seed,
@@ -418,10 +446,9 @@ def bench_race(level, drones, physics, racemode, precision, E, K, W, world, rank
         step_ms = float(np.mean(eager))
     key = race_key(level, drones, physics, precision, E)
     total = E * world
-    rec = {"workload": f"MultiRaceAviary {racemode} {level}, {drones} drones x {E} envs per GPU ({total} in total), "
-                       f"Physics.{physics} 500/25 Hz (20 sub-steps, Mellinger 500 Hz), {precision}"
-                       + (" (float64 physics / wrapper, float32 firmware: the reference's precision)"
-                          if precision == "fp64" else " (narrower than the reference's float64)"),
+    rec = {"workload": f"MultiRaceAviary {racemode} {level}, {drones} drones x {E} envs/GPU ({total} total), "
+                       f"{physics}, 20 sub-steps + Mellinger 500 Hz, {precision}"
+                       + (" (reference precision)" if precision == "fp64" else ""),
            "value": total * K / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
            "ms_per_step": elapsed / K * 1e3, "drone_steps_per_s": total * K / elapsed * drones,
            "envs_per_gpu": E, "global_envs": total, "kernel": env.kernel_name,
@@ -470,7 +497,10 @@ def bench_hover(args, precision, E, K, W, world, rank, dev, sweep=False, sharded
     rec = {"value": E * world * K / elapsed, "ms_per_step": elapsed / K * 1e3,
            "kernel": env.kernel_name,
            "roofline": hbm_roofline(env.step_bytes(), step_ms, eager, f"{args.physics}_{precision}_{E}"),
-           "timing": {"timed_region": f"{K // G} replays of a {G}-step HIP graph (one fused launch per env.step)"}}
+           "timing": {"timed_region": f"{K // G} replays of a {G}-step HIP graph (one fused launch per env.step)",
+                      "replay_overhead_us_per_step": elapsed / K * 1e6 - step_ms * 1e3,
+                      "note": "ms_per_step = host clock around the timed region / K; kernel_us = HIP events around "
+                              "the replays / K; the difference is graph launch + final sync, amortised over K"}}
     if not args.graph_only:
         # eager (no graph) end-to-end rate, for reference
         torch.cuda.synchronize()
@@ -638,6 +668,9 @@ def main():
         # `strong`: the 32,768 envs of config 5 in total over the N GPUs
         cf["config5"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp64", 4096, RK, RW, world, rank, local, 4,
                                    sharded_gather=gather, graph_only=go)
+        if world == 1 and not args.no_allgather:
+            # the RCCL step + all-gather path of an N-GPU job, on a world-1 group
+            cf["config5"]["with_obs_allgather"] = gather_record_world1(local, RK, RW)
         progress("config5")
         cf["config5"]["strong"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp64", None, RK, RW, world, rank,
                                              local, 4, graph_only=go, global_envs=8 * 4096)
@@ -690,10 +723,48 @@ def main():
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:
+        result["summary"] = summary(result)   # last key: the compact per-config view stays in a kept tail
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _sig(x, n=4):
+    return None if x is None else float(f"{x:.{n}g}")
+
+
+def summary(result):
+    """per workload: value (env-steps/s), ms_per_step, dtype, kernel time (us) and roofline fraction"""
+    def one(rec, dtype):
+        if not rec or rec.get("value") is None:
+            return None
+        rf = rec.get("roofline") or {}
+        return {"v": _sig(rec["value"]), "ms": _sig(rec.get("ms_per_step")), "dt": dtype,
+                "k_us": _sig(rf.get("kernel_us")), "frac": _sig(rf.get("frac"), 3)}
+    out = {"value": one(result, result.get("dtype"))}
+    cf = result.get("configs") or {}
+    for name, dt in (("config5", "f64"), ("config5_f32", "f32"), ("config4_gnd_drag_dw", "f64"), ("config3", "f64"),
+                     ("config3_f32", "f32"), ("config3_policy", "f64"), ("config3_policy_f32", "f32"),
+                     ("config2_f32", "f32"), ("config2_f64", "f64")):
+        if name in cf:
+            out[name] = one(cf[name], dt)
+    c5 = cf.get("config5") or {}
+    if "strong" in c5:
+        out["config5_strong"] = one(c5["strong"], "f64")
+    if "with_obs_allgather" in c5:
+        g = c5["with_obs_allgather"]
+        out["config5_allgather"] = {"v": _sig(g.get("value")), "ms": _sig(g.get("ms_per_step")), "dt": "f64",
+                                    "graph": "graph_capture_error" not in g, "world": g.get("world")}
+    if "config1" in cf:
+        c1 = cf["config1"]
+        out["config1"] = {"sync_v": _sig(c1["gpu_sync_per_step"]["value"]), "graph_v": _sig(c1["gpu_graph"]["value"]),
+                          "cpu_1core_v": _sig((c1.get("cpu_oracle_1env") or {}).get("value"))}
+    if "config2_sb3_vecenv" in cf:
+        out["sb3_packed_us"] = _sig(cf["config2_sb3_vecenv"]["packed"]["us_per_step"])
+    if result.get("cpu_baseline"):
+        out["cpu_baseline_v"] = _sig(result["cpu_baseline"]["value"])
+    return out
 
 
 def race_cfg_of(args):

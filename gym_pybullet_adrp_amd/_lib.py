@@ -107,6 +107,13 @@ def kernel_name(cfg):
     return load().adrp_kernel_name(ctypes.byref(cfg)).decode()
 
 
+if hasattr(torch._C, "_cuda_getCurrentRawStream"):
+    _raw_stream = torch._C._cuda_getCurrentRawStream      # device index -> hipStream_t as an int
+else:  # pragma: no cover
+    def _raw_stream(index):
+        return torch.cuda.current_stream(index).cuda_stream
+
+
 def _p(t):
     """device pointer of a tensor (or None)"""
     return None if t is None else ctypes.c_void_p(t.data_ptr())
@@ -135,6 +142,7 @@ class Handle:
         self.nf, self.ni = nf.value, ni.value
         self.real = torch.float64 if cfg.precision else torch.float32
         self._step = self.lib.adrp_step
+        self._dev_index = self.device.index
 
     def close(self):
         if getattr(self, "h", None):
@@ -152,7 +160,8 @@ class Handle:
             raise AdrpError(f"{what}: {self.lib.adrp_last_error(self.h).decode()}")
 
     def _stream(self):
-        return torch.cuda.current_stream(self.device).cuda_stream
+        """the caller's current HIP stream on this handle's device (a raw handle: no Stream object)"""
+        return _raw_stream(self._dev_index)
 
     def field_names(self):
         return ([self.lib.adrp_state_field(self.h, 0, k).decode() for k in range(self.nf)],
@@ -164,8 +173,7 @@ class Handle:
     def step(self, act, obs, rew, term, trunc, tobs=None):
         """act None: command mode, the setpoints the last command() left"""
         rc = self._step(self.h, None if act is None else act.data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
-                        trunc.data_ptr(), None if tobs is None else tobs.data_ptr(),
-                        torch.cuda.current_stream(self.device).cuda_stream)
+                        trunc.data_ptr(), None if tobs is None else tobs.data_ptr(), _raw_stream(self._dev_index))
         if rc != 0:
             self._check(rc, "adrp_step")
 

@@ -263,11 +263,23 @@ static RaceConst<Real> race_const(const adrp_config& c) {
 }
 
 // the race drone's physical constants are race_cf2x_phys' bit for bit (the four-lane kernel's literals)
+// (field by field, bitwise: a whole-struct memcmp would also compare padding bytes, which a struct
+// copy need not preserve)
 template <typename Real>
 static bool race_is_cf2x(const RaceConst<Real>& rt) {
-    RaceConst<Real> ct = rt;
+    RaceConst<Real> ct;
+    memset(&ct, 0, sizeof ct);
     race_cf2x_phys(ct);
-    return memcmp(&rt, &ct, sizeof rt) == 0;
+    bool same = true;
+#define ADRP_SAME(f) same = same && memcmp(&rt.f, &ct.f, sizeof rt.f) == 0
+    ADRP_SAME(dt); ADRP_SAME(gravity); ADRP_SAME(kf); ADRP_SAME(km);
+    ADRP_SAME(px); ADRP_SAME(py); ADRP_SAME(pz);
+    ADRP_SAME(gnd_kf); ADRP_SAME(prop_r4); ADRP_SAME(gnd_clip); ADRP_SAME(drag);
+    ADRP_SAME(dw1); ADRP_SAME(dw2); ADRP_SAME(dw3); ADRP_SAME(prop_r);
+    ADRP_SAME(dyn_mass); ADRP_SAME(dyn_inv_mass); ADRP_SAME(dyn_i); ADRP_SAME(dyn_inv_i); ADRP_SAME(dyn_arm);
+    ADRP_SAME(coll_hh); ADRP_SAME(coll_r); ADRP_SAME(coll_zoff); ADRP_SAME(ang_max);
+#undef ADRP_SAME
+    return same;
 }
 
 template <typename Real>

@@ -159,7 +159,8 @@ __device__ __forceinline__ double sqrt(double x) {
     }
     const double d = fma_(-g, g, x);
     g = fma_(d, h, g);
-    return x > 0.0 ? g : (x == 0.0 ? x : __builtin_nan(""));
+    // +0 / -0 / +inf return x (rsq(inf) = 0 would give inf * 0 = NaN), x < 0 and NaN give NaN
+    return x > 0.0 && x < __builtin_inf() ? g : (x == 0.0 || x == __builtin_inf() ? x : __builtin_nan(""));
 }
 // sqrt of a sum of squares (x >= 0 or NaN): the same iteration on rsq(max(x, 1e-300)), so x = 0
 // gives 0 (0 * 1e150) without the zero / negative selects of sqrt (6 fewer ops on the chain); NaN
@@ -233,7 +234,8 @@ __device__ __forceinline__ double atan2(double y, double x) {
     if (big) r += 0.78539816339744830962;
     if (ay > ax) r = 1.57079632679489661923 - r;
     if (x < 0.0) r = 3.14159265358979323846 - r;
-    return __builtin_copysign(r, y);
+    // NaN in -> NaN out as libm (fmax / fmin above drop a NaN operand)
+    return __builtin_isunordered(x, y) ? x + y : __builtin_copysign(r, y);
 }
 // asin(s), |s| < 1: atan2(s, sqrt((1 - s)(1 + s)))
 __device__ __forceinline__ double asin(double s) { return atan2(s, sqrt((1.0 - s) * (1.0 + s))); }
@@ -302,13 +304,6 @@ __device__ __forceinline__ void small_sincos(float x, float* s, float* c) {
     *c = 1.0f + x2 * (-0.5f + x2 * (1.0f / 24.0f + x2 * (-1.0f / 720.0f + x2 * (1.0f / 40320.0f))));
 }
 __device__ __forceinline__ void small_sincos(double x, double* s, double* c) { f64::sincos_small(x, s, c); }
-// the exp-map half angle of the sub-step chains: the short series when the whole wave is within
-// |x| <= 0.03 (wave-uniform branch), else the full one (fp32: the one series)
-__device__ __forceinline__ void expmap_sincos(float x, float* s, float* c) { small_sincos(x, s, c); }
-__device__ __forceinline__ void expmap_sincos(double x, double* s, double* c) {
-    if (__builtin_expect(__all(__builtin_fabs(x) <= 0.03), 1)) f64::sincos_tiny(x, s, c);
-    else f64::sincos_small(x, s, c);
-}
 // the exp map's sin(x) / x and cos(x) (x = |w| dt / 2): the series above with the leading x of the
 // sine factored out, so the axis factor sin(x) / |w| = (dt / 2) sinc(x) needs no reciprocal and no
 // small-angle select (Bullet's |w| < 0.001 form 0.5 dt - dt^3 |w|^2 / 48 is this series' first two
@@ -319,30 +314,34 @@ __device__ __forceinline__ void expmap_sinc_cos(float x, float* sinc, float* c) 
     *c = 1.0f + x2 * (-0.5f + x2 * (1.0f / 24.0f + x2 * (-1.0f / 720.0f + x2 * (1.0f / 40320.0f))));
 }
 __device__ __forceinline__ void expmap_sinc_cos(double x, double* sinc, double* c) {
+    // per lane: the short series where |x| <= 0.03, the full one elsewhere, so an env's result never
+    // depends on which other envs share its wave; the wave-uniform test only skips the full series
+    // when no lane needs it
     const double x2 = x * x;
-    double ps, pc;
-    if (__builtin_expect(__all(__builtin_fabs(x) <= 0.03), 1)) {   // f64::sincos_tiny's terms
-        ps = -0.0001984126984126984;
-        ps = f64::fma_(ps, x2, 0.008333333333333333);
-        ps = f64::fma_(ps, x2, -0.16666666666666666);
-        pc = 2.48015873015873e-05;
-        pc = f64::fma_(pc, x2, -0.001388888888888889);
-        pc = f64::fma_(pc, x2, 0.041666666666666664);
-        pc = f64::fma_(pc, x2, -0.5);
-    } else {                                                          // f64::sincos_small's terms
-        ps = 1.6059043836821613e-10;
-        ps = f64::fma_(ps, x2, -2.505210838544172e-08);
-        ps = f64::fma_(ps, x2, 2.7557319223985893e-06);
-        ps = f64::fma_(ps, x2, -0.0001984126984126984);
-        ps = f64::fma_(ps, x2, 0.008333333333333333);
-        ps = f64::fma_(ps, x2, -0.16666666666666666);
-        pc = -1.1470745597729725e-11;
-        pc = f64::fma_(pc, x2, 2.08767569878681e-09);
-        pc = f64::fma_(pc, x2, -2.755731922398589e-07);
-        pc = f64::fma_(pc, x2, 2.48015873015873e-05);
-        pc = f64::fma_(pc, x2, -0.001388888888888889);
-        pc = f64::fma_(pc, x2, 0.041666666666666664);
-        pc = f64::fma_(pc, x2, -0.5);
+    const bool tiny = __builtin_fabs(x) <= 0.03;
+    double ps = -0.0001984126984126984;                                // f64::sincos_tiny's terms
+    ps = f64::fma_(ps, x2, 0.008333333333333333);
+    ps = f64::fma_(ps, x2, -0.16666666666666666);
+    double pc = 2.48015873015873e-05;
+    pc = f64::fma_(pc, x2, -0.001388888888888889);
+    pc = f64::fma_(pc, x2, 0.041666666666666664);
+    pc = f64::fma_(pc, x2, -0.5);
+    if (__builtin_expect(!__all(tiny), 0)) {                            // f64::sincos_small's terms
+        double fs = 1.6059043836821613e-10;
+        fs = f64::fma_(fs, x2, -2.505210838544172e-08);
+        fs = f64::fma_(fs, x2, 2.7557319223985893e-06);
+        fs = f64::fma_(fs, x2, -0.0001984126984126984);
+        fs = f64::fma_(fs, x2, 0.008333333333333333);
+        fs = f64::fma_(fs, x2, -0.16666666666666666);
+        double fc = -1.1470745597729725e-11;
+        fc = f64::fma_(fc, x2, 2.08767569878681e-09);
+        fc = f64::fma_(fc, x2, -2.755731922398589e-07);
+        fc = f64::fma_(fc, x2, 2.48015873015873e-05);
+        fc = f64::fma_(fc, x2, -0.001388888888888889);
+        fc = f64::fma_(fc, x2, 0.041666666666666664);
+        fc = f64::fma_(fc, x2, -0.5);
+        ps = tiny ? ps : fs;
+        pc = tiny ? pc : fc;
     }
     *sinc = f64::fma_(x2, ps, 1.0);
     *c = f64::fma_(x2, pc, 1.0);
@@ -369,12 +368,16 @@ __device__ __forceinline__ void expmap_sinc_cos_full(double x, double* sinc, dou
     *c = f64::fma_(x2, pc, 1.0);
 }
 // 1/|q| of the exp-map quaternion: |q1|^2 = |q0|^2 (cos^2 + sin^2) = 1 up to rounding unless the
-// |w| dt threshold clamped the angle, so while |n2 - 1| <= 1e-9 across the wave one Newton step
-// from 1, 1 + (1 - n2) / 2 (error 3/8 (n2 - 1)^2 <= 4e-19), else the refined rsq (fp32: v_rsq)
+// |w| dt threshold clamped the angle, so where |n2 - 1| <= 1e-9 one Newton step from 1,
+// 1 + (1 - n2) / 2 (error 3/8 (n2 - 1)^2 <= 4e-19), else the refined rsq (fp32: v_rsq).  The choice is
+// per lane (batch-invariant); the wave-uniform test only skips the rsq when no lane needs it.
 __device__ __forceinline__ float quat_inv_norm(float n2) { return __builtin_amdgcn_rsqf(n2); }
 __device__ __forceinline__ double quat_inv_norm(double n2) {
-    if (__builtin_expect(__all(__builtin_fabs(n2 - 1.0) <= 1e-9), 1)) return f64::fma_(0.5, 1.0 - n2, 1.0);
-    return f64::rsq_nc(n2);
+    const bool near1 = __builtin_fabs(n2 - 1.0) <= 1e-9;
+    const double newton = f64::fma_(0.5, 1.0 - n2, 1.0);
+    if (__builtin_expect(__all(near1), 1)) return newton;
+    const double r = f64::rsq_nc(n2);
+    return near1 ? newton : r;
 }
 
 // fast fp32 transcendentals for the latency-bound sub-step loop (fp64: the f64 forms above).
@@ -519,6 +522,48 @@ __device__ __forceinline__ Q4<Real> quat_from_euler_fast(Real r, Real p, Real y)
         }
     }
     return quat_from_euler(r, p, y);
+}
+
+// Box-Muller of one Philox word pair from IEEE float operations only (+ - * /, correctly rounded
+// sqrtf, fmaf, frexpf, rintf), the same sequence as the oracle's normal_pair_f (oracle/race.c), so the
+// fp64 kernels' action noise is bit-identical to the oracle's: u1 = (x0 >> 8 + 1) 2^-24,
+// u2 = (x1 >> 8) 2^-24, r = sqrt(-2 log u1) with log u1 = e ln2 + 2 atanh((m - 1) / (m + 1)),
+// (sin, cos)(2 pi u2) from the octant rint(8 u2) and a Taylor pair on |x| <= pi / 8 (~2 float ulp).
+// No contraction: every fma is explicit.  (The fp32 kernels keep the hardware v_log / v_sin / v_cos
+// form, which differs by float rounding.)
+__device__ __forceinline__ void normal_pair_f(uint32_t x0, uint32_t x1, float* z0, float* z1) {
+#pragma clang fp contract(off)
+    const float u1 = (float(x0 >> 8) + 1.0f) * (1.0f / 16777216.0f);
+    const float u2 = float(x1 >> 8) * (1.0f / 16777216.0f);
+    int e;
+    float m = __builtin_frexpf(u1, &e);
+    if (m < 0.70710677f) { m = m * 2.0f; e -= 1; }
+    const float s = (m - 1.0f) / (m + 1.0f);
+    const float z = s * s;
+    float p = 1.0f / 11;
+    p = __builtin_fmaf(p, z, 1.0f / 9); p = __builtin_fmaf(p, z, 1.0f / 7);
+    p = __builtin_fmaf(p, z, 1.0f / 5); p = __builtin_fmaf(p, z, 1.0f / 3);
+    const float lm = __builtin_fmaf(2.0f * s * z, p, 2.0f * s);
+    const float fe = float(e);
+    const float lg = __builtin_fmaf(fe, 0.693145751953125f, __builtin_fmaf(fe, 1.428606765330187e-06f, lm));
+    const float r = __builtin_sqrtf(-2.0f * lg);
+    const float n = __builtin_rintf(u2 * 8.0f);
+    const float x = (u2 - n * 0.125f) * 6.28318548f;
+    const float x2 = x * x;
+    float ps = -1.98412698e-4f;
+    ps = __builtin_fmaf(ps, x2, 8.33333377e-3f); ps = __builtin_fmaf(ps, x2, -0.166666672f);
+    float pc = 2.48015876e-5f;
+    pc = __builtin_fmaf(pc, x2, -1.38888892e-3f); pc = __builtin_fmaf(pc, x2, 4.16666679e-2f);
+    pc = __builtin_fmaf(pc, x2, -0.5f);
+    const float sx = __builtin_fmaf(x * x2, ps, x), cx = __builtin_fmaf(x2, pc, 1.0f);
+    const float h = 0.70710677f;
+    const float a = h * (cx + sx), b = h * (cx - sx);
+    const int o = int(n) & 7;
+    // octant table as selects: sin / cos of o pi / 4 + x
+    const float sn = o == 0 ? sx : o == 1 ? a : o == 2 ? cx : o == 3 ? b : o == 4 ? -sx : o == 5 ? -a : o == 6 ? -cx : -b;
+    const float cs = o == 0 ? cx : o == 1 ? b : o == 2 ? -sx : o == 3 ? -a : o == 4 ? -cx : o == 5 ? -b : o == 6 ? sx : a;
+    *z0 = r * cs;
+    *z1 = r * sn;
 }
 
 // ---- Philox4x32-10 (Salmon et al. SC'11) -------------------------------------------------

@@ -955,7 +955,7 @@ __device__ __forceinline__ void race_pyb_substep_r(const RaceConst<Real>& C, RDr
                          ch * q0.w - ax.x * q0.x - ax.y * q0.y - ax.z * q0.z};
     // fp64: the refined v_rsq_f64 (<= 2 ulp) instead of 1 / IEEE sqrt (two correctly rounded
     // sequences on the chain); fp32 keeps the correctly rounded form.  (The wave-uniform short forms
-    // of the hover step, expmap_sincos / quat_inv_norm / the plane-contact guard, measured slower
+    // of the hover step, the short exp-map series / quat_inv_norm / the plane-contact guard, measured slower
     // in this kernel: config 4 fp64 +1.3 us, A/B)
     const Real nq2 = q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w;
     const Real inv = sizeof(Real) == 8 ? hrsqrt_nc_(nq2) : rsqrt_(nq2);
@@ -1547,6 +1547,15 @@ template <typename Real>
 __device__ __forceinline__ void race_noise_draws(const RaceConst<Real>& H, uint64_t seed, uint64_t gid, uint32_t ep,
                                                  int dn, uint32_t idx, Real noise[4]) {
     const U4 v = draw(seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), idx);
+    if constexpr (sizeof(Real) == 8) {   // the oracle's Box-Muller, bit for bit (normal_pair_f)
+        float z[4];
+        normal_pair_f(v.a, v.b, &z[0], &z[1]);
+        normal_pair_f(v.c, v.d, &z[2], &z[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) noise[k] = Real(z[k]) * H.noise_std;
+        return;
+    }
+    // fp32: hardware log2 / sin / cos (the samples differ from the oracle's by float rounding)
     const uint32_t x[4] = {v.a, v.b, v.c, v.d};
 #pragma unroll
     for (int p = 0; p < 2; ++p) {

@@ -507,7 +507,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
 
 // the sub-step draws of drone qd's sub-steps s = ql, ql + 4, ... into the LDS table [s][7][drone]:
 // fp32 the 3 force components and the 4 motor noises; fp64 the 3 force uniforms (exact in float;
-// the force is formed in Real at use) and the 4 noise samples (float, scaled at use)
+// the force is formed in Real at use) and the 4 noise samples (normal_pair_f, float, scaled at use)
 template <typename Real>
 __device__ __forceinline__ void quad_draws(const RaceConst<Real>& H, float* pre_draws, uint64_t seed, uint64_t gid,
                                            uint32_t ep, int dn, int sc0, int ql, int qd, int S) {
@@ -524,15 +524,11 @@ __device__ __forceinline__ void quad_draws(const RaceConst<Real>& H, float* pre_
             const U4 u = draw(seed, gid, ep, TAG_RACE_DIST | uint32_t(dn), uint32_t(sc0 + s));
             dst[0] = u01r<float>(u.a); dst[kQuadDrones] = u01r<float>(u.b); dst[2 * kQuadDrones] = u01r<float>(u.c);
             const U4 v = draw(seed, gid, ep, TAG_RACE_NOISE | uint32_t(dn), uint32_t(sc0 + s));
-            const uint32_t x[4] = {v.a, v.b, v.c, v.d};
+            float z[4];   // race_noise_draws' fp64 samples (before the std scale): the oracle's, bit for bit
+            normal_pair_f(v.a, v.b, &z[0], &z[1]);
+            normal_pair_f(v.c, v.d, &z[2], &z[3]);
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {   // race_noise_draws' float samples (before the std scale)
-                const float u1 = (float(x[2 * p] >> 8) + 1.0f) * float(1.0 / 16777216.0);
-                const float u2 = float(x[2 * p + 1] >> 8) * float(1.0 / 16777216.0);
-                const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-                dst[(3 + 2 * p) * kQuadDrones] = r * __builtin_amdgcn_cosf(u2);
-                dst[(4 + 2 * p) * kQuadDrones] = r * __builtin_amdgcn_sinf(u2);
-            }
+            for (int k = 0; k < 4; ++k) dst[(3 + k) * kQuadDrones] = z[k];
         }
     }
 }

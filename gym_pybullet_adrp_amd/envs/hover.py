@@ -6,6 +6,9 @@ observation/action spaces, same obs layout [pos, rpy, vel, ang_v, 15 past action
 reward max(0, 2-|p-(0,0,1)|^4), terminated |p-target|<1e-4, truncated by bounds / tilt /
 8 s.  Batched extras: ``num_envs``, ``device``, ``precision``, ``seed``, ``autoreset``
 and ``init_noise`` (per-reset uniform perturbation of the initial state, 0 = reference).
+``precision`` defaults to ``"fp64"`` (the reference integrates in float64; held to 1e-9 of the
+float64 CPU restatement per env.step); ``"fp32"`` is the faster float32 kernel, held to the north
+star's 1e-4.
 
 ``step``/``reset`` take and return torch tensors that live on the GPU (no host copy):
 obs [E, 1, D] float32, reward [E] float32, terminated / truncated [E] bool.
@@ -35,7 +38,7 @@ class HoverAviary(AviaryEnv):
     def __init__(self, drone_model: DroneModel = DroneModel.CF2X, initial_xyzs=None, initial_rpys=None,
                  physics: Physics = Physics.PYB, pyb_freq: int = 240, ctrl_freq: int = 30, gui=False,
                  record=False, obs: ObservationType = ObservationType.KIN, act: ActionType = ActionType.RPM,
-                 *, num_envs: int = 1, device: int = 0, precision: str = "fp32", seed: int = 0,
+                 *, num_envs: int = 1, device: int = 0, precision: str = "fp64", seed: int = 0,
                  autoreset: bool = True, init_noise=None, env_offset: int = 0, link_frame_lag: bool = True):
         if drone_model != DroneModel.CF2X:
             raise ValueError("only DroneModel.CF2X (cf2x_IROS.urdf) is supported")

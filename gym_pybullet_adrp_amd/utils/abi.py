@@ -17,6 +17,7 @@ PHYS_PYB, PHYS_DYN, PHYS_PYB_GND, PHYS_PYB_DRAG, PHYS_PYB_DW, PHYS_PYB_GND_DRAG_
 ACT_RPM, ACT_ONE_D_RPM, ACT_FULLSTATE, ACT_PID, ACT_VEL, ACT_ONE_D_PID = 0, 1, 2, 3, 4, 5
 MATH_RCP, MATH_RSQ, MATH_SQRT, MATH_SIN_SMALL, MATH_COS_SMALL, MATH_ATAN2, MATH_ASIN, MATH_EXP = range(8)   # adrp_math_probe
 MATH_SQRT_NN, MATH_RCP_NC, MATH_RSQ_NC, MATH_SIN_TINY, MATH_COS_TINY = 8, 9, 10, 11, 12
+MATH_EXPMAP_SINC, MATH_EXPMAP_COS, MATH_QUAT_INV_NORM, MATH_NORMAL_Z0, MATH_NORMAL_Z1 = 13, 14, 15, 16, 17
 RACE_COMPARE, RACE_COMPETE = 0, 1
 POLICY_TANH, POLICY_RELU = 0, 1
 POLICY_RAW, POLICY_RELATIVE, POLICY_ABSOLUTE = 0, 1, 2

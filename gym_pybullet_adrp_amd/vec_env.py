@@ -82,7 +82,13 @@ class AviaryVecEnv(_VecEnvBase):
         act_shape = tuple(getattr(env, "_act_shape", (E,) + tuple(self.action_space.shape)))
         self._act_host = torch.zeros(act_shape, dtype=torch.float32, pin_memory=pin)
         self._act_dev = torch.zeros(act_shape, dtype=torch.float32, device=dev)
-        self._event = torch.cuda.Event() if pin else None
+        # the copies and the step run on the env device's current stream, which need not be the current
+        # device's: the event is created on and recorded into that stream
+        if pin:
+            with torch.cuda.device(dev):
+                self._event = torch.cuda.Event()
+        else:
+            self._event = None
 
     # ---- conversion ----
     def _out(self, x):
@@ -106,7 +112,7 @@ class AviaryVecEnv(_VecEnvBase):
         h = self._host[self._slot]
         h.copy_(self._dev, non_blocking=True)
         if self._event is not None:
-            self._event.record()
+            self._event.record(torch.cuda.current_stream(self._dev.device))
             self._event.synchronize()
         return self._views[self._slot]
 

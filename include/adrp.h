@@ -336,6 +336,11 @@ int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_d
 #define ADRP_MATH_RSQ_NC 10        /* finite, positive x (quaternion norm) */
 #define ADRP_MATH_SIN_TINY 11      /* |x| <= 0.03 (exp-map half angle) */
 #define ADRP_MATH_COS_TINY 12      /* |x| <= 0.03 */
+#define ADRP_MATH_EXPMAP_SINC 13   /* sin(x)/x of the hover exp map (per-lane series choice) */
+#define ADRP_MATH_EXPMAP_COS 14    /* cos(x) of the hover exp map */
+#define ADRP_MATH_QUAT_INV_NORM 15 /* 1/sqrt(n2) of the hover exp-map quaternion (per-lane form) */
+#define ADRP_MATH_NORMAL_Z0 16     /* race action-noise Box-Muller of a Philox word pair: in[i]'s bits */
+#define ADRP_MATH_NORMAL_Z1 17     /*   = x1 << 32 | x0; out = z0 / z1 (float samples, as doubles) */
 int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream);
 
 #ifdef __cplusplus

@@ -76,6 +76,8 @@ def _load():
     lib.orc_race_reward.restype = D
     lib.orc_race_command.argtypes = [P, P, P]
     lib.orc_set_noise.argtypes = [P, P, P]
+    lib.orc_race_moment_margin.argtypes = [P, P]
+    lib.orc_normal_pair.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P]
     lib.orc_get_command_state.argtypes = [P, P, P]
     lib.orc_set_command_state.argtypes = [P, P, P]
     lib.orc_poly4d_eval.argtypes = [P, ctypes.c_float, P]
@@ -189,6 +191,14 @@ class Oracle:
         assert f.shape == (self.nf, self.E * self.N) and i.shape == (self.ni, self.E * self.N)
         lib().orc_set_state(self.h, _ptr(f), _ptr(i))
 
+    def moment_margin(self):
+        """[E*N] per drone slot: the smallest distance of a firmware moment (control_t roll / pitch / yaw
+        before the int16 cast) to a truncation point (a nonzero integer) over the last env.step's
+        firmware calls; inf if no call produced moments"""
+        out = np.zeros(self.E * self.N, np.float32)
+        assert lib().orc_race_moment_margin(self.h, _ptr(out)) == 0
+        return out
+
     def contact_count(self):
         return lib().orc_contact_count(self.h)
 
@@ -243,6 +253,13 @@ def dslpid(cfg, dt, inp, st):
     o = np.zeros(4)
     lib().orc_dslpid(ctypes.byref(cfg), dt, _ptr(i), _ptr(st), _ptr(o))
     return o
+
+
+def normal_pair(x0, x1):
+    """the race action-noise Box-Muller of one Philox word pair (oracle/race.c normal_pair)"""
+    z = np.zeros(2, np.float32)
+    lib().orc_normal_pair(int(x0) & 0xFFFFFFFF, int(x1) & 0xFFFFFFFF, _ptr(z))
+    return z
 
 
 def philox(ctr, key):

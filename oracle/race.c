@@ -71,6 +71,9 @@ typedef struct rdrone_s {
     float i_err[3], i_err_m[3];
     float prev_omega_roll, prev_omega_pitch, prev_sp_roll, prev_sp_pitch;
     float ctl[4];                    /* control_t roll, pitch, yaw (int16 values), thrust */
+    float mom_margin;                /* diagnostic, not state: over this env.step's firmware calls, the
+                                        smallest distance of a clamped moment to a point where its int16
+                                        truncation changes (a nonzero integer) */
     /* race progress */
     int gate, elim, fin;
     /* command state (adrp.h ADRP_CMD_NF / ADRP_CMD_NI order): setpoint_t fields the controller
@@ -218,9 +221,15 @@ static void mellinger_fw(rdrone_t* d, const float gyro[3], const float st_pos[3]
     M.z = -MEL_KR_Z * eR.z + MEL_KW_Z * ew.z + MEL_KI_M_Z * d->i_err_m[2];
     d->ctl[3] = MEL_MASS_THRUST * current_thrust;
     if (d->ctl[3] > 0) {   /* control_t roll/pitch/yaw are int16: C float->int truncation */
-        d->ctl[0] = (float)(int16_t)clampf_(M.x, -32000, 32000);
-        d->ctl[1] = (float)(int16_t)clampf_(M.y, -32000, 32000);
-        d->ctl[2] = (float)(int16_t)clampf_(-M.z, -32000, 32000);
+        const float mc[3] = {clampf_(M.x, -32000, 32000), clampf_(M.y, -32000, 32000), clampf_(-M.z, -32000, 32000)};
+        for (int k = 0; k < 3; ++k) {
+            const float a = fabsf(mc[k]);
+            const float dist = a < 1.0f ? 1.0f - a : fabsf(a - rintf(a));
+            if (dist < d->mom_margin) d->mom_margin = dist;
+        }
+        d->ctl[0] = (float)(int16_t)mc[0];
+        d->ctl[1] = (float)(int16_t)mc[1];
+        d->ctl[2] = (float)(int16_t)mc[2];
     } else {
         d->ctl[0] = d->ctl[1] = d->ctl[2] = 0;
         mellinger_reset(d);
@@ -736,17 +745,64 @@ static int race_alloc(orc_t* o) {
     return ADRP_OK;
 }
 
+/* Box-Muller of one Philox pair from IEEE float operations only (+ - * /, sqrtf, fmaf, frexpf, rintf;
+   C float arithmetic, no contraction), so the fp64 kernels (adrp_device.h normal_pair_f, the same
+   sequence) draw bit-identical action noise: u1 = (x0 >> 8 + 1) 2^-24 in (0, 1], u2 = (x1 >> 8) 2^-24
+   in [0, 1); r = sqrt(-2 log u1) with log u1 = e ln2 + 2 atanh(s), s = (m - 1) / (m + 1),
+   m in [sqrt(1/2), sqrt(2)); (sin, cos)(2 pi u2) from the octant n = rint(8 u2) and the Taylor pair
+   on |x| = |2 pi (u2 - n / 8)| <= pi / 8.  Accuracy ~2 float ulp: the samples are float, scaled by the
+   noise std in double. */
+static void normal_pair_f(uint32_t x0, uint32_t x1, float* z0, float* z1) {
+    const float u1 = ((float)(x0 >> 8) + 1.0f) * (1.0f / 16777216.0f);
+    const float u2 = (float)(x1 >> 8) * (1.0f / 16777216.0f);
+    int e;
+    float m = frexpf(u1, &e);                       /* u1 = m 2^e, m in [0.5, 1) */
+    if (m < 0.70710677f) { m = m * 2.0f; e -= 1; }
+    const float s = (m - 1.0f) / (m + 1.0f);
+    const float z = s * s;
+    float p = 1.0f / 11;
+    p = fmaf(p, z, 1.0f / 9); p = fmaf(p, z, 1.0f / 7); p = fmaf(p, z, 1.0f / 5); p = fmaf(p, z, 1.0f / 3);
+    const float lm = fmaf(2.0f * s * z, p, 2.0f * s);  /* log m = 2 s (1 + z/3 + ... + z^5/11) */
+    const float fe = (float)e;
+    const float lg = fmaf(fe, 0.693145751953125f, fmaf(fe, 1.428606765330187e-06f, lm));
+    const float r = sqrtf(-2.0f * lg);
+    const float n = rintf(u2 * 8.0f);
+    const float x = (u2 - n * 0.125f) * 6.28318548f;
+    const float x2 = x * x;
+    float ps = -1.98412698e-4f;
+    ps = fmaf(ps, x2, 8.33333377e-3f); ps = fmaf(ps, x2, -0.166666672f);
+    float pc = 2.48015876e-5f;
+    pc = fmaf(pc, x2, -1.38888892e-3f); pc = fmaf(pc, x2, 4.16666679e-2f); pc = fmaf(pc, x2, -0.5f);
+    const float sx = fmaf(x * x2, ps, x), cx = fmaf(x2, pc, 1.0f);
+    const float h = 0.70710677f;
+    const float a = h * (cx + sx), b = h * (cx - sx);
+    float sn, cs;
+    switch ((int)n & 7) {
+        case 0: sn = sx; cs = cx; break;
+        case 1: sn = a; cs = b; break;
+        case 2: sn = cx; cs = -sx; break;
+        case 3: sn = b; cs = -a; break;
+        case 4: sn = -sx; cs = -cx; break;
+        case 5: sn = -a; cs = -b; break;
+        case 6: sn = -cx; cs = sx; break;
+        default: sn = -b; cs = a; break;
+    }
+    *z0 = r * cs;
+    *z1 = r * sn;
+}
+
 static void draw_normal4(uint64_t seed, uint64_t gid, uint32_t ep, uint32_t tag, uint32_t idx, double z[4]) {
-    /* Box-Muller on one Philox block: u1 in (0,1], u2 in [0,1) */
     uint32_t cc[4] = {(uint32_t)gid, ep, tag, idx}, k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)}, x[4];
     orc_philox4x32_10(cc, k, x);
-    for (int p = 0; p < 2; ++p) {
-        double u1 = ((double)(x[2 * p] >> 8) + 1.0) * (1.0 / 16777216.0);
-        double u2 = (double)(x[2 * p + 1] >> 8) * (1.0 / 16777216.0);
-        double r = sqrt(-2.0 * log(u1));
-        z[2 * p] = r * cos(2 * PI * u2);
-        z[2 * p + 1] = r * sin(2 * PI * u2);
-    }
+    float f[4];
+    normal_pair_f(x[0], x[1], &f[0], &f[1]);
+    normal_pair_f(x[2], x[3], &f[2], &f[3]);
+    for (int j = 0; j < 4; ++j) z[j] = f[j];
+}
+
+int orc_normal_pair(uint32_t x0, uint32_t x1, float* z) {   /* (tests: accuracy, GPU bit-identity) */
+    normal_pair_f(x0, x1, &z[0], &z[1]);
+    return 0;
 }
 
 static v3 body_ang_v(const orc_t* o, const body_t* b) {   /* getBaseVelocity angular part */
@@ -1064,6 +1120,7 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
     body_t* bs = &o->b[(size_t)e * N];
     rdrone_t* ds = &o->rd[(size_t)e * N];
     int touched = 0;
+    for (int i = 0; i < N; ++i) ds[i].mom_margin = INFINITY;
     /* the command message per drone (190-210): FULLSTATE (act[:3], 0, 0, act[3], 0, step_counter)
        from an ndarray action (act = NULL: the commands adrp_race_command / orc_race_command sent);
        eliminated drones get STOP [step_counter] */
@@ -1252,6 +1309,14 @@ static void race_set_row(orc_t* o, size_t slot, int e, int first, const double* 
     }
     d->tick = iv[2]; d->last_att_tick = iv[3]; d->last_pos_tick = iv[4]; d->tumble = iv[5]; d->gate = iv[6];
     d->elim = iv[7] & 1; d->fin = (iv[7] >> 1) & 1;
+}
+
+/* per drone slot: the smallest distance of a firmware moment to an int16 truncation point over the
+   firmware calls of the last env.step (+inf: no call with positive thrust) */
+int orc_race_moment_margin(const orc_t* o, float* out) {
+    if (!o->rd) return ADRP_ERR_INVALID;
+    for (size_t k = 0; k < (size_t)o->E * o->N; ++k) out[k] = o->rd[k].mom_margin;
+    return 0;
 }
 
 int orc_set_noise(orc_t* o, const double* act_noise, const double* force) {

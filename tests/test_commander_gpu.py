@@ -143,7 +143,7 @@ def test_tuple_actions_through_step():
     """the reference's list-of-tuples action (E = 1) through MultiRaceAviary.step, and ndarray
     actions in command mode (FULLSTATE sent by the step kernel) against the oracle"""
     N = 2
-    env = MultiRaceAviary("level0", num_drones=N, num_envs=1, seed=3, autoreset=False)
+    env = MultiRaceAviary("level0", num_drones=N, precision="fp32", num_envs=1, seed=3, autoreset=False)
     orc = O.Oracle(env.cfg.copy())
     env.reset()
     obs0 = orc.reset()
@@ -172,8 +172,8 @@ def test_tuple_actions_through_step():
 def test_enable_commands_matches_reset_state():
     """adrp_enable_commands after a reset leaves what a reset in command mode leaves"""
     E, N = 16, 3
-    a = MultiRaceAviary("level2", num_drones=N, num_envs=E, seed=8, autoreset=False)
-    b = MultiRaceAviary("level2", num_drones=N, num_envs=E, seed=8, autoreset=False, commands=True)
+    a = MultiRaceAviary("level2", num_drones=N, precision="fp32", num_envs=E, seed=8, autoreset=False)
+    b = MultiRaceAviary("level2", num_drones=N, precision="fp32", num_envs=E, seed=8, autoreset=False, commands=True)
     a.reset()
     b.reset()
     a.enable_commands()
@@ -198,7 +198,7 @@ def test_commands_after_ndarray_steps(obs_wrapper):
     the oracle's (which runs the command path on every step) and so must the next steps."""
     from gym_pybullet_adrp_amd.utils.wrapper import DroneObservationWrapper
     E, N = 32, 2
-    env = MultiRaceAviary("level0", num_drones=N, num_envs=E, seed=5, autoreset=False)
+    env = MultiRaceAviary("level0", num_drones=N, precision="fp32", num_envs=E, seed=5, autoreset=False)
     wenv = DroneObservationWrapper(env) if obs_wrapper else env
     orc = O.Oracle(env.cfg.copy())
     wenv.reset()
@@ -299,7 +299,7 @@ def test_hardcoded_controller_free_flight():
     E, N = 256, 2
     env = MultiRaceAviary("getting_started", num_drones=N, racemode=RaceMode.COMPARE, num_envs=E, seed=1,
                           autoreset=False, precision="fp64")
-    orc = O.Oracle(MultiRaceAviary("getting_started", num_drones=N, racemode=RaceMode.COMPARE, num_envs=1,
+    orc = O.Oracle(MultiRaceAviary("getting_started", num_drones=N, racemode=RaceMode.COMPARE, precision="fp32", num_envs=1,
                                    seed=1, autoreset=False).cfg.copy())
     obs, _ = env.reset()
     orc.reset()

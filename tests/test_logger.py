@@ -32,7 +32,7 @@ def test_device_logger_hover(tmp_path, physics, act):
     from gym_pybullet_adrp_amd.logger import DeviceLogger
     from gym_pybullet_adrp_amd.utils.enums import ActionType, Physics
     from oracle import oracle as O
-    env = HoverAviary(physics=Physics[physics], act=ActionType[act], num_envs=64, initial_xyzs=[0, 0, 1.0],
+    env = HoverAviary(physics=Physics[physics], act=ActionType[act], precision="fp32", num_envs=64, initial_xyzs=[0, 0, 1.0],
                       autoreset=False)
     env.reset()
     slots = [0, 5, 63]
@@ -73,7 +73,7 @@ def test_device_logger_race(tmp_path):
     import torch
     from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary
     from gym_pybullet_adrp_amd.logger import DeviceLogger
-    env = MultiRaceAviary("level0", num_drones=2, num_envs=32, seed=1)
+    env = MultiRaceAviary("level0", num_drones=2, precision="fp32", num_envs=32, seed=1)
     obs, _ = env.reset()
     lg = DeviceLogger(env, 25, output_folder=str(tmp_path), duration_steps=8)   # env 0's two drones
     act = torch.cat([obs[..., :3] + 0.2, torch.zeros_like(obs[..., :1])], -1).contiguous()

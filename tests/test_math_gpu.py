@@ -97,3 +97,66 @@ def test_exp():
     ok = ref > L(1e-300)
     assert rel_err(got[ok], ref[ok]).max() < ULP4
     assert got[-1] == 0.0
+
+
+def test_non_finite_inputs():
+    """NaN in -> NaN out for atan2 (fmax / fmin drop a NaN), sqrt(+inf) = +inf"""
+    nan, inf = np.nan, np.inf
+    got = probe(abi.MATH_ATAN2, np.array([nan, 1.0, nan, 0.0]), np.array([nan, nan, 1.0, nan]))
+    assert np.isnan(got).all()
+    got = probe(abi.MATH_ASIN, np.array([nan]))
+    assert np.isnan(got).all()
+    s = probe(abi.MATH_SQRT, np.array([inf, 0.0, -0.0, 4.0, -1.0, nan]))
+    assert s[0] == inf and s[1] == 0.0 and s[3] == 2.0 and np.isnan(s[4]) and np.isnan(s[5])
+    assert np.signbit(s[2])
+
+
+@pytest.mark.parametrize("fn", ["sinc", "cos", "norm"])
+def test_exp_map_forms_are_per_lane(fn):
+    """the hover fp64 exp map picks the short series (|x| <= 0.03) and the Newton norm
+    (|n2 - 1| <= 1e-9) per lane.  A lane's result must not depend on its 63 wave neighbours: the same
+    inputs probed in a wave of like lanes and in waves mixed with lanes that take the other form give
+    bit-identical results, and each form is accurate on its own range."""
+    rng = np.random.default_rng(5)
+    if fn == "norm":
+        fid = abi.MATH_QUAT_INV_NORM
+        near = 1.0 + rng.uniform(-1e-9, 1e-9, 64 * 64)
+        far = 1.0 + rng.uniform(-1e-3, 1e-3, 64 * 64)
+        far = far[np.abs(far - 1) > 1e-9]
+        ref = lambda v: 1 / np.sqrt(v.astype(L))
+        tol = ULP4
+    else:
+        fid = abi.MATH_EXPMAP_SINC if fn == "sinc" else abi.MATH_EXPMAP_COS
+        near = rng.uniform(-0.03, 0.03, 64 * 64)
+        far = rng.uniform(0.031, np.pi / 8, 64 * 64) * rng.choice([-1, 1], 64 * 64)
+        ref = (lambda v: np.sin(v.astype(L)) / v.astype(L)) if fn == "sinc" else (lambda v: np.cos(v.astype(L)))
+        tol = ULP4
+    alone_near, alone_far = probe(fid, near), probe(fid, far[:len(near)])
+    mixed = np.empty(2 * len(near))
+    mixed[0::2], mixed[1::2] = near, far[:len(near)]      # every wave holds both forms
+    got = probe(fid, mixed)
+    np.testing.assert_array_equal(got[0::2], alone_near)
+    np.testing.assert_array_equal(got[1::2], alone_far)
+    assert rel_err(alone_near, ref(near)).max() < tol
+    assert rel_err(alone_far, ref(far[:len(near)])).max() < tol
+
+
+def test_race_noise_box_muller_matches_oracle():
+    """the fp64 race kernels' action noise (normal_pair_f, IEEE float operations only) is the
+    oracle's (oracle/race.c normal_pair_f) bit for bit on the same Philox words; both are within 2
+    float ulp of the float64 libm Box-Muller"""
+    from oracle import oracle as O
+    rng = np.random.default_rng(11)
+    w = rng.integers(0, 2 ** 32, (4096, 2), dtype=np.uint64)
+    w = np.concatenate([w, np.array([[0xFFFFFFFF, 0], [0, 0xFFFFFFFF], [0, 0x80000000], [0x100, 0x1234567]], np.uint64)])
+    bits = (w[:, 1] << np.uint64(32)) | w[:, 0]
+    x = bits.view(np.float64)
+    z0, z1 = probe(abi.MATH_NORMAL_Z0, x), probe(abi.MATH_NORMAL_Z1, x)
+    ref = np.array([O.normal_pair(a, b) for a, b in w], np.float64)
+    np.testing.assert_array_equal(z0, ref[:, 0])
+    np.testing.assert_array_equal(z1, ref[:, 1])
+    u1 = ((w[:, 0] >> np.uint64(8)).astype(np.float64) + 1) / 2 ** 24
+    u2 = (w[:, 1] >> np.uint64(8)).astype(np.float64) / 2 ** 24
+    r = np.sqrt(-2 * np.log(u1))
+    assert (np.abs(z0 - r * np.cos(2 * np.pi * u2)) <= 2.5e-7 * np.maximum(r, 1e-30) + 1e-30).all()
+    assert (np.abs(z1 - r * np.sin(2 * np.pi * u2)) <= 2.5e-7 * np.maximum(r, 1e-30) + 1e-30).all()

@@ -10,8 +10,6 @@ call order from a gymnasium-style seeded numpy Generator).
 CPU: the injected arrays are laid out and consumed as the oracle's own Philox draws (feeding the
 Philox values back through injection is bit-identical).  GPU (-m gpu): the kernels consume the
 injected reference-order draws as the oracle does (teacher-forced env.steps)."""
-import math
-
 import numpy as np
 import pytest
 
@@ -72,12 +70,10 @@ def philox_draws(cfg, ints, names):
                     uk = float(u[k] >> 8) * (1.0 / 16777216.0)
                     force[e, i, s, k] = t.dyn_dist_low[k] + (t.dyn_dist_high[k] - t.dyn_dist_low[k]) * uk
                 x = O.philox([gid, int(ep[e]), TAG_RACE_NOISE | i, idx], key)
-                for p in range(2):
-                    u1 = (float(x[2 * p] >> 8) + 1.0) * (1.0 / 16777216.0)
-                    u2 = float(x[2 * p + 1] >> 8) * (1.0 / 16777216.0)
-                    r = math.sqrt(-2.0 * math.log(u1))
-                    act[e, i, s, 2 * p] = r * math.cos(2 * math.pi * u2) * t.action_noise_std
-                    act[e, i, s, 2 * p + 1] = r * math.sin(2 * math.pi * u2) * t.action_noise_std
+                for p in range(2):   # race.c normal_pair_f: float samples, scaled by the std in double
+                    z = O.normal_pair(x[2 * p], x[2 * p + 1]).astype(np.float64)
+                    act[e, i, s, 2 * p] = z[0] * t.action_noise_std
+                    act[e, i, s, 2 * p + 1] = z[1] * t.action_noise_std
     return act, force
 
 

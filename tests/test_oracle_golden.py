@@ -155,3 +155,19 @@ def test_philox_known_answers():
     assert [hex(x) for x in O.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344],
                                      [0xa4093822, 0x299f31d0])] == \
         ["0xd16cfe09", "0x94fdcceb", "0x5001e420", "0x24126ea1"]
+
+
+def test_race_noise_box_muller_accuracy():
+    """oracle/race.c normal_pair_f (the race action noise, shared bit for bit with the fp64 kernels):
+    within 2 float ulp of the float64 libm Box-Muller on the same Philox words, edge words included"""
+    import math
+    rng = np.random.default_rng(3)
+    words = [tuple(int(v) for v in rng.integers(0, 2 ** 32, 2)) for _ in range(5000)]
+    words += [(0xFFFFFFFF, 0), (0, 0xFFFFFFFF), (0, 0x80000000), (0x100, 0x1234567), (0, 0)]
+    for x0, x1 in words:
+        z = O.normal_pair(x0, x1).astype(np.float64)
+        u1 = ((x0 >> 8) + 1) / 16777216.0
+        u2 = (x1 >> 8) / 16777216.0
+        r = math.sqrt(-2 * math.log(u1))
+        ref = np.array([r * math.cos(2 * math.pi * u2), r * math.sin(2 * math.pi * u2)])
+        assert np.abs(z - ref).max() <= 2.5e-7 * max(r, 1e-30) + 1e-30, (x0, x1, z, ref)

@@ -77,7 +77,7 @@ def test_closed_loop_race_rollout_graph():
     env.step + one policy launch per iteration, captured in a HIP graph; the setpoints fed to
     each step equal the oracle policy of that step's observation."""
     from gym_pybullet_adrp_amd.envs.race import MultiRaceAviary
-    env = MultiRaceAviary("level0", num_drones=2, num_envs=512, seed=5)
+    env = MultiRaceAviary("level0", num_drones=2, precision="fp32", num_envs=512, seed=5)
     pol, w, relu = make("example_RL_model", "relative")
     obs, _ = env.reset()
     act = torch.empty((512, 2, 4), device=obs.device)

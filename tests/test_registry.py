@@ -22,15 +22,25 @@ def test_gymnasium_registration_when_available():
         assert gym.envs.registration.registry[env_id].entry_point == entry
 
 
+def test_default_precision_is_the_references():
+    """the reference integrates in float64: both envs default to the fp64 kernels"""
+    import inspect
+    from gym_pybullet_adrp_amd.envs import HoverAviary, MultiRaceAviary
+    for c in (HoverAviary, MultiRaceAviary):
+        assert inspect.signature(c.__init__).parameters["precision"].default == "fp64"
+
+
 @pytest.mark.gpu
 def test_make_builds_the_batched_env():
     env = pkg.make("multi-race-aviary-v0", race_config="level1", num_drones=2, num_envs=8)
     obs, _ = env.reset()
     assert tuple(obs.shape) == (8, 2, 49)
+    assert env.cfg.precision == 1 and env.kernel_name.startswith("race_step<f64,")   # the default
     env.close()
     env = pkg.make("hover-aviary-v0", num_envs=16)
     obs, _ = env.reset()
     assert tuple(obs.shape) == (16, 1, 72)
+    assert env.cfg.precision == 1 and env.kernel_name.startswith("hover_step<f64,")
     env.close()
 
 

@@ -125,3 +125,78 @@ def test_packed_gather_one_rank():
         ref.close()
     finally:
         dist.destroy_process_group()
+
+
+def _nccl_world1():
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    return dist
+
+
+def test_packed_gather_rccl_graph():
+    """the north star's RCCL obs all-gather on the one GPU a box has: a world-1 "nccl" (RCCL) group,
+    BASELINE config 5's per-GPU workload (level3 / COMPETE / 4 drones / PYB_DW / disturbances, 4,096
+    envs, auto-reset) in ShardedAviary(packed=True); step_gather (env.step + all_gather_into_tensor of
+    the packed send buffer) captured in ONE HIP graph and replayed 20 times: after every replay the
+    gathered obs / reward / flags equal, bit for bit, an unsharded env stepped eagerly on the same
+    actions (sharding.py:98-115)"""
+    import functools
+    from gym_pybullet_adrp_amd.sharding import ShardedAviary
+    dist = _nccl_world1()
+    try:
+        E = E_SHARD
+        make = functools.partial(MultiRaceAviary, "level3", num_drones=N, physics=Physics.PYB_DW,
+                                 racemode=RaceMode.COMPETE, seed=2024, autoreset=True, reward="wrapper")
+        sh = ShardedAviary(E, make, packed=True)
+        ref = make(num_envs=E)
+        assert sh.env.kernel_name == ref.kernel_name == "race_step<f64,PYB_DW,G4,Q4>"
+        obs, _ = sh.reset()
+        obs_r, _ = ref.reset()
+        assert torch.equal(obs, obs_r)
+        acts = _actions(obs_r.clone(), obs_r.device)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            sh.step_gather(acts[0])                  # warm-up outside the capture (step 0)
+        torch.cuda.current_stream().wait_stream(side)
+        ref.step(acts[0])
+        a_buf = acts[1].clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = sh.step_gather(a_buf)
+        done = 0
+        for k in range(1, 21):
+            a_buf.copy_(acts[k])
+            g.replay()
+            o, r, te, tr, _ = ref.step(acts[k])
+            torch.cuda.synchronize()
+            assert torch.equal(out.obs.reshape(E, N, -1), o), f"gathered obs differ at replay {k}"
+            assert torch.equal(out.rew.reshape(E), r)
+            assert torch.equal(out.term.reshape(E), te) and torch.equal(out.trunc.reshape(E), tr)
+            done += int((te | tr).sum())
+        assert done > 0, "the replays should include auto-resets"
+        sh.close()
+        ref.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("refuse", [False, True])
+def test_bench_gather_record_graph_and_eager_fallback(refuse):
+    """bench.py's config-5 all-gather record on a world-1 RCCL group: the graph-captured form (no
+    graph_capture_error), and with the capture refused the eager fallback (one launch + one
+    collective per step, timed under barriers) that bench.py takes then"""
+    import bench
+    dist = _nccl_world1()
+    try:
+        rec = bench.gather_record_world1(0, 64, 8, precision="fp64", E=512, refuse_capture=refuse)
+        assert rec["world"] == 1 and rec["backend"] == "nccl" and rec["value"] > 0
+        if refuse:
+            assert "graph_capture_error" in rec and rec["timed_region"].endswith("eager steps (step kernel + RCCL all-gather each)")
+        else:
+            assert "graph_capture_error" not in rec and "HIP graph" in rec["timed_region"]
+    finally:
+        dist.destroy_process_group()
