@@ -102,14 +102,14 @@ def launch_ranks(n):
     return subprocess.call(cmd)
 
 
-def launch_check(args, world, rank):
+def launch_check(args, world, rank, out=None):
     dist.init_process_group("gloo")
     seen = dist.get_world_size()
     t = torch.tensor([rank, 1], dtype=torch.int64)
     dist.all_reduce(t)
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_arg": args.gpus, "world_seen": seen,
-                          "ranks_reported": int(t[1]), "rank_sum": int(t[0])}), flush=True)
+                          "ranks_reported": int(t[1]), "rank_sum": int(t[0])}), file=out or sys.stdout, flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -610,17 +610,28 @@ def progress(msg):
     print(f"[bench {time.perf_counter() - _T0:6.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
+def _stdout_to_stderr():
+    """keep stdout for the ONE JSON line: libraries (RCCL prints its version banner when a
+    communicator comes up) write to fd 1 directly, so fd 1 goes to stderr and the record is printed
+    to a duplicate of the original stdout"""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
+    record_out = _stdout_to_stderr()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.launch_check:
-        return launch_check(args, world, rank)
+        return launch_check(args, world, rank, record_out)
     if torch.cuda.device_count() < world:
         sys.exit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPUs")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -724,7 +735,7 @@ def main():
         result["cpu_baseline"] = None
     if rank == 0:
         result["summary"] = summary(result)   # last key: the compact per-config view stays in a kept tail
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=record_out, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

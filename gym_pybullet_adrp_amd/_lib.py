@@ -85,6 +85,15 @@ def load():
     lib.adrp_policy_act.restype = I
     lib.adrp_policy_destroy.argtypes = [P]
     lib.adrp_policy_destroy.restype = None
+    if hasattr(lib, "adrp_policy_sample"):   # (A/B runs may load an older build without it)
+        lib.adrp_policy_create2.argtypes = [I, I, I, I, I, I, P, P, P, P, P, P, ctypes.POINTER(P)]
+        lib.adrp_policy_create2.restype = I
+        lib.adrp_policy_set_critic.argtypes = [P] + [P] * 7
+        lib.adrp_policy_set_critic.restype = I
+        lib.adrp_policy_sample.argtypes = [P, P, I, I, I, ctypes.c_uint64, ctypes.c_uint32, P, P, P, P, P, P]
+        lib.adrp_policy_sample.restype = I
+        lib.adrp_gae.argtypes = [P, P, P, P, P, I, I, ctypes.c_double, ctypes.c_double, P, P, P]
+        lib.adrp_gae.restype = I
     if hasattr(lib, "adrp_math_probe"):      # (A/B runs may load an older build without it)
         lib.adrp_math_probe.argtypes = [I, P, P, I, P]
         lib.adrp_math_probe.restype = I

@@ -177,6 +177,17 @@ __device__ __forceinline__ double sqrt_nn(double x) {
     const double d = fma_(-g, g, x);
     return fma_(d, h, g);
 }
+// x / c for a constant c > 0, equal to the IEEE (correctly rounded) quotient for normal x and quotient:
+// y = RN(1 / c) folds at compile time, q = RN(x y) is within 1 ulp of x / c, r = x - q c is exact
+// (one FMA), and RN(q + r y) = RN(x / c) (Markstein's correction theorem; checked on 1.4e9 random x
+// for each divisor the kernels use, and on the device by tests/test_math_gpu.py).  3 ops instead of the
+// ~12-op v_div_scale / v_div_fmas / v_div_fixup sequence; a zero quotient takes x's sign.
+__device__ __forceinline__ double div_c(double x, double c) {
+    const double y = 1.0 / c;
+    const double q = x * y;
+    const double r = fma_(-q, c, x);
+    return __builtin_copysign(fma_(r, y, q), x);
+}
 // sin / cos for |x| <= pi/8: Taylor to x^13 / x^14 (relative error <= 1.7e-16 before rounding)
 __device__ __forceinline__ void sincos_small(double x, double* s, double* c) {
     const double x2 = x * x;
@@ -195,6 +206,28 @@ __device__ __forceinline__ void sincos_small(double x, double* s, double* c) {
     pc = fma_(pc, x2, -0.5);
     *s = fma_(x * x2, ps, x);
     *c = fma_(x2, pc, 1.0);
+}
+// sin / cos for |x| < 2^20 (gate / part yaws, reset attitudes): octant n = rint(4 x / pi), r = x - n pi/4
+// (two-part pi/4 through FMAs, |r| <= pi/8), sincos_small(r), then the octant's rotation without a
+// branch: odd n starts from (sin, cos)(pi/4 + r) = sqrt(1/2) (c + s, c - s), bit 1 maps (s, c) ->
+// (c, -s), bit 2 negates both.  Within 2 ulp of the correctly rounded values (tests/test_math_gpu.py);
+// ~40 instructions where the libm sincos pays a range-reduction branch and ~3x the work.
+__device__ __forceinline__ void sincos_fast(double x, double* s, double* c) {
+    const double n = __builtin_rint(x * 1.2732395447351628);
+    double r = fma_(-n, 0.78539816339744828, x);
+    r = fma_(-n, 3.0616169978683830e-17, r);
+    double sx, cx;
+    sincos_small(r, &sx, &cx);
+    const double h = 0.70710678118654752440;
+    const double a = h * (cx + sx), b = h * (cx - sx);
+    const uint32_t o = uint32_t(int(n)) & 7u;
+    const bool odd = (o & 1u) != 0;
+    const double s0 = odd ? a : sx, c0 = odd ? b : cx;
+    const bool turn = (o & 2u) != 0;
+    const double s1 = turn ? c0 : s0, c1 = turn ? -s0 : c0;
+    const bool neg = (o & 4u) != 0;
+    *s = neg ? -s1 : s1;
+    *c = neg ? -c1 : c1;
 }
 // sin / cos for |x| <= 0.03 (the exp-map half angle |w| dt / 2 below 14 rad/s at 240 Hz): Taylor to
 // x^7 / x^8; the first omitted terms are x^8/9! = 1.8e-18 and x^10/10! = 1.6e-22 relative
@@ -269,6 +302,9 @@ __device__ __forceinline__ float sqrt_(float x) { return __fsqrt_rn(x); }
 __device__ __forceinline__ double sqrt_(double x) { return ::sqrt(x); }
 __device__ __forceinline__ void sincos_(float x, float* s, float* c) { sincosf(x, s, c); }
 __device__ __forceinline__ void sincos_(double x, double* s, double* c) { ::sincos(x, s, c); }
+// sincos_ for the kernels' angles (|x| < 2^20): fp64 the octant-reduced polynomial, fp32 libm
+__device__ __forceinline__ void sincos_f_(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __forceinline__ void sincos_f_(double x, double* s, double* c) { f64::sincos_fast(x, s, c); }
 __device__ __forceinline__ float atan2_(float y, float x) { return atan2f(y, x); }
 __device__ __forceinline__ double atan2_(double y, double x) { return ::atan2(y, x); }
 __device__ __forceinline__ float asin_(float x) { return asinf(x); }
@@ -281,6 +317,9 @@ __device__ __forceinline__ double fabs_(double x) { return fabs(x); }
 // latency-oriented primitives of the step loops: 1-ulp hardware ops in fp32, the refined
 // hardware approximations above in fp64 (sqrt_ / rsqrt_ / atan2_ / asin_ / exp_ / sincos_ keep
 // the correctly rounded / libm forms for code outside the loops)
+// x / c for a constant c: fp64 the correctly rounded f64::div_c, fp32 the IEEE division
+__device__ __forceinline__ double divc_(double x, double c) { return f64::div_c(x, c); }
+__device__ __forceinline__ float divc_(float x, float c) { return x / c; }
 __device__ __forceinline__ float rcp_(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ double rcp_(double x) { return f64::rcp(x); }
 __device__ __forceinline__ float hsqrt_(float x) { return __builtin_amdgcn_sqrtf(x); }
@@ -505,23 +544,25 @@ __device__ __forceinline__ Q4<Real> quat_from_euler(Real r, Real p, Real y) {
 }
 
 // getQuaternionFromEuler with the half-angle sin/cos from the small-angle polynomial when all
-// three half angles are within pi/8 (exact in fp32, as small_sincos), else from libm; fp64
-// is always libm
+// three half angles are within pi/8 (exact in fp32, as small_sincos; fp64: f64::sincos_small, within
+// an ulp of libm), else from libm (fp32) / the octant-reduced f64::sincos_fast (fp64)
 template <typename Real>
 __device__ __forceinline__ Q4<Real> quat_from_euler_fast(Real r, Real p, Real y) {
-    if constexpr (sizeof(Real) == 4) {
-        const Real hr = r * Real(0.5), hp = p * Real(0.5), hy = y * Real(0.5);
-        const Real lim = Real(0.39269908169872414);
-        if (fabs_(hr) <= lim && fabs_(hp) <= lim && fabs_(hy) <= lim) {
-            Real sr, cr, sp, cp, sy, cy;
-            small_sincos(hr, &sr, &cr);
-            small_sincos(hp, &sp, &cp);
-            small_sincos(hy, &sy, &cy);
-            return {sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy,
-                    cr * cp * sy - sr * sp * cy, cr * cp * cy + sr * sp * sy};
-        }
+    const Real hr = r * Real(0.5), hp = p * Real(0.5), hy = y * Real(0.5);
+    const Real lim = Real(0.39269908169872414);
+    Real sr, cr, sp, cp, sy, cy;
+    if (fabs_(hr) <= lim && fabs_(hp) <= lim && fabs_(hy) <= lim) {
+        small_sincos(hr, &sr, &cr);
+        small_sincos(hp, &sp, &cp);
+        small_sincos(hy, &sy, &cy);
+    } else {
+        if constexpr (sizeof(Real) == 4) return quat_from_euler(r, p, y);
+        sincos_f_(hr, &sr, &cr);
+        sincos_f_(hp, &sp, &cp);
+        sincos_f_(hy, &sy, &cy);
     }
-    return quat_from_euler(r, p, y);
+    return {sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy,
+            cr * cp * sy - sr * sp * cy, cr * cp * cy + sr * sp * sy};
 }
 
 // Box-Muller of one Philox word pair from IEEE float operations only (+ - * /, correctly rounded
@@ -558,10 +599,18 @@ __device__ __forceinline__ void normal_pair_f(uint32_t x0, uint32_t x1, float* z
     const float sx = __builtin_fmaf(x * x2, ps, x), cx = __builtin_fmaf(x2, pc, 1.0f);
     const float h = 0.70710677f;
     const float a = h * (cx + sx), b = h * (cx - sx);
-    const int o = int(n) & 7;
-    // octant table as selects: sin / cos of o pi / 4 + x
-    const float sn = o == 0 ? sx : o == 1 ? a : o == 2 ? cx : o == 3 ? b : o == 4 ? -sx : o == 5 ? -a : o == 6 ? -cx : -b;
-    const float cs = o == 0 ? cx : o == 1 ? b : o == 2 ? -sx : o == 3 ? -a : o == 4 ? -cx : o == 5 ? -b : o == 6 ? sx : a;
+    // sin / cos of o pi / 4 + x, o = n mod 8, branch-free (the oracle's octant table, the same values):
+    // odd o starts from (sin, cos)(pi / 4 + x) = (a, b), even o from (sx, cx); then the quadrant
+    // q = o >> 1 turns it by q pi / 2: bit 0 maps (s, c) -> (c, -s), bit 1 negates both
+    const uint32_t o = uint32_t(int(n)) & 7u;
+    const bool odd = (o & 1u) != 0;
+    const float s0 = odd ? a : sx, c0 = odd ? b : cx;
+    const bool turn = (o & 2u) != 0;
+    const uint32_t neg = (o & 4u) << 29;                    // sign bit when bit 2 is set
+    const float s1 = turn ? c0 : s0;
+    const float c1 = turn ? __uint_as_float(__float_as_uint(s0) ^ 0x80000000u) : c0;
+    const float sn = __uint_as_float(__float_as_uint(s1) ^ neg);
+    const float cs = __uint_as_float(__float_as_uint(c1) ^ neg);
     *z0 = r * cs;
     *z1 = r * sn;
 }

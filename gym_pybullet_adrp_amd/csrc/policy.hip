@@ -21,16 +21,19 @@ int seterr(adrp_t* h, int code, const std::string& msg);
 
 struct adrp_policy {
     int device = 0;
-    int in_dim = 0, h1 = 0, h2 = 0, relu = 0;
+    int in_dim = 0, h1 = 0, h2 = 0, relu = 0, act_dim = 4;
     int row_tiles = 0;       // 16-row tiles per block (ADRP_POLICY_RT; 0 = default)
     PolicyLayout L{};
     float* blob = nullptr;   // device fragment blob
+    PolicyLayout Lc{};       // critic (adrp_policy_set_critic)
+    float* critic = nullptr;
+    float* log_std = nullptr;
 };
 
 // Pre-permute the Linear weights (torch layout [out][in], row-major) into the per-lane MFMA
 // fragments policy_kernel reads (see policy_kernel.h for the k order).
 static std::vector<float> build_blob(int in_dim, int H1, int H2, const float* w1, const float* b1, const float* w2,
-                                     const float* b2, const float* w3, const float* b3, PolicyLayout* L) {
+                                     const float* b2, const float* w3, const float* b3, PolicyLayout* L, int n_out = 4) {
     const int T1 = H1 / 16, T2 = H2 / 16, S1 = kPolicyS1;
     L->in_dim = in_dim;
     L->f1 = 0;
@@ -58,11 +61,11 @@ static std::vector<float> build_blob(int in_dim, int H1, int H2, const float* w1
         for (int i = 0; i < 4; ++i)
             for (int l = 0; l < 64; ++l) {
                 const int out = l & 15, k = 16 * u + 4 * (l >> 4) + i;
-                v[L->f3 + (u * 4 + i) * 64 + l] = out < 4 ? w3[size_t(out) * H2 + k] : 0.0f;
+                v[L->f3 + (u * 4 + i) * 64 + l] = out < n_out ? w3[size_t(out) * H2 + k] : 0.0f;
             }
     memcpy(&v[L->b1], b1, sizeof(float) * H1);
     memcpy(&v[L->b2], b2, sizeof(float) * H2);
-    memcpy(&v[L->b3], b3, sizeof(float) * 4);
+    memcpy(&v[L->b3], b3, sizeof(float) * n_out);
     return v;
 }
 
@@ -107,7 +110,24 @@ static bool pow2_tiles(int h) { return h == 16 || h == 32 || h == 64 || h == 128
 extern "C" int adrp_policy_create(int device, int in_dim, int hidden1, int hidden2, int activation, const float* w1,
                                   const float* b1, const float* w2, const float* b2, const float* w3, const float* b3,
                                   adrp_policy_t** out) {
+    return adrp_policy_create2(device, in_dim, hidden1, hidden2, 4, activation, w1, b1, w2, b2, w3, b3, out);
+}
+
+static int upload(const std::vector<float>& v, float** dst) {
+    if (hipMalloc((void**)dst, v.size() * sizeof(float)) != hipSuccess) return ADRP_ERR_OOM;
+    if (hipMemcpy(*dst, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        hipFree(*dst);
+        *dst = nullptr;
+        return ADRP_ERR_DEVICE;
+    }
+    return ADRP_OK;
+}
+
+extern "C" int adrp_policy_create2(int device, int in_dim, int hidden1, int hidden2, int act_dim, int activation,
+                                   const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                                   const float* b3, adrp_policy_t** out) {
     if (!out) return seterr(nullptr, ADRP_ERR_INVALID, "out is NULL");
+    if (act_dim < 1 || act_dim > 4) return seterr(nullptr, ADRP_ERR_INVALID, "policy act_dim must be 1..4");
     *out = nullptr;
     if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3) return seterr(nullptr, ADRP_ERR_INVALID, "NULL weight pointer");
     if (in_dim < 1 || in_dim > 4 * kPolicyS1) return seterr(nullptr, ADRP_ERR_INVALID, "policy in_dim must be 1..64");
@@ -122,8 +142,9 @@ extern "C" int adrp_policy_create(int device, int in_dim, int hidden1, int hidde
     adrp_policy_t* p = new adrp_policy_t();
     p->device = device;
     p->in_dim = in_dim; p->h1 = hidden1; p->h2 = hidden2; p->relu = activation == ADRP_POLICY_RELU;
+    p->act_dim = act_dim;
     if (const char* env = getenv("ADRP_POLICY_RT")) p->row_tiles = atoi(env);
-    const std::vector<float> blob = build_blob(in_dim, hidden1, hidden2, w1, b1, w2, b2, w3, b3, &p->L);
+    const std::vector<float> blob = build_blob(in_dim, hidden1, hidden2, w1, b1, w2, b2, w3, b3, &p->L, act_dim);
     DeviceGuard g(device);
     if (hipMalloc((void**)&p->blob, blob.size() * sizeof(float)) != hipSuccess) {
         delete p;
@@ -143,12 +164,77 @@ extern "C" void adrp_policy_destroy(adrp_policy_t* p) {
     DeviceGuard g(p->device);
     hipDeviceSynchronize();
     hipFree(p->blob);
+    if (p->critic) hipFree(p->critic);
+    if (p->log_std) hipFree(p->log_std);
     delete p;
+}
+
+extern "C" int adrp_policy_set_critic(adrp_policy_t* p, const float* vw1, const float* vb1, const float* vw2,
+                                      const float* vb2, const float* vw3, const float* vb3, const float* log_std) {
+    if (!p || !vw1 || !vb1 || !vw2 || !vb2 || !vw3 || !vb3 || !log_std)
+        return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_set_critic: NULL argument");
+    DeviceGuard g(p->device);
+    if (p->critic) { hipFree(p->critic); p->critic = nullptr; }
+    if (p->log_std) { hipFree(p->log_std); p->log_std = nullptr; }
+    const std::vector<float> blob = build_blob(p->in_dim, p->h1, p->h2, vw1, vb1, vw2, vb2, vw3, vb3, &p->Lc, 1);
+    int rc = upload(blob, &p->critic);
+    if (rc == ADRP_OK) rc = upload(std::vector<float>(log_std, log_std + p->act_dim), &p->log_std);
+    if (rc != ADRP_OK) return seterr(nullptr, rc, "adrp_policy_set_critic: upload failed");
+    return ADRP_OK;
+}
+
+template <int T1, int T2>
+static hipError_t launch_sample(const adrp_policy_t* p, const PolicySampleArgs& a, hipStream_t s) {
+    constexpr int NW = T1 > T2 ? T1 : T2;
+    const dim3 grid((a.rows + 15) / 16), blk(2 * 64 * NW);
+    if (p->relu) hipLaunchKernelGGL((policy_sample_kernel<T1, T2, true>), grid, blk, 0, s, a);
+    else hipLaunchKernelGGL((policy_sample_kernel<T1, T2, false>), grid, blk, 0, s, a);
+    return hipGetLastError();
+}
+template <int T1>
+static hipError_t sample_t2(const adrp_policy_t* p, const PolicySampleArgs& a, hipStream_t s) {
+    switch (p->h2 / 16) {
+        case 1: return launch_sample<T1, 1>(p, a, s);
+        case 2: return launch_sample<T1, 2>(p, a, s);
+        case 4: return launch_sample<T1, 4>(p, a, s);
+        default: return launch_sample<T1, 8>(p, a, s);
+    }
+}
+
+extern "C" int adrp_policy_sample(adrp_policy_t* p, const float* obs_dev, int rows, int obs_stride, int mode,
+                                  uint64_t seed, uint32_t counter, float* env_act_dev, float* action_dev,
+                                  float* value_dev, float* logprob_dev, float* eps_dev, void* stream) {
+    if (!p || !obs_dev || !env_act_dev || !action_dev || !value_dev || !logprob_dev)
+        return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_sample: NULL argument");
+    if (!p->critic) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_sample: no critic (adrp_policy_set_critic)");
+    if (rows < 0 || obs_stride < p->in_dim) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_sample: rows / obs_stride");
+    if (mode != ADRP_POLICY_RAW && mode != ADRP_POLICY_RELATIVE && mode != ADRP_POLICY_ABSOLUTE)
+        return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_sample: mode");
+    if (mode != ADRP_POLICY_RAW && (p->act_dim != 4 || p->in_dim < 6))
+        return seterr(nullptr, ADRP_ERR_INVALID, "RELATIVE / ABSOLUTE need 4 actions (and the pose in obs[0:6])");
+    if (rows == 0) return ADRP_OK;
+    PolicySampleArgs a;
+    a.actor = p->blob; a.La = p->L; a.critic = p->critic; a.Lc = p->Lc; a.log_std = p->log_std;
+    a.obs = obs_dev; a.rows = rows; a.obs_stride = obs_stride; a.mode = mode; a.act_dim = p->act_dim;
+    a.seed = seed; a.counter = counter;
+    a.env_act = env_act_dev; a.action = action_dev; a.value = value_dev; a.log_prob = logprob_dev; a.eps = eps_dev;
+    DeviceGuard g(p->device);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    switch (p->h1 / 16) {
+        case 1: e = sample_t2<1>(p, a, s); break;
+        case 2: e = sample_t2<2>(p, a, s); break;
+        case 4: e = sample_t2<4>(p, a, s); break;
+        default: e = sample_t2<8>(p, a, s); break;
+    }
+    if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("policy sample launch: ") + hipGetErrorString(e));
+    return ADRP_OK;
 }
 
 extern "C" int adrp_policy_act(adrp_policy_t* p, const float* obs_dev, int rows, int obs_stride, int mode,
                                float* act_dev, void* stream) {
     if (!p || !obs_dev || !act_dev) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_act: NULL argument");
+    if (p->act_dim != 4) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_act: 4 actions (adrp_policy_sample takes 1..4)");
     if (rows < 0 || obs_stride < p->in_dim) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_act: rows / obs_stride");
     if (mode != ADRP_POLICY_RAW && mode != ADRP_POLICY_RELATIVE && mode != ADRP_POLICY_ABSOLUTE)
         return seterr(nullptr, ADRP_ERR_INVALID, "adrp_policy_act: mode");
@@ -165,5 +251,44 @@ extern "C" int adrp_policy_act(adrp_policy_t* p, const float* obs_dev, int rows,
         default: e = dispatch_t2<8>(p, obs_dev, rows, obs_stride, act_dev, mode, s); break;
     }
     if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("policy launch: ") + hipGetErrorString(e));
+    return ADRP_OK;
+}
+
+// ---- GAE (SB3 RolloutBuffer.compute_returns_and_advantage) -----------------------------------
+// one lane per env walks its n_steps backwards; every [step][env] access is coalesced across the
+// wave.  float32 arithmetic with the NumPy expression order (float32 arrays x Python floats).
+__global__ void __launch_bounds__(256) gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
+                                                  const float* __restrict__ starts, const float* __restrict__ last_val,
+                                                  const float* __restrict__ dones, int T, int E, float gamma, float gl,
+                                                  float* __restrict__ adv, float* __restrict__ ret) {
+#pragma clang fp contract(off)
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    float last = 0.0f;
+    float next_v = last_val[e], next_nt = 1.0f - dones[e];
+    for (int t = T - 1; t >= 0; --t) {
+        const size_t k = size_t(t) * E + e;
+        const float v = val[k];
+        const float delta = rew[k] + gamma * next_v * next_nt - v;
+        last = delta + gl * next_nt * last;   // gl = float32(gamma * gae_lambda): NumPy multiplies the two Python floats first
+        adv[k] = last;
+        ret[k] = last + v;
+        next_v = v;
+        next_nt = 1.0f - starts[k];
+    }
+}
+
+extern "C" int adrp_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
+                        const float* dones, int n_steps, int n_envs, double gamma, double gae_lambda, float* advantages,
+                        float* returns, void* stream) {
+    if (!rewards || !values || !episode_starts || !last_values || !dones || !advantages || !returns)
+        return seterr(nullptr, ADRP_ERR_INVALID, "adrp_gae: NULL argument");
+    if (n_steps < 0 || n_envs < 0) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_gae: sizes");
+    if (n_steps == 0 || n_envs == 0) return ADRP_OK;
+    hipLaunchKernelGGL(gae_kernel, dim3((n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, values,
+                       episode_starts, last_values, dones, n_steps, n_envs, float(gamma), float(gamma * gae_lambda), advantages,
+                       returns);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("gae launch: ") + hipGetErrorString(e));
     return ADRP_OK;
 }

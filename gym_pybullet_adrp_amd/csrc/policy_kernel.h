@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "adrp_device.h"
+
 namespace adrp {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -179,6 +181,156 @@ __global__ void __launch_bounds__(512) policy_kernel(const float* __restrict__ b
     }
     }
     __syncthreads();          // h1s / h2s are rewritten by the next row tile
+    }
+}
+
+// ---- PPO rollout step: actor + critic + diagonal-Gaussian sample ----------
+// SB3 2.3.2 OnPolicyAlgorithm.collect_rollouts: actions, values, log_probs = policy(obs) with
+// ActorCriticPolicy.forward(obs, deterministic=False): latent_pi / latent_vf = the two MLPs of
+// mlp_extractor, mean = action_net(latent_pi), value = value_net(latent_vf),
+// DiagGaussianDistribution(mean, exp(log_std)).sample() = mean + std * eps, log_prob = sum over the
+// action dims of Normal.log_prob; the env then gets clip(action, low, high) (and here the
+// RLController transform).  One block = 16 rows and 2 NW waves: waves [0, NW) run the actor's
+// hidden layers, waves [NW, 2 NW) the critic's, on their own LDS tiles (same barrier sequence);
+// wave 0 finishes the action, wave NW the value.  eps: one Philox4x32-10 block per row, counter
+// {row, counter, kTagPolicy, 0}, Box-Muller by normal_pair_f (the oracle's restatement draws the
+// same floats).
+constexpr uint32_t kTagPolicy = 0x504f4c00u;   // "POL"
+
+struct PolicySampleArgs {
+    const float* actor;   PolicyLayout La;      // fragment blobs (build_blob) of the two MLPs
+    const float* critic;  PolicyLayout Lc;
+    const float* log_std;                       // [act_dim]
+    const float* obs; int rows, obs_stride, mode, act_dim;
+    uint64_t seed; uint32_t counter;
+    float* env_act;     // [rows][act_dim == 4 ? 4 : act_dim] clip + transform
+    float* action;      // [rows][act_dim] the sample (rollout-buffer action)
+    float* value;       // [rows]
+    float* log_prob;    // [rows]
+    float* eps;         // [rows][act_dim] or null
+};
+
+// hidden layers of one MLP for the 16 rows of xb: unit tile w of layer 1 / 2 into h1s / h2s (two
+// barriers, taken by every wave of the block)
+template <int T1, int T2, bool RELU>
+__device__ __forceinline__ void policy_hidden(const float* __restrict__ blob, const PolicyLayout& L, int w, int lane,
+                                              const float (&xb)[kPolicyS1], float* h1s, float* h2s) {
+    const int g = lane >> 4;
+    const bool l1 = w < T1, l2 = w < T2;
+    if (l1) {
+        f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll
+        for (int s = 0; s < kPolicyS1; s += 2) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(blob[L.f1 + (w * kPolicyS1 + s) * 64 + lane], xb[s], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(blob[L.f1 + (w * kPolicyS1 + s + 1) * 64 + lane], xb[s + 1], a1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            h1s[(w * 4 + i) * 64 + lane] = policy_act<RELU>(a0[i] + a1[i] + blob[L.b1 + 16 * w + 4 * g + i]);
+    }
+    __syncthreads();
+    if (l2) {
+        f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll
+        for (int t = 0; t < T1; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; i += 2) {
+                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(blob[L.f2 + ((w * T1 + t) * 4 + i) * 64 + lane],
+                                                          h1s[(t * 4 + i) * 64 + lane], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(blob[L.f2 + ((w * T1 + t) * 4 + i + 1) * 64 + lane],
+                                                          h1s[(t * 4 + i + 1) * 64 + lane], a1, 0, 0, 0);
+            }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            h2s[(w * 4 + i) * 64 + lane] = policy_act<RELU>(a0[i] + a1[i] + blob[L.b2 + 16 * w + 4 * g + i]);
+    }
+    __syncthreads();
+}
+
+// the output layer (a 16-unit tile, outputs < n_out live) of the MLP whose layer-2 tiles are in h2s
+template <int T2>
+__device__ __forceinline__ f32x4 policy_out(const float* __restrict__ blob, const PolicyLayout& L, int lane,
+                                            const float* h2s) {
+    f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
+#pragma unroll
+    for (int u = 0; u < T2; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+            o0 = __builtin_amdgcn_mfma_f32_16x16x4f32(blob[L.f3 + (u * 4 + i) * 64 + lane], h2s[(u * 4 + i) * 64 + lane],
+                                                      o0, 0, 0, 0);
+            o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(blob[L.f3 + (u * 4 + i + 1) * 64 + lane],
+                                                      h2s[(u * 4 + i + 1) * 64 + lane], o1, 0, 0, 0);
+        }
+    return o0 + o1;
+}
+
+template <int T1, int T2, bool RELU>
+__global__ void __launch_bounds__(1024) policy_sample_kernel(PolicySampleArgs a) {
+    constexpr int NW = T1 > T2 ? T1 : T2;
+    __shared__ float h1s[2][T1 * 4 * 64];
+    __shared__ float h2s[2][T2 * 4 * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int net = wave >= NW ? 1 : 0;            // 0 actor, 1 critic
+    const int w = wave - net * NW;
+    const int g = lane >> 4;
+    const int row0 = blockIdx.x * 16;
+    const int r = row0 + (lane & 15);
+    const bool live = r < a.rows;
+    const float* xrow = a.obs + size_t(live ? r : row0) * a.obs_stride;
+    const PolicyLayout& L = net ? a.Lc : a.La;
+    const float* blob = net ? a.critic : a.actor;
+    float xb[kPolicyS1];
+#pragma unroll
+    for (int s = 0; s < kPolicyS1; ++s) {
+        const int k = 4 * s + g;
+        const float v = xrow[k < L.in_dim ? k : 0];
+        xb[s] = (live && k < L.in_dim) ? v : 0.0f;
+    }
+    policy_hidden<T1, T2, RELU>(blob, L, w, lane, xb, h1s[net], h2s[net]);
+    if (w != 0 || g != 0 || !live) return;          // lanes 0..15 of waves 0 / NW: row lane & 15
+    const f32x4 o = policy_out<T2>(blob, L, lane, h2s[net]);
+    if (net == 1) {                                  // value_net: output 0
+        a.value[r] = o[0] + blob[L.b3];
+        return;
+    }
+    // Philox block of this row -> 4 standard normals (act_dim <= 4 of them used)
+    const U4 u = philox4x32_10(U4{uint32_t(r), a.counter, kTagPolicy, 0u}, uint32_t(a.seed), uint32_t(a.seed >> 32));
+    float eps[4];
+    normal_pair_f(u.a, u.b, &eps[0], &eps[1]);
+    normal_pair_f(u.c, u.d, &eps[2], &eps[3]);
+    float act[4], clipped[4], lp = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bool on = i < a.act_dim;
+        const float mean = o[i] + blob[L.b3 + i];
+        const float ls = on ? a.log_std[i] : 0.0f;
+        const float sd = expf(ls);
+        const float x = mean + sd * eps[i];
+        // torch Normal.log_prob: -((x - loc)^2) / (2 var) - log(scale) - log(sqrt(2 pi))
+        const float d = x - mean;
+        const float l = -(d * d) / (2.0f * sd * sd) - ls - 0.91893853320467274f;
+        lp += on ? l : 0.0f;
+        act[i] = x;
+        clipped[i] = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+        if (on) {
+            a.action[size_t(r) * a.act_dim + i] = x;
+            if (a.eps) a.eps[size_t(r) * a.act_dim + i] = eps[i];
+        }
+    }
+    (void)act;
+    a.log_prob[r] = lp;
+    if (a.mode == POLICY_RAW) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (i < a.act_dim) a.env_act[size_t(r) * a.act_dim + i] = clipped[i];
+    } else {   // RLController / RLControllerTwoGates transform of the clipped action (act_dim 4)
+        const bool rel = a.mode == POLICY_RELATIVE;
+        const double px = rel ? double(xrow[0]) : 0.0, py = rel ? double(xrow[1]) : 0.0,
+                     pz = rel ? double(xrow[2]) : 0.0, pyaw = rel ? double(xrow[5]) : 0.0;
+        reinterpret_cast<float4*>(a.env_act)[r] =
+            make_float4(float(px + double(clipped[0])), float(py + double(clipped[1])), float(pz + double(clipped[2])),
+                        float(map2pi_d(pyaw + 0.0 * 3.141592653589793)));
     }
 }
 

@@ -474,7 +474,7 @@ __device__ __forceinline__ Real ray_cylinder(const Shape<Real>& s, V3<Real> p0, 
 template <typename Real>
 __device__ __forceinline__ M3<Real> rotz_(Real yaw) {
     Real s, c;
-    sincos_(yaw, &s, &c);
+    sincos_f_(yaw, &s, &c);
     return {c, -s, Real(0), s, c, Real(0), Real(0), Real(0), Real(1)};
 }
 template <typename Real>
@@ -780,11 +780,11 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
     Real acc_z = 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        rates[k] = F32 ? (rr[k] - d.prev_rpy[k]) * Real(500) : (rr[k] - d.prev_rpy[k]) / fdt;
+        rates[k] = F32 ? (rr[k] - d.prev_rpy[k]) * Real(500) : divc_(rr[k] - d.prev_rpy[k], fdt);
         d.prev_rpy[k] = rr[k];
         if (k == 2)
             acc_z = F32 ? (vv[k] - d.prev_vel[k]) * Real(500.0 / 9.8) + Real(1)
-                        : (vv[k] - d.prev_vel[k]) / fdt / Real(9.8) + Real(1);
+                        : divc_(divc_(vv[k] - d.prev_vel[k], fdt), Real(9.8)) + Real(1);
         d.prev_vel[k] = vv[k];
     }
     float gyro[3];
@@ -842,9 +842,9 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const Real x = F32 ? clampr_(m4[k], Real(0), Real(65535)) * Real(60.0 / 65535)
-                               : clampr_(m4[k], Real(0), Real(65535)) / Real(65535) * Real(60);
+                               : divc_(clampr_(m4[k], Real(0), Real(65535)), Real(65535)) * Real(60);
             const Real volts = Real(-0.0006239) * x * x + Real(0.088) * x;
-            const Real pct = minr_(F32 ? volts * Real(1.0 / 3) : volts / Real(3), Real(1));
+            const Real pct = minr_(F32 ? volts * Real(1.0 / 3) : divc_(volts, Real(3)), Real(1));
             pwm[k] = pct * Real(65535);
         }
     }
@@ -859,7 +859,7 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
     for (int k = 0; k < 4; ++k) {
         const Real t = maxr_(th[3 - k] + noise[k], Real(0));
         Real mp = F32 ? (hsqrt_(t * Real(1.0 / 3.16e-10)) - Real(4070.3)) * Real(1.0 / 0.2685)
-                      : (sqrt_(t / Real(1) / Real(3.16e-10)) - Real(4070.3)) / Real(0.2685);
+                      : divc_(sqrt_(divc_(t, Real(3.16e-10))) - Real(4070.3), Real(0.2685));
         mp = clampr_(mp, Real(20000), Real(65535));
         d.prev[k] = d.rpm[k];
         d.rpm[k] = Real(0.2685) * mp + Real(4070.3);
@@ -1149,7 +1149,7 @@ __device__ __forceinline__ void track_bounds(const RaceConst<Real>& C, const TS&
         if (g < C.num_gates) {
             const V3<Real> dp = p - v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
             Real sn, cs;
-            sincos_(T(RF_GATE + 4 * g + 3), &sn, &cs);
+            sincos_f_(T(RF_GATE + 4 * g + 3), &sn, &cs);
             const V3<Real> lg = v3(cs * dp.x + sn * dp.y, -sn * dp.x + cs * dp.y, dp.z);   // Rz(yaw)^T dp
             const V3<Real> ag = v3(cs * ax.x + sn * ax.y, -sn * ax.x + cs * ax.y, ax.z);
             const int low = C.gate_type[g] > 0;
@@ -1815,7 +1815,7 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
         const Real rotg = T(RF_GATE + 4 * gate0 + 3);
         const Real h = C.gate_type[gate0] == 0 ? Real(1.0) : Real(0.525), half = Real(0.1875);
         Real sn, cs;
-        sincos_(rotg, &sn, &cs);
+        sincos_f_(rotg, &sn, &cs);
         const Real dx = Real(0.05) * cs, dy = Real(0.05) * sn;
         // the 7 rays span the rectangle {g + t u + z e_z : |t| <= 0.15, |z - h| <= half};
         // drones whose bounding sphere (about pos: |z offset| + cylinder radius) misses it

@@ -102,17 +102,18 @@ __device__ __forceinline__ Real euler_axis_q4(Q4<Real> q, int a) {
 // MellingerControl.computeControl (154-262) for the quad: lane ql owns axis min(ql, 2) of the
 // rates / gyro filter (rpy_a, prv, l1, l2) and motor ql of the PWM chain (noise_m).  Same
 // arithmetic as mellinger_compute<Real> (FP contraction off; fp32: reciprocal multiplies, fp64:
-// numpy's divisions and the firmware's C float divisions), split across the quad.
+// numpy's correctly rounded divisions (by constants: divc_) and the firmware's C float divisions),
+// split across the quad.
 template <typename Real>
 __device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, const float sp[3], float xc_x,
                                              float xc_y, Real rpy_a, Real& prv, float& l1, float& l2, Real noise_m,
                                              int ql, const M3<Real>& Rq) {
 #pragma clang fp contract(off)
     constexpr bool F32 = sizeof(Real) == 4;
-    const Real rate = F32 ? (rpy_a - prv) * Real(500) : (rpy_a - prv) / Real(0.002);
+    const Real rate = F32 ? (rpy_a - prv) * Real(500) : divc_(rpy_a - prv, Real(0.002));
     prv = rpy_a;
     const Real acc_z = F32 ? (d.vel.z - d.prev_vel[2]) * Real(500.0 / 9.8) + Real(1)
-                           : (d.vel.z - d.prev_vel[2]) / Real(0.002) / Real(9.8) + Real(1);
+                           : divc_(divc_(d.vel.z - d.prev_vel[2], Real(0.002)), Real(9.8)) + Real(1);
     d.prev_vel[0] = d.vel.x; d.prev_vel[1] = d.vel.y; d.prev_vel[2] = d.vel.z;
     const float g_a = lpf_apply(lpf, l1, l2, float(rate * Real(57.29577951308232)));
     const float gyro[3] = {qbc(g_a, 0), qbc(g_a, 1), qbc(g_a, 2)};
@@ -156,16 +157,16 @@ __device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, co
         const Real r = Real(d.ctl[0]) / Real(2), p = Real(d.ctl[1]) / Real(2), y = Real(d.ctl[2]), th = Real(d.ctl[3]);
         const Real m = ((th + (ql < 2 ? -r : r)) + ((ql == 0 || ql == 3) ? p : -p)) + ((ql & 1) ? -y : y);
         const Real x = F32 ? clampr_(m, Real(0), Real(65535)) * Real(60.0 / 65535)
-                           : clampr_(m, Real(0), Real(65535)) / Real(65535) * Real(60);
+                           : divc_(clampr_(m, Real(0), Real(65535)), Real(65535)) * Real(60);
         const Real volts = Real(-0.0006239) * x * x + Real(0.088) * x;
-        pwm = minr_(F32 ? volts * Real(1.0 / 3) : volts / Real(3), Real(1)) * Real(65535);
+        pwm = minr_(F32 ? volts * Real(1.0 / 3) : divc_(volts, Real(3)), Real(1)) * Real(65535);
     }
     // clip -> thrust -> reorder [3,2,1,0] -> + noise -> _thr2pwm -> rpm (246-262)
     const Real rp = Real(0.2685) * clampr_(pwm, Real(20000), Real(65535)) + Real(4070.3);
     const Real thr = qmirror(Real(3.16e-10) * rp * rp);
     const Real t = maxr_(thr + noise_m, Real(0));
     const Real mp = clampr_(F32 ? (hsqrt_(t * Real(1.0 / 3.16e-10)) - Real(4070.3)) * Real(1.0 / 0.2685)
-                                : (sqrt_(t / Real(1) / Real(3.16e-10)) - Real(4070.3)) / Real(0.2685),
+                                : divc_(sqrt_(divc_(t, Real(3.16e-10))) - Real(4070.3), Real(0.2685)),
                             Real(20000), Real(65535));
     const Real rnew = Real(0.2685) * mp + Real(4070.3);
 #pragma unroll
@@ -206,7 +207,7 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<Real>& C, const 
     if (g < C.num_gates) {
         const V3<Real> dp = p - v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
         Real sn, cs;
-        sincos_(T(RF_GATE + 4 * g + 3), &sn, &cs);
+        sincos_f_(T(RF_GATE + 4 * g + 3), &sn, &cs);
         const V3<Real> lg = v3(cs * dp.x + sn * dp.y, -sn * dp.x + cs * dp.y, dp.z);
         const V3<Real> ag = v3(cs * ax.x + sn * ax.y, -sn * ax.x + cs * ax.y, ax.z);
         const int low = C.gate_type[g] > 0;
@@ -600,12 +601,12 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     const int tick0 = a.ist[RI_TICK * EN + slot];
     uint32_t att0, pos0;
     tick_window(a.ticks, tick0, att0, pos0);
-    // the env's actual track: 7 of its 28 fields per lane, into LDS after the loop
-    Real trk[(kTrackFields + 3) / 4];
+    // the env's actual track: 7 of its 28 fields per lane, into LDS for the post-loop queries (written
+    // before the loop, so no register holds them through the sub-steps)
 #pragma unroll
     for (int i = 0; i < (kTrackFields + 3) / 4; ++i) {
         const int k = ql + 4 * i;
-        trk[i] = k < kTrackFields ? ld(a.f, RF_GATE + k, EN, slot) : Real(0);
+        if (k < kTrackFields) trk_lds[k * kQuadDrones + qd] = ld(a.f, RF_GATE + k, EN, slot);
     }
     RDrone<Real> d;
     load_drone<Real, false>(a, EN, slot, d);
@@ -751,11 +752,6 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     if constexpr (kEarlyStore) {
         if (owner) store_drone_body(a, EN, slot, d);
     }
-#pragma unroll
-    for (int i = 0; i < (kTrackFields + 3) / 4; ++i) {
-        const int k = ql + 4 * i;
-        if (k < kTrackFields) trk_lds[k * kQuadDrones + qd] = trk[i];
-    }
     __syncthreads();
     const TrackSrcQ<Real> T{trk_lds, qd};
     // ---- _gate_progress (471-506) ----
@@ -772,7 +768,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         const Real rotg = T(RF_GATE + 4 * gate0 + 3);
         const Real h = C.gate_type[gate0] == 0 ? Real(1.0) : Real(0.525), half = Real(0.1875);
         Real sn, cs;
-        sincos_(rotg, &sn, &cs);
+        sincos_f_(rotg, &sn, &cs);
         const Real dx = Real(0.05) * cs, dy = Real(0.05) * sn;
         const Real br = fabs_(C.coll_zoff) + hsqrt_(C.coll_r * C.coll_r + C.coll_hh * C.coll_hh) + Real(1e-5);
         uint32_t near = 0;

@@ -27,17 +27,22 @@ MODES = {"raw": abi.POLICY_RAW, "relative": abi.POLICY_RELATIVE, "absolute": abi
 ACTOR_KEYS = ("mlp_extractor.policy_net.0.weight", "mlp_extractor.policy_net.0.bias",
               "mlp_extractor.policy_net.2.weight", "mlp_extractor.policy_net.2.bias",
               "action_net.weight", "action_net.bias")
+CRITIC_KEYS = ("mlp_extractor.value_net.0.weight", "mlp_extractor.value_net.0.bias",
+               "mlp_extractor.value_net.2.weight", "mlp_extractor.value_net.2.bias",
+               "value_net.weight", "value_net.bias", "log_std")
 
 
-def load_sb3_zip(path):
-    """-> (actor weights {name: float32 ndarray}, activation "tanh" | "relu")"""
+def load_sb3_zip(path, critic=False):
+    """-> (actor weights {name: float32 ndarray}, activation "tanh" | "relu"); critic=True: the
+    weights dict also holds CRITIC_KEYS (value MLP, value_net, log_std) for rollout collection"""
     with zipfile.ZipFile(path) as zf:
         sd = torch.load(io.BytesIO(zf.read("policy.pth")), map_location="cpu", weights_only=True)
         data = json.loads(zf.read("data"))
     kw = data.get("policy_kwargs") or {}
     act = str(kw.get("activation_fn", "Tanh"))
     activation = "relu" if "ReLU" in act else "tanh"       # SB3 MlpPolicy default: nn.Tanh
-    return {k: sd[k].float().numpy() for k in ACTOR_KEYS}, activation
+    keys = ACTOR_KEYS + (CRITIC_KEYS if critic else ())
+    return {k: sd[k].float().numpy() for k in keys}, activation
 
 
 class DevicePolicy:
@@ -53,8 +58,11 @@ class DevicePolicy:
             raise _lib.AdrpError("no HIP device visible: libadrp has no CPU fallback")
         w = [np.ascontiguousarray(weights[k], np.float32) for k in ACTOR_KEYS]
         (w1, b1, w2, b2, w3, b3) = w
-        if w3.shape[0] != 4:
-            raise ValueError("the action_net must have 4 outputs (x, y, z, yaw)")
+        if not 1 <= w3.shape[0] <= 4:
+            raise ValueError("the action_net must have 1..4 outputs")
+        self.act_dim = w3.shape[0]
+        if self.act_dim != 4 and mode != "raw":
+            raise ValueError("RLController transforms need the 4 outputs (x, y, z, yaw)")
         self.in_dim, self.h1, self.h2 = w1.shape[1], w1.shape[0], w2.shape[0]
         self.mode = MODES[mode]
         self.device = torch.device("cuda", device)
@@ -62,16 +70,56 @@ class DevicePolicy:
         h = ctypes.c_void_p()
         act = abi.POLICY_RELU if activation == "relu" else abi.POLICY_TANH
         ptr = [a.ctypes.data_as(ctypes.c_void_p) for a in w]
-        rc = self.lib.adrp_policy_create(device, self.in_dim, self.h1, self.h2, act, *ptr, ctypes.byref(h))
+        rc = self.lib.adrp_policy_create2(device, self.in_dim, self.h1, self.h2, self.act_dim, act, *ptr, ctypes.byref(h))
         if rc != 0:
             msg = self.lib.adrp_last_error(None).decode()
             raise (ValueError if rc == abi.ERR_INVALID else _lib.AdrpError)(f"adrp_policy_create: {msg}")
         self.h = h
+        self.has_critic = False
+        if all(k in weights for k in CRITIC_KEYS):
+            self.set_critic(weights)
 
     @classmethod
-    def from_zip(cls, path, device=0, mode="relative"):
-        w, activation = load_sb3_zip(path)
+    def from_zip(cls, path, device=0, mode="relative", critic=False):
+        w, activation = load_sb3_zip(path, critic=critic)
         return cls(w, activation, device, mode)
+
+    def set_critic(self, weights):
+        """attach the critic (CRITIC_KEYS: value MLP of the same shape, value_net, log_std) for
+        ``sample`` (PPO rollout collection)"""
+        v = [np.ascontiguousarray(weights[k], np.float32) for k in CRITIC_KEYS]
+        if v[0].shape != (self.h1, self.in_dim) or v[2].shape != (self.h2, self.h1) or v[4].shape != (1, self.h2) \
+                or v[6].shape != (self.act_dim,):
+            raise ValueError("critic shapes must mirror the actor (value MLP in -> h1 -> h2 -> 1, log_std [act_dim])")
+        ptr = [a.ctypes.data_as(ctypes.c_void_p) for a in v]
+        rc = self.lib.adrp_policy_set_critic(self.h, *ptr)
+        if rc != 0:
+            raise _lib.AdrpError(f"adrp_policy_set_critic: {self.lib.adrp_last_error(None).decode()}")
+        self.has_critic = True
+
+    def sample(self, obs, seed, counter, env_act=None, action=None, value=None, log_prob=None, eps=None):
+        """PPO rollout step (include/adrp.h adrp_policy_sample; SB3 ActorCriticPolicy.forward with
+        deterministic=False) on the rows of obs [..., D]: returns (env_act, action, value, log_prob),
+        device tensors, written into the given ones if passed.  ``counter`` (e.g. the rollout step)
+        and ``seed`` key the Philox draws of the Gaussian sample."""
+        rows = obs.numel() // obs.shape[-1]
+        if not (obs.is_cuda and obs.dtype == torch.float32 and obs.is_contiguous()):
+            raise ValueError("obs must be a contiguous float32 device tensor")
+        dev = obs.device
+        ea = 4 if self.mode != MODES["raw"] else self.act_dim
+        env_act = torch.empty((rows, ea), dtype=torch.float32, device=dev) if env_act is None else env_act
+        action = torch.empty((rows, self.act_dim), dtype=torch.float32, device=dev) if action is None else action
+        value = torch.empty(rows, dtype=torch.float32, device=dev) if value is None else value
+        log_prob = torch.empty(rows, dtype=torch.float32, device=dev) if log_prob is None else log_prob
+        for t, n in ((env_act, rows * ea), (action, rows * self.act_dim), (value, rows), (log_prob, rows)):
+            assert t.is_contiguous() and t.dtype == torch.float32 and t.numel() == n
+        rc = self.lib.adrp_policy_sample(self.h, obs.data_ptr(), rows, obs.shape[-1], self.mode,
+                                         int(seed) & (2 ** 64 - 1), int(counter) & 0xFFFFFFFF, env_act.data_ptr(),
+                                         action.data_ptr(), value.data_ptr(), log_prob.data_ptr(),
+                                         None if eps is None else eps.data_ptr(), _lib._raw_stream(dev.index))
+        if rc != 0:
+            raise _lib.AdrpError(f"adrp_policy_sample: {self.lib.adrp_last_error(None).decode()}")
+        return env_act, action, value, log_prob
 
     def act(self, obs, out=None):
         """obs [..., D] float32 on the device (D >= in_dim; the first in_dim columns are the
@@ -83,7 +131,7 @@ class DevicePolicy:
             out = torch.empty(obs.shape[:-1] + (4,), dtype=torch.float32, device=obs.device)
         assert out.is_contiguous() and out.numel() == rows * 4
         rc = self.lib.adrp_policy_act(self.h, obs.data_ptr(), rows, obs.shape[-1], self.mode, out.data_ptr(),
-                                      torch.cuda.current_stream(obs.device).cuda_stream)
+                                      _lib._raw_stream(obs.device.index))
         if rc != 0:
             raise _lib.AdrpError(f"adrp_policy_act: {self.lib.adrp_last_error(None).decode()}")
         return out

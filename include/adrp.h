@@ -303,6 +303,39 @@ int adrp_policy_create(int device, int in_dim, int hidden1, int hidden2, int act
 int adrp_policy_act(adrp_policy_t* p, const float* obs_dev, int rows, int obs_stride, int mode,
                     float* act_dev, void* stream);
 void adrp_policy_destroy(adrp_policy_t* p);
+/* act_dim 1..4 (HoverAviary ONE_D_RPM policies: 1); adrp_policy_act needs 4, adrp_policy_sample any */
+int adrp_policy_create2(int device, int in_dim, int hidden1, int hidden2, int act_dim, int activation,
+                        const float* w1, const float* b1, const float* w2, const float* b2,
+                        const float* w3, const float* b3, adrp_policy_t** out);
+
+/* ---------------------------------------------------------------------------------------
+ * On-device PPO rollout step (examples/learn.py:72-94 trains PPO): what SB3's
+ * OnPolicyAlgorithm.collect_rollouts does per step, `actions, values, log_probs = policy(obs)`
+ * with ActorCriticPolicy.forward(obs, deterministic=False) (stable_baselines3 2.3.2): the actor
+ * mean (as adrp_policy_act), the critic mlp_extractor.value_net (in_dim -> hidden1 -> hidden2, the
+ * same activation) + value_net (-> 1), a DiagGaussianDistribution sample a = mean +
+ * exp(log_std) eps and log_prob = sum_i Normal(mean_i, std_i).log_prob(a_i).  eps ~ N(0, 1): one
+ * Philox4x32-10 block per row, counter {row, counter, 0x504f4c00, 0} keyed by seed, Box-Muller of
+ * its word pairs (the race action noise's IEEE float form).  Replaces, batched on the device,
+ * policy(obs_tensor) inside collect_rollouts plus the np.clip of the actions it sends the env.
+ * adrp_policy_set_critic: value_net.{0,2}.* / value_net.* in torch layout and log_std [act_dim].
+ * adrp_policy_sample: action_dev [rows][act_dim] (the sample, what the rollout buffer stores),
+ * env_act_dev (clip to [-1, 1], then the mode transform; [rows][act_dim], RELATIVE / ABSOLUTE
+ * [rows][4]), value_dev [rows], logprob_dev [rows], eps_dev [rows][act_dim] or NULL.
+ * --------------------------------------------------------------------------------------- */
+int adrp_policy_set_critic(adrp_policy_t* p, const float* vw1, const float* vb1, const float* vw2,
+                           const float* vb2, const float* vw3, const float* vb3, const float* log_std);
+int adrp_policy_sample(adrp_policy_t* p, const float* obs_dev, int rows, int obs_stride, int mode,
+                       uint64_t seed, uint32_t counter, float* env_act_dev, float* action_dev,
+                       float* value_dev, float* logprob_dev, float* eps_dev, void* stream);
+
+/* GAE over a rollout (SB3 RolloutBuffer.compute_returns_and_advantage, stable_baselines3 2.3.2):
+ * rewards / values / episode_starts [n_steps][n_envs] float32 on the device, last_values /
+ * dones [n_envs]; writes advantages and returns [n_steps][n_envs] (returns = advantages + values).
+ * One lane per env runs the backward recursion. */
+int adrp_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
+             const float* dones, int n_steps, int n_envs, double gamma, double gae_lambda, float* advantages,
+             float* returns, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Parity mode noise (MultiRaceAviary).  The reference draws, per sub-step, the disturbance force
@@ -321,7 +354,8 @@ int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_d
  * Numerics probe (no reference counterpart: test support).  Evaluates one of the fp64
  * fast transcendentals the fp64 step kernels inline (csrc/adrp_device.h namespace f64:
  * refined v_rcp_f64 / v_rsq_f64, range-reduced polynomials) on n device doubles:
- * out[i] = f(in[i]); ATAN2 reads y = in[i], x = in[n + i].  Stream-ordered.
+ * out[i] = f(in[i]); ATAN2 reads y = in[i], x = in[n + i], DIVC x = in[i], c = in[n + i].
+ * Stream-ordered.
  * --------------------------------------------------------------------------------------- */
 #define ADRP_MATH_RCP 0
 #define ADRP_MATH_RSQ 1
@@ -341,6 +375,9 @@ int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_d
 #define ADRP_MATH_QUAT_INV_NORM 15 /* 1/sqrt(n2) of the hover exp-map quaternion (per-lane form) */
 #define ADRP_MATH_NORMAL_Z0 16     /* race action-noise Box-Muller of a Philox word pair: in[i]'s bits */
 #define ADRP_MATH_NORMAL_Z1 17     /*   = x1 << 32 | x0; out = z0 / z1 (float samples, as doubles) */
+#define ADRP_MATH_DIVC 18          /* in[i] / in[n + i] by the fp64 kernels' constant-divisor form */
+#define ADRP_MATH_SIN_FAST 19      /* octant-reduced sin / cos (gate yaws, reset attitudes) */
+#define ADRP_MATH_COS_FAST 20
 int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream);
 
 #ifdef __cplusplus

@@ -847,6 +847,29 @@ def policy_fixtures(pb, m):
     return out
 
 
+def critic_fixtures():
+    """On-device PPO rollout: the critic (mlp_extractor.value_net, value_net) and
+    the Gaussian log_std of the reference's two SB3 zips (user_controller/*.zip; policy.pth read with
+    torch.load(weights_only=True), the `data` member as JSON: nothing unpickled), and the PPO
+    hyper-parameters the zips were trained with (gamma, gae_lambda, n_steps)."""
+    import io
+    import json
+    import zipfile
+    import torch
+    out = {}
+    keys = ("mlp_extractor.value_net.0.weight", "mlp_extractor.value_net.0.bias",
+            "mlp_extractor.value_net.2.weight", "mlp_extractor.value_net.2.bias",
+            "value_net.weight", "value_net.bias", "log_std")
+    for name in ("example_RL_model", "twogates"):
+        with zipfile.ZipFile(os.path.join(REF, "user_controller", name + ".zip")) as zf:
+            sd = torch.load(io.BytesIO(zf.read("policy.pth")), map_location="cpu", weights_only=True)
+            data = json.loads(zf.read("data"))
+        for i, k in enumerate(keys):
+            out[f"{name}_v{i}"] = sd[k].float().numpy()
+        out[f"{name}_hp"] = np.array([float(data["gamma"]), float(data["gae_lambda"]), float(data["n_steps"])])
+    return out
+
+
 def hardcoded_fixtures(pb, m):
     """HardCodedController (user_controller/HardCodedController.py:14-190) as scripts/sim.py:68-106
     drives it: config/getting_started.yaml, 2 drones, COMPARE, info["delay"] = drone_id, one
@@ -912,6 +935,12 @@ def logger_fixtures(pb, m):
 
 
 def main():
+    if os.environ.get("GOLDEN_ONLY") == "critic":   # weights only: no reference module is imported
+        px = critic_fixtures()
+        path = os.path.join(HERE, "critic_golden.npz")
+        np.savez_compressed(path, **px)
+        print("wrote", path, len(px), "arrays")
+        return
     os.chdir(REF)   # MultiRaceAviary resolves URDF_DIR relative to the cwd (read only)
     pb = install_stubs()
     m = import_reference(pb)
@@ -975,6 +1004,10 @@ def main():
     print("wrote", path, len(px), "arrays")
     px = hardcoded_fixtures(pb, m)
     path = os.path.join(HERE, "hardcoded_golden.npz")
+    np.savez_compressed(path, **px)
+    print("wrote", path, len(px), "arrays")
+    px = critic_fixtures()
+    path = os.path.join(HERE, "critic_golden.npz")
     np.savez_compressed(path, **px)
     print("wrote", path, len(px), "arrays")
 

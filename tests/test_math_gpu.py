@@ -160,3 +160,31 @@ def test_race_noise_box_muller_matches_oracle():
     r = np.sqrt(-2 * np.log(u1))
     assert (np.abs(z0 - r * np.cos(2 * np.pi * u2)) <= 2.5e-7 * np.maximum(r, 1e-30) + 1e-30).all()
     assert (np.abs(z1 - r * np.sin(2 * np.pi * u2)) <= 2.5e-7 * np.maximum(r, 1e-30) + 1e-30).all()
+
+
+@pytest.mark.parametrize("c", [0.002, 9.8, 65535.0, 3.0, 3.16e-10, 0.2685])
+def test_constant_divisor_division_is_ieee(c):
+    """f64::div_c (the fp64 kernels' x / c for the wrapper's constant divisors: numpy's rates / 0.002,
+    acc / 0.002 / 9.8, _compute_pwms / 65535 / 3, _thr2pwm / 3.16e-10 / 0.2685) equals the IEEE
+    quotient bit for bit, signed zeros included, over 10^6 random x across 2^-60 .. 2^60"""
+    rng = np.random.default_rng(int(c * 1000) % 2 ** 31)
+    x = np.ldexp(1 + rng.random(1_000_000), rng.integers(-60, 61, 1_000_000)) * rng.choice([-1.0, 1.0], 1_000_000)
+    x = np.concatenate([x, [0.0, -0.0, 1.0, -1.0, c, 3 * c]])
+    got = probe(abi.MATH_DIVC, x, np.full_like(x, c))
+    want = x / c
+    np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_sincos_fast():
+    """f64::sincos_fast (gate / part yaws and reset attitudes of the fp64 race kernels): within 2 ulp
+    of the correctly rounded sin / cos on |x| <= 100 (relative; absolute 2^-52 near zero crossings),
+    octant boundaries and signed zeros included"""
+    rng = np.random.default_rng(19)
+    x = np.concatenate([rng.uniform(-100, 100, 400000), rng.uniform(-4, 4, 200000),
+                        np.arange(-40, 41) * np.pi / 8, [0.0, -0.0, 1e-300, np.pi, -np.pi, 0.5 * np.pi]])
+    s, c = probe(abi.MATH_SIN_FAST, x), probe(abi.MATH_COS_FAST, x)
+    xl = x.astype(L)
+    for got, ref in ((s, np.sin(xl)), (c, np.cos(xl))):
+        err = np.abs(got.astype(L) - ref)
+        assert (err <= np.maximum(np.abs(ref) * L(2.0 ** -51), L(2.0 ** -52))).all(), float(err.max())
+    assert s[-6] == 0.0 and c[-6] == 1.0

@@ -168,6 +168,9 @@ def check_closed_loop(env, orc, precision, stats=None, floors=None):
             stats["over"] = stats.get("over", 0) + int(over.sum())
             stats["near"] = stats.get("near", 0) + int((margin < ATTR_TAU).sum())
             stats["max_unattributed"] = max(stats.get("max_unattributed", 0.0), float(err[~(margin < ATTR_TAU)].max(initial=0)))
+            stats["over_margin_max"] = max(stats.get("over_margin_max", 0.0), float(margin[over].max(initial=0)))
+            for t in (1e-3, 1e-4):
+                stats[f"margin<{t:g}"] = stats.get(f"margin<{t:g}", 0) + int((margin < t).sum())
     return worst
 
 
@@ -604,6 +607,8 @@ def test_full_size_subset_vs_oracle(E, N, level, physics, mode, precision):
                 bad = (err > FP64_BAR) & flags_same & ~(margin < ATTR_TAU)
                 assert not bad.any(), (f"env {e} {g}: {err.max():.3e} over {FP64_BAR:g}, moment margins {margin}")
                 over += int(((err > FP64_BAR) & flags_same).sum())
+                if ((err > FP64_BAR) & flags_same).any():
+                    print(f"env {e} {g}: over-bar margins {margin[(err > FP64_BAR) & flags_same]}")
         near += int((margin < ATTR_TAU).sum())
         for k in ("step_counter", "episode", "gate", "tick", "last_att_tick", "last_pos_tick"):
             np.testing.assert_array_equal(ig[inames.index(k), sl], io[inames.index(k)], err_msg=f"env {e} {k}")
