@@ -179,6 +179,18 @@ class Handle:
     def reset(self, obs, mask=None):
         self._check(self.lib.adrp_reset(self.h, _p(mask), _p(obs), self._stream()), "adrp_reset")
 
+    def bind(self, obs, rew, term, trunc, tobs=None):
+        """cache the device addresses of an env's persistent output buffers for step_ptr"""
+        self._outs = (obs.data_ptr(), rew.data_ptr(), term.data_ptr(), trunc.data_ptr(),
+                      None if tobs is None else tobs.data_ptr())
+
+    def step_ptr(self, act_ptr):
+        """adrp_step on the buffers of the last bind() (the hot call of a Python-driven loop: one
+        ctypes call, no tensor introspection)"""
+        rc = self._step(self.h, act_ptr, *self._outs, _raw_stream(self._dev_index))
+        if rc != 0:
+            self._check(rc, "adrp_step")
+
     def step(self, act, obs, rew, term, trunc, tobs=None):
         """act None: command mode, the setpoints the last command() left"""
         rc = self._step(self.h, None if act is None else act.data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),

@@ -179,6 +179,7 @@ static int upload_const(adrp_t* h) {
         hipMemcpy((char*)h->cblk + sizeof k, &r, sizeof r, hipMemcpyHostToDevice) != hipSuccess)
         return ADRP_ERR_DEVICE;
     h->cf2x = is_cf2x<Real>(h->cfg);
+    if (const char* env = getenv("ADRP_HOVER_GENERIC")) h->cf2x = h->cf2x && atoi(env) == 0;   // A/B: runtime constants
     return ADRP_OK;
 }
 
@@ -332,7 +333,13 @@ extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
 extern "C" const char* adrp_handle_kernel_name(const adrp_t* h) {
     static thread_local char buf[96];
     if (!h) return nullptr;
-    if (h->cfg.task != ADRP_TASK_RACE) return adrp_kernel_name(&h->cfg);
+    if (h->cfg.task != ADRP_TASK_RACE) {
+        const char* n = adrp_kernel_name(&h->cfg);
+        const char* c = strstr(n, ",cf2x>");
+        if (!c || h->cf2x) return n;
+        snprintf(buf, sizeof buf, "%.*s,generic>", int(c - n), n);   // ADRP_HOVER_GENERIC
+        return buf;
+    }
     static const char* ph[] = {"PYB", "DYN", "PYB_GND", "PYB_DRAG", "PYB_DW", "PYB_GND_DRAG_DW"};
     const int p = h->cfg.physics >= 0 && h->cfg.physics <= 5 ? h->cfg.physics : 0;
     const char* prec = h->real_size == 8 ? "f64" : "f32";

@@ -447,6 +447,76 @@ __device__ __forceinline__ double fasin_(double s) { return f64::asin(s); }
 __device__ __forceinline__ float fexp_(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ double fexp_(double x) { return f64::exp(x); }
 
+// ---- literal constants of the fp64 sub-step chains, held in VGPRs ----------------------------
+// gfx950 has no 64-bit literal operand: an fp64 constant costs two s_mov / v_mov at every use the
+// compiler rematerialises it for (about a sixth of the hover fp64 sub-step's instructions).  The
+// chains take their constants from a ChainK that the kernel pins into VGPRs once, before the
+// sub-step loop (an empty asm that "modifies" the value: it cannot be re-derived as a literal).
+template <typename Real>
+struct ChainK {
+    Real k004, c100, nn_min, near1, tiny;   // 0.04, 100, 1e-300, 1e-9, 0.03
+    Real ts[3], tc[4];                      // the exp map's short series (f64::sincos_tiny's terms)
+};
+template <typename Real>
+__device__ __forceinline__ ChainK<Real> chain_consts() {
+    return ChainK<Real>{Real(0.04), Real(100), Real(1e-300), Real(1e-9), Real(0.03),
+                        {Real(-0.0001984126984126984), Real(0.008333333333333333), Real(-0.16666666666666666)},
+                        {Real(2.48015873015873e-05), Real(-0.001388888888888889), Real(0.041666666666666664), Real(-0.5)}};
+}
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(float&) {}
+template <typename Real>
+__device__ __forceinline__ void pin_all(ChainK<Real>& k) {
+    pin(k.k004); pin(k.c100); pin(k.nn_min); pin(k.near1); pin(k.tiny);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) pin(k.ts[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pin(k.tc[i]);
+}
+// the pinned-constant forms of sqrt_nn / expmap_sinc_cos / quat_inv_norm (same arithmetic)
+__device__ __forceinline__ float hsqrt_nn_(float x, const ChainK<float>&) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ double hsqrt_nn_(double x, const ChainK<double>& k) {
+    const double y = __builtin_amdgcn_rsq(__builtin_fmax(x, k.nn_min));
+    double g = x * y, h = 0.5 * y;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double r = f64::fma_(-g, h, 0.5);
+        g = f64::fma_(g, r, g);
+        h = f64::fma_(h, r, h);
+    }
+    const double d = f64::fma_(-g, g, x);
+    return f64::fma_(d, h, g);
+}
+__device__ __forceinline__ void expmap_sinc_cos(float x, float* sinc, float* c, const ChainK<float>&) {
+    expmap_sinc_cos(x, sinc, c);
+}
+__device__ __forceinline__ void expmap_sinc_cos(double x, double* sinc, double* c, const ChainK<double>& k) {
+    const double x2 = x * x;
+    const bool tiny = __builtin_fabs(x) <= k.tiny;
+    double ps = f64::fma_(k.ts[0], x2, k.ts[1]);
+    ps = f64::fma_(ps, x2, k.ts[2]);
+    double pc = f64::fma_(k.tc[0], x2, k.tc[1]);
+    pc = f64::fma_(pc, x2, k.tc[2]);
+    pc = f64::fma_(pc, x2, k.tc[3]);
+    if (__builtin_expect(!__all(tiny), 0)) {   // the full series (cold: literal coefficients)
+        double fs, fc;
+        expmap_sinc_cos_full(x, &fs, &fc);
+        *sinc = tiny ? f64::fma_(x2, ps, 1.0) : fs;
+        *c = tiny ? f64::fma_(x2, pc, 1.0) : fc;
+        return;
+    }
+    *sinc = f64::fma_(x2, ps, 1.0);
+    *c = f64::fma_(x2, pc, 1.0);
+}
+__device__ __forceinline__ float quat_inv_norm(float n2, const ChainK<float>&) { return quat_inv_norm(n2); }
+__device__ __forceinline__ double quat_inv_norm(double n2, const ChainK<double>& k) {
+    const bool near1 = __builtin_fabs(n2 - 1.0) <= k.near1;
+    const double newton = f64::fma_(0.5, 1.0 - n2, 1.0);
+    if (__builtin_expect(__all(near1), 1)) return newton;
+    const double r = f64::rsq_nc(n2);
+    return near1 ? newton : r;
+}
+
 // btClamp(x, -100, 100) of the six coordinate velocities (btMultiBody m_maxCoordinateVelocity) after
 // the semi-implicit Euler update.  fp32: one v_med3 each.  fp64 has no med3, and the select form
 // (x < -100 ? -100 : x > 100 ? 100 : x) is 2 compares + 4 32-bit selects per component on every
@@ -462,6 +532,17 @@ __device__ __forceinline__ double clamp100_sel(double x) { return x < -100.0 ? -
 __device__ __forceinline__ void clamp100_wv(V3<double>& w, V3<double>& v) {
     const bool big = (__builtin_fabs(w.x) > 100.0) | (__builtin_fabs(w.y) > 100.0) | (__builtin_fabs(w.z) > 100.0) |
                      (__builtin_fabs(v.x) > 100.0) | (__builtin_fabs(v.y) > 100.0) | (__builtin_fabs(v.z) > 100.0);
+    if (__builtin_expect(__any(big), 0)) {
+        w = {clamp100_sel(w.x), clamp100_sel(w.y), clamp100_sel(w.z)};
+        v = {clamp100_sel(v.x), clamp100_sel(v.y), clamp100_sel(v.z)};
+    }
+}
+
+__device__ __forceinline__ void clamp100_wv(V3<float>& w, V3<float>& v, const ChainK<float>&) { clamp100_wv(w, v); }
+__device__ __forceinline__ void clamp100_wv(V3<double>& w, V3<double>& v, const ChainK<double>& k) {
+    const double c = k.c100;
+    const bool big = (__builtin_fabs(w.x) > c) | (__builtin_fabs(w.y) > c) | (__builtin_fabs(w.z) > c) |
+                     (__builtin_fabs(v.x) > c) | (__builtin_fabs(v.y) > c) | (__builtin_fabs(v.z) > c);
     if (__builtin_expect(__any(big), 0)) {
         w = {clamp100_sel(w.x), clamp100_sel(w.y), clamp100_sel(w.z)};
         v = {clamp100_sel(v.x), clamp100_sel(v.y), clamp100_sel(v.z)};

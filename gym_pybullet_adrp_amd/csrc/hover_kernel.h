@@ -141,9 +141,11 @@ __device__ __forceinline__ float rpm_gain(float a) {
 // next sub-step's |R^T w| of the damping term: a rotation keeps the norm, so the chain takes one
 // square root per sub-step, not two; rounding-level difference).  Returns true if the plane
 // contact model acted.
+// K: the chain's literal constants (pinned into VGPRs by the fp64 caller, ChainK)
 template <typename Real, int PH>
 __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real>& b, M3<Real>& R, M3<Real>& Rs,
-                                            const Real rpm[4], Real sum_f, V3<Real> P, Real tau_z, Real& wn) {
+                                            const Real rpm[4], Real sum_f, V3<Real> P, Real tau_z, Real& wn,
+                                            const ChainK<Real>& K) {
     constexpr bool GND = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     // _physics: 4 prop forces + z torque on link 4, LINK_FRAME, cached basis
@@ -188,23 +190,23 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     // ---- Bullet: forwardKinematics, ABA of the floating base, semi-implicit Euler ----
     const V3<Real> wb = mulT(R, b.w);
     const V3<Real> Iw = v3(a.ixx * wb.x, a.iyy * wb.y, a.izz * wb.z);
-    const Real kw = Real(0.04) + Real(0.04) * wn;
+    const Real kw = K.k004 + K.k004 * wn;
     const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
     const V3<Real> wdot = mul(R, v3(rhs.x * a.inv_ixx, rhs.y * a.inv_iyy, rhs.z * a.inv_izz));
-    const Real kv = Real(0.04) + Real(0.04) * hsqrt_nn_(dot(b.vel, b.vel));
+    const Real kv = K.k004 + K.k004 * hsqrt_nn_(dot(b.vel, b.vel), K);
     const V3<Real> acc = a.inv_mass * Fw - kv * b.vel;
     b.w = v3(b.w.x + a.dt * wdot.x, b.w.y + a.dt * wdot.y, b.w.z + a.dt * wdot.z);
     b.vel = v3(b.vel.x + a.dt * acc.x, b.vel.y + a.dt * acc.y, b.vel.z + a.dt * acc.z);
-    clamp100_wv(b.w, b.vel);
+    clamp100_wv(b.w, b.vel, K);
     b.pos = b.pos + a.dt * b.vel;
     // exp-map quaternion update (btMultiBody::stepPositionsMultiDof)
-    Real ang = hsqrt_nn_(dot(b.w, b.w));
+    Real ang = hsqrt_nn_(dot(b.w, b.w), K);
     wn = ang;
     if (ang > a.ang_max) ang = a.ang_max;          // |w| dt > ANGULAR_MOTION_THRESHOLD
     // sin(|w| dt / 2) / |w| = (dt / 2) sinc(|w| dt / 2): no reciprocal, and Bullet's small-angle
     // form (|w| < 0.001: 0.5 dt - dt^3 |w|^2 / 48) is the same series to rounding
     Real sinc, ch;
-    expmap_sinc_cos(Real(0.5) * ang * a.dt, &sinc, &ch);
+    expmap_sinc_cos(Real(0.5) * ang * a.dt, &sinc, &ch, K);
     const Real sc = (Real(0.5) * a.dt) * sinc;
     const V3<Real> ax = sc * b.w;
     const Q4<Real> q0 = b.q;
@@ -212,7 +214,7 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
                          ch * q0.y + ax.y * q0.w + ax.z * q0.x - ax.x * q0.z,
                          ch * q0.z + ax.z * q0.w + ax.x * q0.y - ax.y * q0.x,
                          ch * q0.w - ax.x * q0.x - ax.y * q0.y - ax.z * q0.z};
-    const Real inv = quat_inv_norm(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w);
+    const Real inv = quat_inv_norm(q1.x * q1.x + q1.y * q1.y + q1.z * q1.z + q1.w * q1.w, K);
     // the basis cached by this step's forwardKinematics is the pre-integration pose
     if (a.link_lag) {
         b.ql = b.q;
@@ -682,9 +684,18 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         const Real tau_z = t2 * C.km;    // KM*(rpm0^2 - rpm1^2 + rpm2^2 - rpm3^2), IROS sign
         M3<Real> R = rot(b.q);
         M3<Real> Rs = lag ? rot(b.ql) : R;
-        Real wn = hsqrt_nn_(dot(b.w, b.w));
+        // the chain's constants in VGPRs for the whole loop (fp64: no 64-bit literal operands)
+        ChainK<Real> K = chain_consts<Real>();
+        HoverConst<Real> Cp = C;
+        if constexpr (sizeof(Real) == 8) {
+            pin_all(K);
+            pin(Cp.dt); pin(Cp.mass); pin(Cp.gravity); pin(Cp.inv_mass); pin(Cp.ang_max);
+            pin(Cp.ixx); pin(Cp.iyy); pin(Cp.izz); pin(Cp.inv_ixx); pin(Cp.inv_iyy); pin(Cp.inv_izz);
+            pin(Cp.coll_hh); pin(Cp.coll_r); pin(Cp.coll_zoff);
+        }
+        Real wn = hsqrt_nn_(dot(b.w, b.w), K);
         auto substep = [&]() {
-            touched |= pyb_substep<Real, PH>(C, b, R, Rs, rpm, sum_f, P, tau_z, wn);
+            touched |= pyb_substep<Real, PH>(Cp, b, R, Rs, rpm, sum_f, P, tau_z, wn, K);
 #pragma unroll
             for (int i = 0; i < 4; ++i) b.prev_rpm[i] = rpm[i];  // last_clipped_action
         };

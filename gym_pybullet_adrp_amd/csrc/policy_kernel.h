@@ -288,8 +288,9 @@ __global__ void __launch_bounds__(1024) policy_sample_kernel(PolicySampleArgs a)
         xb[s] = (live && k < L.in_dim) ? v : 0.0f;
     }
     policy_hidden<T1, T2, RELU>(blob, L, w, lane, xb, h1s[net], h2s[net]);
-    if (w != 0 || g != 0 || !live) return;          // lanes 0..15 of waves 0 / NW: row lane & 15
-    const f32x4 o = policy_out<T2>(blob, L, lane, h2s[net]);
+    if (w != 0) return;                              // waves 0 / NW finish (wave-uniform exit)
+    const f32x4 o = policy_out<T2>(blob, L, lane, h2s[net]);   // the MFMA needs all 64 lanes
+    if (g != 0 || !live) return;                     // lanes 0..15: the outputs of row lane & 15
     if (net == 1) {                                  // value_net: output 0
         a.value[r] = o[0] + blob[L.b3];
         return;

@@ -102,6 +102,8 @@ class HoverAviary(AviaryEnv):
         self._trunc = torch.zeros(E, dtype=torch.bool, device=self.device)
         self._act_shape = (E, 1, self.h.A)
         self._info = {"answer": 42, "terminal_observation": self._tobs}
+        self.h.bind(self._obs, self._rew, self._term, self._trunc, self._tobs)
+        self._act_ok = (None, 0)        # (tensor, address) of the last validated action
 
     # ---- spaces (BaseRLAviary.py:132-156, 243-277) ----
     def _actionSpace(self):
@@ -138,26 +140,39 @@ class HoverAviary(AviaryEnv):
 
         Returns views of persistent device buffers (obs [E,1,D], reward [E],
         terminated [E], truncated [E]) that the next step overwrites."""
+        ok, ptr = self._act_ok
+        if action is ok and action.data_ptr() == ptr:      # the tensor validated last time, unchanged
+            self.h.step_ptr(ptr)
+            return self._obs, self._rew, self._term, self._trunc, self._info
         act = action
         if not (isinstance(act, torch.Tensor) and act.dtype == torch.float32 and act.device == self.device
                 and act.is_contiguous() and act.shape == self._act_shape):
             act = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(self._act_shape)
             act = act.contiguous()
-        self.h.step(act, self._obs, self._rew, self._term, self._trunc, self._tobs)
+        else:
+            self._act_ok = (action, action.data_ptr())
+        self.h.step_ptr(act.data_ptr())
         return self._obs, self._rew, self._term, self._trunc, self._info
 
     def close(self):
         self.h.close()
 
-    def bind_outputs(self, obs, rew, term, trunc):
+    def bind_outputs(self, obs, rew, term, trunc, tobs=None):
         """Write step / reset outputs into caller-owned device tensors from now on (e.g. views of a
-        collective's send buffer, sharding.ShardedAviary(packed=True)): obs [E,N,D] float32, reward
-        [E] float32, terminated / truncated [E] bool, all contiguous on this env's device."""
+        collective's send buffer, sharding.ShardedAviary(packed=True), or the SB3 adapter's packed
+        host-copy buffer): obs [E,N,D] float32, reward [E] float32, terminated / truncated [E] bool,
+        optionally the terminal observations [E,N,D] float32, all contiguous on this env's device."""
         want = ((self._obs, obs), (self._rew, rew), (self._term, term), (self._trunc, trunc))
+        if tobs is not None:
+            want += ((self._tobs, tobs),)
         for old, new in want:
             if new.shape != old.shape or new.dtype != old.dtype or new.device != old.device or not new.is_contiguous():
                 raise ValueError(f"bind_outputs: need a contiguous {old.dtype} {tuple(old.shape)} tensor on {old.device}")
         self._obs, self._rew, self._term, self._trunc = obs, rew, term, trunc
+        if tobs is not None:
+            self._tobs = tobs
+            self._info["terminal_observation"] = tobs
+        self.h.bind(self._obs, self._rew, self._term, self._trunc, self._tobs)
 
     # ---- introspection (tests / teacher forcing) ----
     def get_state(self):

@@ -16,22 +16,56 @@ returns the device tensors untouched (for torch-native learners).  When
 stable_baselines3 is importable the class derives from its ``VecEnv`` so
 ``isinstance`` checks in SB3 pass; otherwise it is a plain class with the same methods.
 
-Host path (SURVEY.md §7 hard part 7).  The env writes obs / reward / terminated / truncated
-into ONE packed device buffer (``bind_outputs``); ``step_wait`` issues one asynchronous copy of
-it into pinned host memory and waits once; the actions go the other way through a pinned
-staging buffer (one asynchronous copy).  Terminal observations are fetched only for the envs
-that finished (a second small copy, only then).  ``infos`` is built lazily: the envs that
-finished get their own dict, every other entry is one shared read-only empty mapping (SB3
-reads infos and copies the dicts it annotates; writing into a shared entry raises).  Returned
+Host path (SURVEY.md §7 hard part 7).  The env writes obs / terminal obs / reward / terminated /
+truncated into ONE packed device buffer (``bind_outputs``); ``step_wait`` issues one asynchronous
+copy of it into pinned host memory and waits once; the actions go the other way through a pinned
+staging buffer (one asynchronous copy).  The terminal observations of the envs that finished are
+read from that same copy (a second, dependent round trip for them cost more than the bytes).
+``infos`` is a lazy sequence: a finished env's dict is made when the caller first reads it; every
+other entry is one shared read-only empty mapping (SB3 reads infos and copies the dicts it
+annotates; writing into a shared entry raises).  Returned
 arrays are fresh copies (DummyVecEnv semantics) unless ``zero_copy=True``: then they are views
 of a ring of ``ring`` pinned buffers, valid until ``ring`` more steps have been taken.
 """
 import types
+from collections.abc import Sequence
 
 import numpy as np
 import torch
 
 _NO_INFO = types.MappingProxyType({})
+
+
+class _StepInfos(Sequence):
+    """infos of one step, as SB3's VecEnv returns them (one mapping per env), built lazily: the envs
+    that finished get their own dict ({"terminal_observation", "TimeLimit.truncated"}) when first
+    read, then the same (mutable) dict on every read; every other entry is the shared read-only
+    empty mapping.  A step with hundreds of finished envs no longer builds hundreds of dicts that
+    the caller may never look at."""
+    __slots__ = ("_n", "_row", "_tobs", "_tl", "_made")
+
+    def __init__(self, n, idx, tobs, tl):
+        self._n = n
+        self._row = dict(zip(idx.tolist(), range(len(idx))))
+        self._tobs, self._tl, self._made = tobs, tl, {}
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, e):
+        if isinstance(e, slice):
+            return [self[i] for i in range(*e.indices(self._n))]
+        if e < 0:
+            e += self._n
+        if not 0 <= e < self._n:
+            raise IndexError(e)
+        j = self._row.get(e)
+        if j is None:
+            return _NO_INFO
+        d = self._made.get(e)
+        if d is None:
+            d = self._made[e] = {"terminal_observation": self._tobs[j], "TimeLimit.truncated": bool(self._tl[j])}
+        return d
 
 try:  # pragma: no cover - SB3 is not part of this image
     from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _VecEnvBase
@@ -60,17 +94,21 @@ class AviaryVecEnv(_VecEnvBase):
             _VecEnvBase.__init__(self, self.num_envs, self.observation_space, self.action_space)
 
     def _bind_packed(self, ring):
+        """[obs | terminal obs | reward | terminated | truncated] in one device buffer the env writes
+        into (bind_outputs), so a step's outputs reach the host in ONE asynchronous copy and one wait
+        (the terminal rows of the envs that finished are read from it; no second round trip)"""
         env, E = self.env, self.num_envs
         obs_shape = tuple(env._obs.shape)
         dev = env._obs.device
         nobs = int(np.prod(obs_shape)) * 4
-        self._off = (nobs, nobs + 4 * E, nobs + 5 * E)
-        self._nbytes = (nobs + 6 * E + 15) // 16 * 16
+        self._off = (2 * nobs, 2 * nobs + 4 * E, 2 * nobs + 5 * E)
+        self._nbytes = (2 * nobs + 6 * E + 15) // 16 * 16
         self._dev = torch.zeros(self._nbytes, dtype=torch.uint8, device=dev)
         o_rew, o_term, o_trunc = self._off
         d = self._dev
         env.bind_outputs(d[:nobs].view(torch.float32).view(obs_shape), d[o_rew:o_term].view(torch.float32),
-                         d[o_term:o_trunc].view(torch.bool), d[o_trunc:o_trunc + E].view(torch.bool))
+                         d[o_term:o_trunc].view(torch.bool), d[o_trunc:o_trunc + E].view(torch.bool),
+                         tobs=d[nobs:2 * nobs].view(torch.float32).view(obs_shape))
         pin = dev.type == "cuda"
         self._host = [torch.zeros(self._nbytes, dtype=torch.uint8, pin_memory=pin) for _ in range(ring)]
         self._slot = 0
@@ -78,7 +116,8 @@ class AviaryVecEnv(_VecEnvBase):
         for h in self._host:
             hn = h.numpy()
             self._views.append((hn[:nobs].view(np.float32).reshape(obs_shape), hn[o_rew:o_term].view(np.float32),
-                                hn[o_term:o_trunc].view(np.bool_), hn[o_trunc:o_trunc + E].view(np.bool_)))
+                                hn[o_term:o_trunc].view(np.bool_), hn[o_trunc:o_trunc + E].view(np.bool_),
+                                hn[nobs:2 * nobs].view(np.float32).reshape(obs_shape)))
         act_shape = tuple(getattr(env, "_act_shape", (E,) + tuple(self.action_space.shape)))
         self._act_host = torch.zeros(act_shape, dtype=torch.float32, pin_memory=pin)
         self._act_dev = torch.zeros(act_shape, dtype=torch.float32, device=dev)
@@ -125,16 +164,12 @@ class AviaryVecEnv(_VecEnvBase):
         return self._act_dev
 
     def _step_wait_packed(self):
-        _, _, _, _, info = self.env.step(self._act_in(self._actions))
-        obs, rew, term, trunc = self._copy_out()
+        self.env.step(self._act_in(self._actions))
+        obs, rew, term, trunc, tobs_all = self._copy_out()
         done = term | trunc
         idx = np.flatnonzero(done)
-        infos = [_NO_INFO] * self.num_envs
-        if len(idx):
-            tobs = info["terminal_observation"].index_select(
-                0, torch.from_numpy(idx).to(self._dev.device, non_blocking=True)).cpu().numpy()
-            for j, e in enumerate(idx):
-                infos[e] = {"terminal_observation": tobs[j], "TimeLimit.truncated": bool(trunc[e] and not term[e])}
+        # terminal rows copied out of the (reused) pinned slot now; their dicts are built on demand
+        infos = _StepInfos(self.num_envs, idx, tobs_all[idx], (trunc & ~term)[idx])
         if not self.zero_copy:
             obs, rew = obs.copy(), rew.copy()
         return obs, rew, done, infos

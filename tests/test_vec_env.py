@@ -25,10 +25,15 @@ class _Scripted:
         self._act_shape = (E, 1, 4)
         self.actions = []
 
-    def bind_outputs(self, obs, rew, term, trunc):      # the batched envs' contract
-        for old, new in ((self._obs, obs), (self._rew, rew), (self._term, term), (self._trunc, trunc)):
+    def bind_outputs(self, obs, rew, term, trunc, tobs=None):      # the batched envs' contract
+        want = ((self._obs, obs), (self._rew, rew), (self._term, term), (self._trunc, trunc))
+        if tobs is not None:
+            want += ((self.tobs, tobs),)
+        for old, new in want:
             assert new.shape == old.shape and new.dtype == old.dtype and new.is_contiguous()
         self._obs, self._rew, self._term, self._trunc = obs, rew, term, trunc
+        if tobs is not None:
+            self.tobs = tobs
 
     def reset(self, seed=None):
         self._obs.zero_()
