@@ -1321,12 +1321,25 @@ __device__ __forceinline__ bool track_query_wave(const RaceConst<Real>& C, const
 // obs row (MultiRaceAviary._computeObs, 566-661) written straight to global memory
 // ---------------------------------------------------------------------------------------
 template <typename Real, class TS>
+__device__ __forceinline__ void race_obs_row_rpy(const RaceConst<Real>& C, const TS& T, V3<Real> pos, V3<Real> rpy,
+                                                 V3<Real> vel, V3<Real> w, int gate, float* row, bool write, Real* row0,
+                                                 uint32_t gin, uint32_t oin);
+// the obs row from the pose quaternion (its Euler angles computed here)
+template <typename Real, class TS>
 __device__ __forceinline__ void race_obs_row(const RaceConst<Real>& C, const TS& T,
                                              V3<Real> pos, Q4<Real> q, V3<Real> vel, V3<Real> w, int gate,
                                              float* row, bool write, Real* row0, uint32_t gin, uint32_t oin,
                                              V3<Real>* rpy_out = nullptr) {
     const V3<Real> rpy = euler_xyz_fast_u(q);
     if (rpy_out) *rpy_out = rpy;
+    race_obs_row_rpy(C, T, pos, rpy, vel, w, gate, row, write, row0, gin, oin);
+}
+// the obs row from given Euler angles (a reset's nominal pose: RaceConst::nom_rpy, the same bits
+// euler_xyz_fast gives for nom_q)
+template <typename Real, class TS>
+__device__ __forceinline__ void race_obs_row_rpy(const RaceConst<Real>& C, const TS& T, V3<Real> pos, V3<Real> rpy,
+                                                 V3<Real> vel, V3<Real> w, int gate, float* row, bool write, Real* row0,
+                                                 uint32_t gin, uint32_t oin) {
     const Real k12[12] = {pos.x, pos.y, pos.z, rpy.x, rpy.y, rpy.z, vel.x, vel.y, vel.z, w.x, w.y, w.z};
     if (write)
 #pragma unroll
@@ -1421,7 +1434,7 @@ __device__ __forceinline__ void race_reset_lane(const RaceArgs<Real>& a, const R
     uint32_t gin, oin;
     const TrackSrc<Real, false> T{f, EN, slot, nullptr, 0};   // the fields just written above
     track_query(C, T, drone_shape(C, npos, nq), Real(0.45), false, Real(0), gin, oin);
-    race_obs_row(C, T, npos, nq, zero, zero, 0, obs_row, obs_row != nullptr, row0, gin, oin);
+    race_obs_row_rpy(C, T, npos, nominal_rpy(C, dn), zero, zero, 0, obs_row, obs_row != nullptr, row0, gin, oin);
     if (C.compete && obs_row) {   // other drones' nominal pos + rpy
         int idx = 0;
         for (int k = 0; k < C.N; ++k) {

@@ -104,12 +104,24 @@ __device__ __forceinline__ Real euler_axis_q4(Q4<Real> q, int a) {
 // arithmetic as mellinger_compute<Real> (FP contraction off; fp32: reciprocal multiplies, fp64:
 // numpy's correctly rounded divisions (by constants: divc_) and the firmware's C float divisions),
 // split across the quad.
+#ifdef ADRP_CTRL_PHASES   // measurement-only: the controller's sub-phases (tools/race_phases.py, make devc)
+#define CP_PARAM , uint64_t (&cp)[8]
+#define CP_ARG , cp
+#define CP_MARK(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define CP_ADD(i, dt) cp[i] += (dt)
+#else
+#define CP_PARAM
+#define CP_ARG
+#define CP_MARK(var)
+#define CP_ADD(i, dt)
+#endif
 template <typename Real>
 __device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, const float sp[3], float xc_x,
                                              float xc_y, Real rpy_a, Real& prv, float& l1, float& l2, Real noise_m,
-                                             int ql, const M3<Real>& Rq) {
+                                             int ql, const M3<Real>& Rq CP_PARAM) {
 #pragma clang fp contract(off)
     constexpr bool F32 = sizeof(Real) == 4;
+    CP_MARK(m0);
     const Real rate = F32 ? (rpy_a - prv) * Real(500) : divc_(rpy_a - prv, Real(0.002));
     prv = rpy_a;
     const Real acc_z = F32 ? (d.vel.z - d.prev_vel[2]) * Real(500.0 / 9.8) + Real(1)
@@ -118,6 +130,8 @@ __device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, co
     const float g_a = lpf_apply(lpf, l1, l2, float(rate * Real(57.29577951308232)));
     const float gyro[3] = {qbc(g_a, 0), qbc(g_a, 1), qbc(g_a, 2)};
     Real pwm;
+    CP_MARK(m1);
+    CP_ADD(1, m1 - m0);
     if (float(acc_z) < -0.5f) d.tumble += 1; else d.tumble = 0;
     if (d.tumble >= 30) {
         d.tick += 1;
@@ -152,6 +166,8 @@ __device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, co
             mellinger_fw<Real, F32, false>(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
 #endif
         }
+        CP_MARK(m2);
+        CP_ADD(2, m2 - m1);
         d.tick += 1;
         // _compute_pwms (423-442), motor ql of [t-r+p+y, t-r-p-y, t+r-p+y, t+r+p-y]
         const Real r = Real(d.ctl[0]) / Real(2), p = Real(d.ctl[1]) / Real(2), y = Real(d.ctl[2]), th = Real(d.ctl[3]);
@@ -174,6 +190,8 @@ __device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, co
         d.prev[k] = d.rpm[k];
         d.rpm[k] = qbc(rnew, k);
     }
+    CP_MARK(m3);
+    CP_ADD(3, m3 - m0);   // whole wrapper (pwm / rpm chain = slot 3 - 1 - 2)
 }
 
 // the block's LDS copy of its drones' env tracks, [field][drone] (owner lane l -> drone l / 4)
@@ -430,7 +448,7 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
 #ifdef ADRP_EXP_RESET_NOROW
     for (int k = 0; k < 15; ++k) row0[k] = T.v[k];
 #else
-    race_obs_row(C, T, npos, nq, zero, zero, 0, obs_row, owner, row0, gin, oin);
+    race_obs_row_rpy(C, T, npos, nominal_rpy(C, dn), zero, zero, 0, obs_row, owner, row0, gin, oin);
 #endif
     RESET_MARK(5);
     // the nominal Euler angles (RaceConst::nom_rpy, race_const_init_kernel)
@@ -642,6 +660,9 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
 #ifdef ADRP_RACE_TIMING
     uint64_t acc_phys = 0;
 #endif
+#ifdef ADRP_CTRL_PHASES
+    uint64_t cp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     for (int s0 = 0; s0 < H.S; s0 += 32) {
     if (s0 > 0) {
         d.tick_base = d.tick;
@@ -721,6 +742,8 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
                 Fx = Fx + fd;
                 Tx = cross(d.kpos - lo, fd);
             }
+            CP_MARK(f1);
+            CP_ADD(4, f1 - ta);
             race_pyb_substep_r<Real, PH>(H, d, Fx, Tx, Rq, Rl);
         }
 #ifdef ADRP_RACE_TIMING
@@ -732,7 +755,11 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) d.rpm[k] = d.prev[k] = Real(0);
         } else {
-            mellinger_q4(d, lpf, sp, xc_x, xc_y, euler_axis_q4(d.q, cax), prv, l1, l2, noise_m, ql, Rq);
+            CP_MARK(e0);
+            const Real rpy_a = euler_axis_q4(d.q, cax);
+            CP_MARK(e1);
+            CP_ADD(0, e1 - e0);
+            mellinger_q4(d, lpf, sp, xc_x, xc_y, rpy_a, prv, l1, l2, noise_m, ql, Rq CP_ARG);
         }
     }
     }
@@ -930,7 +957,10 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
 #ifdef ADRP_RACE_TIMING
     RACE_MARK(t6);   // tail: reward, flags, stores and the auto-reset of done envs
     if (threadIdx.x == 0) {
-#ifdef ADRP_RESET_PHASES   // the reset's sub-phases of this block's last reset (0 if none)
+#if defined(ADRP_CTRL_PHASES)   // euler, wrapper head, firmware, wrapper (all), forces, physics, loop
+        RACE_WAVE(0, cp[0]); RACE_WAVE(1, cp[1]); RACE_WAVE(2, cp[2]); RACE_WAVE(3, cp[3]);
+        RACE_WAVE(4, cp[4]); RACE_WAVE(5, acc_phys); RACE_WAVE(6, t2 - t1); RACE_WAVE(7, t6 - t0);
+#elif defined(ADRP_RESET_PHASES)   // the reset's sub-phases of this block's last reset (0 if none)
         for (int k = 0; k < 8; ++k) RACE_WAVE(k, reset ? g_reset_mark[k + 1] - g_reset_mark[k] : 0);
 #else
         RACE_WAVE(0, t1 - t0); RACE_WAVE(1, acc_phys); RACE_WAVE(2, (t2 - t1) - acc_phys); RACE_WAVE(3, t3 - t2);
