@@ -94,6 +94,9 @@ def load():
         lib.adrp_policy_sample.restype = I
         lib.adrp_gae.argtypes = [P, P, P, P, P, I, I, ctypes.c_double, ctypes.c_double, P, P, P]
         lib.adrp_gae.restype = I
+    if hasattr(lib, "adrp_compact_rows"):
+        lib.adrp_compact_rows.argtypes = [P, P, P, I, I, I, P, P, P, P]
+        lib.adrp_compact_rows.restype = I
     if hasattr(lib, "adrp_math_probe"):      # (A/B runs may load an older build without it)
         lib.adrp_math_probe.argtypes = [I, P, P, I, P]
         lib.adrp_math_probe.restype = I

@@ -246,12 +246,14 @@ __device__ __forceinline__ void sincos_tiny(double x, double* s, double* c) {
 // atan2(y, x): octant reduction to a = min/max in [0, 1], then t = a or (a - 1)/(a + 1) (one
 // division either way: (min - max)/(min + max)) so |t| <= tan(pi/8), atan t = t + t^3 P(t^2)
 // with a degree-9 near-minimax P (1.7e-16 relative).  atan2(0, 0) = 0 (as the fp32 fatan2_).
-__device__ __forceinline__ double atan2(double y, double x) {
+// NC: finite arguments only (the race controller's Euler angles): no non-finite fix-ups
+template <bool NC>
+__device__ __forceinline__ double atan2_t(double y, double x) {
     const double ax = __builtin_fabs(x), ay = __builtin_fabs(y);
     const double mx = __builtin_fmax(ax, ay), mn = __builtin_fmin(ax, ay);
     const bool big = mn > 0.41421356237309504880 * mx;
     const double num = big ? mn - mx : mn, den = big ? mn + mx : mx;
-    const double t = mx > 0.0 ? num * rcp(den) : 0.0;
+    const double t = mx > 0.0 ? num * (NC ? rcp_nc(den) : rcp(den)) : 0.0;
     const double s = t * t;
     double p = 0.021428368220326288;
     p = fma_(p, s, -0.04375458729368037);
@@ -268,7 +270,39 @@ __device__ __forceinline__ double atan2(double y, double x) {
     if (ay > ax) r = 1.57079632679489661923 - r;
     if (x < 0.0) r = 3.14159265358979323846 - r;
     // NaN in -> NaN out as libm (fmax / fmin above drop a NaN operand)
+    if constexpr (NC) return __builtin_copysign(r, y);
     return __builtin_isunordered(x, y) ? x + y : __builtin_copysign(r, y);
+}
+__device__ __forceinline__ double atan2(double y, double x) { return atan2_t<false>(y, x); }
+__device__ __forceinline__ double atan2_nc(double y, double x) { return atan2_t<true>(y, x); }
+// 2^(j/32), j = 0..31 (correctly rounded), the table of f64::exp_tab (the race kernel copies it to LDS)
+static __device__ __constant__ double kExp2Tab32[32] = {
+    1.0, 1.0218971486541166, 1.0442737824274138, 1.0671404006768237, 1.0905077326652577, 1.1143867425958924,
+    1.1387886347566916, 1.1637248587775775, 1.189207115002721, 1.215247359980469, 1.241857812073484,
+    1.2690509571917332, 1.2968395546510096, 1.3252366431597413, 1.3542555469368927, 1.383909881963832,
+    1.4142135623730951, 1.4451808069770467, 1.4768261459394993, 1.5091644275934228, 1.5422108254079407,
+    1.5759808451078865, 1.6104903319492543, 1.645755478153965, 1.681792830507429, 1.718619298122478,
+    1.7562521603732995, 1.7947090750031072, 1.8340080864093424, 1.8741676341103, 1.9152065613971474,
+    1.9571441241754002};
+// exp(x), x <= 0 (the race downwash): k = 32 m + j = rint(32 x / ln 2), 2^(j/32) from a table the
+// caller holds in LDS (kExp2Tab32), r = x - k ln2/32 (two-part, |r| <= ln2/64), exp r by Taylor to r^6
+// (truncation 3.4e-18 relative), 2^m by v_ldexp_f64: 7 FMAs and 7 two-word constants where exp() pays
+// 14 FMAs and 14 constants on the chain (tests/test_math_gpu.py, ADRP_MATH_EXP_TAB)
+__device__ __forceinline__ double exp_tab(double x, const double* tab) {
+    x = __builtin_fmax(x, -1000.0);
+    const double k = __builtin_rint(x * 46.16624130844683);
+    double r = fma_(-k, 0.021660849390173098, x);   // ln2/32, 33 significant bits: k * hi is exact
+    r = fma_(-k, 2.325192846878874e-12, r);
+    const int ki = int(k);
+    const double t = tab[ki & 31];
+    double p = 1.0 / 720;
+    p = fma_(p, r, 1.0 / 120);
+    p = fma_(p, r, 1.0 / 24);
+    p = fma_(p, r, 1.0 / 6);
+    p = fma_(p, r, 0.5);
+    p = fma_(p, r, 1.0);
+    p = fma_(p, r, 1.0);
+    return __builtin_amdgcn_ldexp(t * p, ki >> 5);
 }
 // asin(s), |s| < 1: atan2(s, sqrt((1 - s)(1 + s)))
 __device__ __forceinline__ double asin(double s) { return atan2(s, sqrt((1.0 - s) * (1.0 + s))); }
@@ -442,6 +476,9 @@ __device__ __forceinline__ float fatan2_(float y, float x) {
     return copysignf(r, y);
 }
 __device__ __forceinline__ double fatan2_(double y, double x) { return f64::atan2(y, x); }
+// finite arguments (no NaN / inf fix-ups in fp64)
+__device__ __forceinline__ float fatan2_nc_(float y, float x) { return fatan2_(y, x); }
+__device__ __forceinline__ double fatan2_nc_(double y, double x) { return f64::atan2_nc(y, x); }
 __device__ __forceinline__ float fasin_(float s) { return fatan2_(s, __builtin_amdgcn_sqrtf((1.0f - s) * (1.0f + s))); }
 __device__ __forceinline__ double fasin_(double s) { return f64::asin(s); }
 __device__ __forceinline__ float fexp_(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }

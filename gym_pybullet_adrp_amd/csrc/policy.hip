@@ -292,3 +292,61 @@ extern "C" int adrp_gae(const float* rewards, const float* values, const float* 
     if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("gae launch: ") + hipGetErrorString(e));
     return ADRP_OK;
 }
+
+// ---------------------------------------------------------------------------------------
+// SB3 VecEnv host path (vec_env.py): the terminal observations of the envs that finished, gathered
+// behind the step's packed outputs so one device -> host copy carries them (DummyVecEnv puts
+// infos[e]["terminal_observation"] only on the envs whose episode ended).  One workgroup of 1024
+// lanes scans the done flags in 1024-env chunks: wave ballots + per-wave counts in LDS give each
+// done env its rank, idx[rank] = env (ascending); then the first min(count, cap) rows are copied.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) compact_rows_kernel(const uint8_t* __restrict__ term,
+                                                            const uint8_t* __restrict__ trunc,
+                                                            const float* __restrict__ rows, int n, int rf, int cap,
+                                                            int32_t* __restrict__ count, int32_t* __restrict__ idx,
+                                                            float* __restrict__ out) {
+    __shared__ int wsum[16];
+    __shared__ int total;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int base = 0;
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+        const int i = c0 + tid;
+        const bool f = i < n && (term[i] | trunc[i]) != 0;
+        const uint64_t b = __ballot(f);
+        if (lane == 0) wsum[wave] = __popcll(b);
+        __syncthreads();
+        int off = base, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const int c = wsum[w];
+            off += w < wave ? c : 0;
+            tot += c;
+        }
+        if (f) idx[off + __popcll(b & ((uint64_t(1) << lane) - 1))] = i;
+        base += tot;
+        __syncthreads();   // wsum is rewritten by the next chunk
+    }
+    if (tid == 0) {
+        count[0] = base;
+        total = base;
+    }
+    __syncthreads();   // idx (global, this workgroup's writes) and total visible to every lane
+    const int m = total < cap ? total : cap;
+    const long long nf = (long long)m * rf;
+    for (long long k = tid; k < nf; k += 1024) {
+        const int j = int(k / rf), c = int(k - (long long)j * rf);
+        out[k] = rows[(long long)idx[j] * rf + c];
+    }
+}
+
+extern "C" int adrp_compact_rows(const uint8_t* term, const uint8_t* trunc, const float* rows, int n, int row_floats,
+                                 int cap, int32_t* count, int32_t* idx, float* out_rows, void* stream) {
+    if (!term || !trunc || !rows || !count || !idx || (cap > 0 && !out_rows))
+        return seterr(nullptr, ADRP_ERR_INVALID, "adrp_compact_rows: NULL argument");
+    if (n < 0 || row_floats <= 0 || cap < 0) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_compact_rows: sizes");
+    hipLaunchKernelGGL(compact_rows_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, term, trunc, rows, n, row_floats,
+                       cap, count, idx, out_rows);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("compact launch: ") + hipGetErrorString(e));
+    return ADRP_OK;
+}

@@ -887,7 +887,10 @@ __device__ __forceinline__ void race_pyb_substep_r(const RaceConst<Real>& C, RDr
         const Real r2 = d.rpm[i] * d.rpm[i];
         const Real f = r2 * C.kf;
         sum_f += f;
-        P = P + v3(f * C.px[i], f * C.py[i], f * C.pz[i]);
+        // the reference drone's props sit in the body plane: a literal pz = 0 adds f * 0 = +0
+        // (f >= 0) to +0, so P.z stays +0 without the 8 multiply-adds
+        const bool pz0 = __builtin_constant_p(C.pz[i]) && C.pz[i] == Real(0);
+        P = v3(P.x + f * C.px[i], P.y + f * C.py[i], pz0 ? P.z : P.z + f * C.pz[i]);
         t2 += (i & 1) ? -r2 : r2;
     }
     const Real tau_z = t2 * C.km;

@@ -32,6 +32,10 @@ namespace adrp {
 
 constexpr int kQuadDrones = kRaceBlock / 4;   // drones per 64-lane block
 
+// the downwash exponential: fp32 v_exp_f32; fp64 the table form (x <= 0)
+__device__ __forceinline__ float dw_exp(float x, const double*) { return fexp_(x); }
+__device__ __forceinline__ double dw_exp(double x, const double* tab) { return f64::exp_tab(x, tab); }
+
 // DPP quad moves (one VALU op): value of quad lane k (k must fold to a constant), and the mirror
 // lane 3 - ql
 __device__ __forceinline__ int qbc_i(int v, int k) {
@@ -45,6 +49,21 @@ __device__ __forceinline__ int qbc_i(int v, int k) {
 __device__ __forceinline__ float qbc(float v, int k) { return __int_as_float(qbc_i(__float_as_int(v), k)); }
 __device__ __forceinline__ double qbc(double v, int k) {
     return __hiloint2double(qbc_i(__double2hiint(v), k), qbc_i(__double2loint(v), k));
+}
+// quad butterfly partners: quad_perm [1, 0, 3, 2] and [2, 3, 0, 1]
+__device__ __forceinline__ float qswap1(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float qswap2(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double qswap1(double v) {
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0xb1, 0xf, 0xf, false),
+                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0xb1, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double qswap2(double v) {
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x4e, 0xf, 0xf, false),
+                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x4e, 0xf, 0xf, false));
 }
 __device__ __forceinline__ float qmirror(float v) {   // quad_perm [3, 2, 1, 0]
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x1b, 0xf, 0xf, false));
@@ -94,9 +113,10 @@ __device__ __forceinline__ Real euler_axis_q4(Q4<Real> q, int a) {
     const Real sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
     const Real y0 = Real(2) * (q.y * q.z + q.w * q.x), x0 = squ - sqx - sqy + sqz;
     const Real y2 = Real(2) * (q.x * q.y + q.w * q.z), x2 = squ + sqx - sqy - sqz;
-    const Real x1 = hsqrt_((Real(1) - sarg) * (Real(1) + sarg));   // fasin_(sarg)
+    // fasin_(sarg); the argument is > 0 here (|sarg| < 0.99999), the operands finite
+    const Real x1 = hsqrt_nn_((Real(1) - sarg) * (Real(1) + sarg));
     const Real yy = a == 0 ? y0 : (a == 1 ? sarg : y2), xx = a == 0 ? x0 : (a == 1 ? x1 : x2);
-    return fatan2_(yy, xx);
+    return fatan2_nc_(yy, xx);
 }
 
 // MellingerControl.computeControl (154-262) for the quad: lane ql owns axis min(ql, 2) of the
@@ -104,6 +124,17 @@ __device__ __forceinline__ Real euler_axis_q4(Q4<Real> q, int a) {
 // arithmetic as mellinger_compute<Real> (FP contraction off; fp32: reciprocal multiplies, fp64:
 // numpy's correctly rounded divisions (by constants: divc_) and the firmware's C float divisions),
 // split across the quad.
+// measurement-only (make devx XD=-DADRP_EXP_DUP_...): a phase evaluated twice, the second pass
+// made to wait for the first through an empty asm, so the kernel's time grows by the phase's cost on
+// the chain while every result (and so the trajectory) is unchanged
+template <typename T, typename U>
+__device__ __forceinline__ void exp_dep(T& x, const U& after) { asm volatile("" : "+v"(x) : "v"(after)); }
+template <typename T>
+__device__ __forceinline__ void exp_sink(const T& x) { asm volatile("" ::"v"(x)); }
+
+template <typename T>
+__device__ __forceinline__ T sel3(const T (&v)[3], int a) { return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]); }
+
 #ifdef ADRP_CTRL_PHASES   // measurement-only: the controller's sub-phases (tools/race_phases.py, make devc)
 #define CP_PARAM , uint64_t (&cp)[8]
 #define CP_ARG , cp
@@ -162,7 +193,19 @@ __device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, co
             }
             const float pos[3] = {float(d.pos.x), float(d.pos.y), float(d.pos.z)};
             const float vel[3] = {float(d.vel.x), float(d.vel.y), float(d.vel.z)};
-#ifndef ADRP_EXP_NOFW   // measurement-only switch (phase profile without the firmware)
+            // (a quad split of the firmware, one division per lane for the thrust / z_des / y_des
+            // components and DPP broadcasts, measured slower in both precisions: +1.1 us fp64,
+            // +0.1 us fp32 on config 4, A/B round 4)
+#ifdef ADRP_EXP_DUP_FW
+            {
+                RDrone<Real> d2 = d;
+                mellinger_fw<Real, F32, false>(d2, sp, xc_x, xc_y, gyro, pos, vel, Rm);
+                float p0 = pos[0];
+                exp_dep(p0, d2.ctl[0]);
+                const float pos2[3] = {p0, pos[1], pos[2]};
+                mellinger_fw<Real, F32, false>(d, sp, xc_x, xc_y, gyro, pos2, vel, Rm);
+            }
+#else
             mellinger_fw<Real, F32, false>(d, sp, xc_x, xc_y, gyro, pos, vel, Rm);
 #endif
         }
@@ -211,46 +254,146 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {   // OR over the quad 
 
 // track_bounds with the track dealt over the quad: lane ql tests gate ql and obstacle ql (same
 // per-part arithmetic), the bit masks are OR-ed over the quad
+// The support-bound refinement of part_bounds_refined, pooled over the block: each (lane, part) pair
+// whose centre bounds straddle a cut is queued in LDS and the block's 64 lanes work the queue, so a
+// wave runs ceil(jobs / 64) refinements (usually one) instead of one per part index that any lane
+// needs (up to 7, ~330 instructions each in fp64).  The pool holds every lane's part-frame inputs
+// (gate-frame drone centre / axis, obstacle offsets, gate type) and the refined bounds per (lane,
+// part); the results are the inline form's, operation for operation.
+template <typename Real>
+struct RefinePool {
+    Real in[12][kRaceBlock];   // lg.xyz, ag.xyz (gate frame), dp.xyz, ax.xyz (obstacle frame) per lane
+    Real lo[kRaceBlock * 7], up[kRaceBlock * 7];
+    uint16_t job[kRaceBlock * 7];
+    int low[kRaceBlock];
+};
+
+template <typename Real>
+__device__ __forceinline__ void refine_part(const RaceConst<Real>& C, int k, int low, V3<Real> lg, V3<Real> ag,
+                                            V3<Real> dp, V3<Real> ax, Real& lo2, Real& up2) {
+    V3<Real> off, h;
+    Real r;
+    int cyl;
+    if (k < kGateParts) {
+        M3<Real> R;
+        gate_part(k, low, off, R, h, r, cyl);
+        part_bounds_refined(mulT(R, lg - off), mulT(R, ag), h, r, cyl, C.coll_r, C.coll_hh, lo2, up2);
+    } else {
+        obst_part(k - kGateParts, off, h, r, cyl);
+        part_bounds_refined(dp - off, ax, h, r, cyl, C.coll_r, C.coll_hh, lo2, up2);
+    }
+}
+
+// pool: nullptr refines inline (the auto-reset's divergent lanes); otherwise every lane of the block
+// must call it (two barriers)
 template <typename Real, class TS>
 __device__ __forceinline__ void track_bounds_q4(const RaceConst<Real>& C, const TS& T, const Shape<Real>& ds,
                                                 Real cut, Real ccut, int ql, bool want_contact, uint32_t& gin,
-                                                uint32_t& oin, uint32_t& amb, uint32_t& camb_all, bool& ccert) {
+                                                uint32_t& oin, uint32_t& amb, uint32_t& camb_all, bool& ccert,
+                                                RefinePool<Real>* pool = nullptr) {
     const Real tol = Real(1e-5);
     const Real dr = hsqrt_(ds.r * ds.r + ds.h.z * ds.h.z);
     const V3<Real> p = ds.c, ax = col2(ds.R);
     amb = 0; camb_all = 0;
     gin = 0; oin = 0;
     ccert = false;
-    const int g = ql;
-    if (g < C.num_gates) {
-        const V3<Real> dp = p - v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
+    const int g = ql, o = ql;
+    const bool has_g = g < C.num_gates, has_o = o < C.num_obstacles;
+    // centre bounds of this lane's gate (parts 0-4) and obstacle (parts 5-6)
+    Real plo[7], pup[7];
+    uint32_t need = 0;
+    V3<Real> lg = v3(Real(0), Real(0), Real(0)), ag = lg, dp = lg;
+    int low = 0;
+    if (has_g) {
+        const V3<Real> dg = p - v3(T(RF_GATE + 4 * g), T(RF_GATE + 4 * g + 1), T(RF_GATE + 4 * g + 2));
         Real sn, cs;
         sincos_f_(T(RF_GATE + 4 * g + 3), &sn, &cs);
-        const V3<Real> lg = v3(cs * dp.x + sn * dp.y, -sn * dp.x + cs * dp.y, dp.z);
-        const V3<Real> ag = v3(cs * ax.x + sn * ax.y, -sn * ax.x + cs * ax.y, ax.z);
-        const int low = C.gate_type[g] > 0;
+        lg = v3(cs * dg.x + sn * dg.y, -sn * dg.x + cs * dg.y, dg.z);
+        ag = v3(cs * ax.x + sn * ax.y, -sn * ax.x + cs * ax.y, ax.z);
+        low = C.gate_type[g] > 0;
+    }
+    if (has_o) dp = p - v3(T(RF_OBST + 3 * o), T(RF_OBST + 3 * o + 1), T(RF_OBST + 3 * o + 2));
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        V3<Real> off, h, lp;
+        Real r;
+        int cyl;
+        if (k < kGateParts) {
+            M3<Real> R;
+            gate_part(k, low, off, R, h, r, cyl);
+            lp = mulT(R, lg - off);
+        } else {
+            obst_part(k - kGateParts, off, h, r, cyl);
+            lp = dp - off;
+        }
+        const Real pd = point_part_dist(lp, h, r, cyl);
+        plo[k] = pd - dr;
+        pup[k] = pd;
+        const bool live = k < kGateParts ? has_g : has_o;
+        if (live && C.refine && ((!(pd < cut - tol) && plo[k] < cut + tol) || (want_contact && plo[k] < ccut + tol)))
+            need |= 1u << k;
+    }
+    if (pool == nullptr) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            if ((need >> k) & 1u) {
+                Real lo2, up2;
+                refine_part(C, k, low, lg, ag, dp, ax, lo2, up2);
+                plo[k] = fmaxr_(plo[k], lo2);
+                pup[k] = up2 < pup[k] ? up2 : pup[k];
+            }
+        }
+    } else {
+        const int tl = threadIdx.x;
+        const Real iv[12] = {lg.x, lg.y, lg.z, ag.x, ag.y, ag.z, dp.x, dp.y, dp.z, ax.x, ax.y, ax.z};
+#pragma unroll
+        for (int i = 0; i < 12; ++i) pool->in[i][tl] = iv[i];
+        pool->low[tl] = low;
+        const int n = __popc(need);
+        int incl = n;   // inclusive scan of the queue lengths
+#pragma unroll
+        for (int s = 1; s < kRaceBlock; s <<= 1) {
+            const int t = __shfl_up(incl, s, kRaceBlock);
+            if (tl >= s) incl += t;
+        }
+        const int total = __shfl(incl, kRaceBlock - 1, kRaceBlock);
+        int pos = incl - n;
+        for (uint32_t m = need; m; m &= m - 1) pool->job[pos++] = uint16_t((tl << 3) | __builtin_ctz(m));
+        __syncthreads();
+        for (int base = 0; base < total; base += kRaceBlock) {
+            const int j = base + tl;
+            if (j < total) {
+                const int job = pool->job[j], L = job >> 3, k = job & 7;
+                const V3<Real> jl = v3(pool->in[0][L], pool->in[1][L], pool->in[2][L]);
+                const V3<Real> ja = v3(pool->in[3][L], pool->in[4][L], pool->in[5][L]);
+                const V3<Real> jd = v3(pool->in[6][L], pool->in[7][L], pool->in[8][L]);
+                const V3<Real> jx = v3(pool->in[9][L], pool->in[10][L], pool->in[11][L]);
+                Real lo2, up2;
+                refine_part(C, k, pool->low[L], jl, ja, jd, jx, lo2, up2);
+                pool->lo[L * 7 + k] = lo2;
+                pool->up[L * 7 + k] = up2;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            if ((need >> k) & 1u) {
+                const Real lo2 = pool->lo[tl * 7 + k], up2 = pool->up[tl * 7 + k];
+                plo[k] = fmaxr_(plo[k], lo2);
+                pup[k] = up2 < pup[k] ? up2 : pup[k];
+            }
+        }
+    }
+    // classification (race_kernel.h track_bounds): in the cut / ambiguous / contact certain or open
+    if (has_g) {
         bool in = false;
         uint32_t gamb = 0, camb = 0;
 #pragma unroll
         for (int k = 0; k < kGateParts; ++k) {
-            V3<Real> off, h;
-            M3<Real> R;
-            Real r;
-            int cyl;
-            gate_part(k, low, off, R, h, r, cyl);
-            const V3<Real> lp = mulT(R, lg - off);
-            const Real pd = point_part_dist(lp, h, r, cyl);
-            Real lo = pd - dr, up = pd;
-            if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || (want_contact && lo < ccut + tol))) {   // support bounds
-                Real lo2, up2;
-                part_bounds_refined(lp, mulT(R, ag), h, r, cyl, ds.r, ds.h.z, lo2, up2);
-                lo = fmaxr_(lo, lo2);
-                up = up2 < up ? up2 : up;
-            }
-            in |= up < cut - tol;
-            if (lo < cut + tol) gamb |= 1u << k;
-            if (want_contact && lo < ccut + tol) {   // centre inside the part: contact (race_kernel.h)
-                if (up == Real(0)) ccert = true;
+            in |= pup[k] < cut - tol;
+            if (plo[k] < cut + tol) gamb |= 1u << k;
+            if (want_contact && plo[k] < ccut + tol) {   // centre inside the part: contact (race_kernel.h)
+                if (pup[k] == Real(0)) ccert = true;
                 else camb |= 1u << k;
             }
         }
@@ -258,29 +401,15 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<Real>& C, const 
         amb |= ((in ? 0u : gamb) | camb) << (g * kGateParts);
         camb_all |= camb << (g * kGateParts);
     }
-    const int o = ql;
-    if (o < C.num_obstacles) {
-        const V3<Real> dp = p - v3(T(RF_OBST + 3 * o), T(RF_OBST + 3 * o + 1), T(RF_OBST + 3 * o + 2));
+    if (has_o) {
         bool in = false;
         uint32_t gamb = 0, camb = 0;
 #pragma unroll
         for (int k = 0; k < kObstParts; ++k) {
-            V3<Real> off, h;
-            Real r;
-            int cyl;
-            obst_part(k, off, h, r, cyl);
-            const Real pd = point_part_dist(dp - off, h, r, cyl);
-            Real lo = pd - dr, up = pd;
-            if (C.refine && ((!(pd < cut - tol) && lo < cut + tol) || (want_contact && lo < ccut + tol))) {
-                Real lo2, up2;
-                part_bounds_refined(dp - off, ax, h, r, cyl, ds.r, ds.h.z, lo2, up2);
-                lo = fmaxr_(lo, lo2);
-                up = up2 < up ? up2 : up;
-            }
-            in |= up < cut - tol;
-            if (lo < cut + tol) gamb |= 1u << k;
-            if (want_contact && lo < ccut + tol) {   // centre inside the part: contact (race_kernel.h)
-                if (up == Real(0)) ccert = true;
+            in |= pup[kGateParts + k] < cut - tol;
+            if (plo[kGateParts + k] < cut + tol) gamb |= 1u << k;
+            if (want_contact && plo[kGateParts + k] < ccut + tol) {
+                if (pup[kGateParts + k] == Real(0)) ccert = true;
                 else camb |= 1u << k;
             }
         }
@@ -292,8 +421,6 @@ __device__ __forceinline__ void track_bounds_q4(const RaceConst<Real>& C, const 
     ccert = quad_or(ccert ? 1u : 0u) != 0;
 }
 
-template <typename T>
-__device__ __forceinline__ T sel3(const T (&v)[3], int a) { return a == 0 ? v[0] : (a == 1 ? v[1] : v[2]); }
 
 // ---- auto-reset of a done drone by its quad ----
 // race_reset_lane's arithmetic (MultiRaceAviary.reset 127-167, _addObstacles 347-403, _drone_init
@@ -562,15 +689,22 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     constexpr int kRowF = 49 + 6 * (G - 1);   // widest obs row of this G
     // the sub-step draw table is dead after the loop: the GJK job pool reuses its LDS
     constexpr size_t kDrawBytes = DRAWS ? size_t(kRacePreS) * 7 * kQuadDrones * sizeof(float) : 16;
-    constexpr size_t kScratchBytes = kDrawBytes > sizeof(TrackJobs) ? kDrawBytes : sizeof(TrackJobs);
+    constexpr size_t kPost = sizeof(TrackJobs) > sizeof(RefinePool<Real>) ? sizeof(TrackJobs) : sizeof(RefinePool<Real>);
+    constexpr size_t kScratchBytes = kDrawBytes > kPost ? kDrawBytes : kPost;
     __shared__ __attribute__((aligned(16))) unsigned char scratch_lds[kScratchBytes];
     float* const pre_draws = reinterpret_cast<float*>(scratch_lds);
     TrackJobs& tjobs = *reinterpret_cast<TrackJobs*>(scratch_lds);
+    RefinePool<Real>* const rpool = reinterpret_cast<RefinePool<Real>*>(scratch_lds);   // (bounds, then tjobs)
     __shared__ Real trk_lds[kTrackFields * kQuadDrones];                   // [field][drone]
     __shared__ float4 rows4[kQuadDrones * kRowF / 4];
     // the constant block in LDS: the post-loop phases and the auto-reset index it by drone / gate /
     // obstacle (lane-varying), which from global memory is a dependent miss per table
     __shared__ __attribute__((aligned(16))) RaceConst<Real> c_lds;
+    __shared__ double exp_lds[32];
+    constexpr bool kDwF64 = !F32 && (PH == ADRP_PHYS_PYB_DW || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
+    if constexpr (kDwF64) {
+        if (threadIdx.x < 32) exp_lds[threadIdx.x] = f64::kExp2Tab32[threadIdx.x];
+    }
     {
         constexpr int nw = int(sizeof(RaceConst<Real>) / 4);
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.c);
@@ -648,9 +782,18 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
     if (threadIdx.x == 0) g_gjk_wave_iters = 0;
 #endif
+    if constexpr (!DRAWS && kDwF64) __syncthreads();   // the exp table (DRAWS: the barrier below)
     if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
         if (!inj) quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
         __syncthreads();
+#ifdef ADRP_EXP_DUP_DRAWS
+        {
+            uint32_t ep2 = ep;
+            exp_dep(ep2, pre_draws[tl]);
+            if (!inj) quad_draws<Real>(H, pre_draws, a.seed, gid, ep2, dn, sc0, ql, qd, H.S);
+            __syncthreads();
+        }
+#endif
     }
     // lane-distributed controller state: axis cax of the rate history and the gyro filter
     Real prv = sel3(d.prev_rpy, cax);
@@ -682,35 +825,46 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         } else {
             V3<Real> Fx = v3(Real(0), Real(0), Real(0)), Tx = v3(Real(0), Real(0), Real(0));
             if constexpr (PH == ADRP_PHYS_PYB_DW || PH == ADRP_PHYS_PYB_GND_DRAG_DW) {
-                // _downwash (BaseAviary.py:792-818): lane ql evaluates partner drones ql, ql + 4;
-                // the sum runs in partner order with the one-lane loop's fused update
-                Real al[(G + 3) / 4], ex[(G + 3) / 4];
+#ifdef ADRP_EXP_DUP_DW
+              V3<Real> dwp = d.pos;
+              for (int rep = 0; rep < 2; ++rep) {
+                if (rep == 1) exp_dep(dwp.x, Fx.z);
+                const V3<Real> pos = dwp;
+#else
+              {
+                const V3<Real>& pos = d.pos;
+#endif
+                // _downwash (BaseAviary.py:792-818): lane ql evaluates partner drones ql, ql + 4 (its
+                // term alpha exp(-(dxy / beta)^2 / 2); 4 dz and beta are > 0 where it is used, dxy
+                // a root of a sum of squares); the quad sums the terms by a DPP butterfly, so every
+                // lane holds the same (t0 + t1) + (t2 + t3)
+                Real tsum = Real(0);
 #pragma unroll
                 for (int j = 0; j < (G + 3) / 4; ++j) {
                     const int k = ql + 4 * j;
                     // ds_bpermute: DPP row broadcasts of the four partners' positions (row_newbcast +
                     // selects) measured 2.5-3 us slower on config 4 (tools/gpu_r3_t20.sh)
                     const int src = (tl & ~(4 * G - 1)) + 4 * (k < G ? k : 0);
-                    const Real ox = __shfl(d.pos.x, src), oy = __shfl(d.pos.y, src), oz = __shfl(d.pos.z, src);
-                    const Real dz = oz - d.pos.z, dx = ox - d.pos.x, dy = oy - d.pos.y;
-                    const Real dxy = hsqrt_(dx * dx + dy * dy);
-                    al[j] = Real(0);
-                    ex[j] = Real(0);
-                    if (k < N && dz > Real(0) && dxy < Real(10)) {
-                        const Real kk = H.prop_r * rcp_(Real(4) * dz);
-                        al[j] = H.dw1 * kk * kk;
-                        const Real beta = H.dw2 * dz + H.dw3;
-                        const Real qq = dxy * rcp_(beta);
-                        ex[j] = fexp_(Real(-0.5) * qq * qq);
-                    }
+                    const Real ox = __shfl(pos.x, src), oy = __shfl(pos.y, src), oz = __shfl(pos.z, src);
+                    const Real dz = oz - pos.z, dx = ox - pos.x, dy = oy - pos.y;
+                    const Real dxy = hsqrt_nn_(dx * dx + dy * dy);
+                    const Real kk = H.prop_r * rcp_nc_(Real(4) * dz);
+                    const Real qq = dxy * rcp_nc_(H.dw2 * dz + H.dw3);
+                    const Real term = H.dw1 * kk * kk * dw_exp(Real(-0.5) * qq * qq, exp_lds);
+                    tsum += (k < N && dz > Real(0) && dxy < Real(10)) ? term : Real(0);
                 }
-                Real fz = 0;
-#pragma unroll
-                for (int k = 0; k < G; ++k) fz -= qbc(al[k / 4], k % 4) * qbc(ex[k / 4], k % 4);
+                tsum += qswap1(tsum);
+                tsum += qswap2(tsum);
+                const Real fz = -tsum;
                 const M3<Real>& Rs = H.link_lag && !(PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? Rl : Rq;
                 Fx = fz * col2(Rs);
+              }
             }
+#ifdef ADRP_EXP_NODIST
+            if (false) {
+#else
             if (H.disturbances) {
+#endif
                 V3<Real> fd;
                 if (inj) {
                     Real f3[3], nz[4];
@@ -744,6 +898,14 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
             }
             CP_MARK(f1);
             CP_ADD(4, f1 - ta);
+#ifdef ADRP_EXP_DUP_STEP
+            {
+                RDrone<Real> d2 = d;
+                M3<Real> Rq2 = Rq, Rl2 = Rl;
+                race_pyb_substep_r<Real, PH>(H, d2, Fx, Tx, Rq2, Rl2);
+                exp_dep(Fx.x, d2.q.x);
+            }
+#endif
             race_pyb_substep_r<Real, PH>(H, d, Fx, Tx, Rq, Rl);
         }
 #ifdef ADRP_RACE_TIMING
@@ -756,7 +918,22 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
             for (int k = 0; k < 4; ++k) d.rpm[k] = d.prev[k] = Real(0);
         } else {
             CP_MARK(e0);
+#ifdef ADRP_EXP_DUP_EUL
+            Q4<Real> q2 = d.q;
+            exp_dep(q2.x, euler_axis_q4(d.q, cax));
+            const Real rpy_a = euler_axis_q4(q2, cax);
+#else
             const Real rpy_a = euler_axis_q4(d.q, cax);
+#endif
+#ifdef ADRP_EXP_DUP_WRAP
+            {
+                RDrone<Real> d2 = d;
+                Real prv2 = prv;
+                float l12 = l1, l22 = l2;
+                mellinger_q4(d2, lpf, sp, xc_x, xc_y, rpy_a, prv2, l12, l22, noise_m, ql, Rq CP_ARG);
+                exp_dep(prv, d2.rpm[0]);
+            }
+#endif
             CP_MARK(e1);
             CP_ADD(0, e1 - e0);
             mellinger_q4(d, lpf, sp, xc_x, xc_y, rpy_a, prv, l1, l2, noise_m, ql, Rq CP_ARG);
@@ -838,7 +1015,11 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
 #ifdef ADRP_OBS_PHASES
     RACE_MARK(o0);
 #endif
-    track_bounds_q4(C, T, ds, Real(0.45), Real(1e-6), ql, !(d.flags & 1), gin, oin, amb, camb_all, ccert);
+    // the pooled refinement in fp64 (config 3 + actor 82.4 -> 78.5 us, config 4 71.5 -> 71.2 us); fp32
+    // refines inline (pooled: config 4 43.7 -> 44.1 us, config 3 + actor 58.4 -> 57.4 us; A/B round 4)
+    track_bounds_q4(C, T, ds, Real(0.45), Real(1e-6), ql, !(d.flags & 1), gin, oin, amb, camb_all, ccert,
+                    F32 ? nullptr : rpool);
+    if constexpr (!F32) __syncthreads();   // the refine pool's LDS becomes the GJK job pool
 #ifdef ADRP_OBS_PHASES
     RACE_MARK(o1);
 #endif

@@ -16,11 +16,12 @@ returns the device tensors untouched (for torch-native learners).  When
 stable_baselines3 is importable the class derives from its ``VecEnv`` so
 ``isinstance`` checks in SB3 pass; otherwise it is a plain class with the same methods.
 
-Host path (SURVEY.md §7 hard part 7).  The env writes obs / terminal obs / reward / terminated /
-truncated into ONE packed device buffer (``bind_outputs``); ``step_wait`` issues one asynchronous
-copy of it into pinned host memory and waits once; the actions go the other way through a pinned
-staging buffer (one asynchronous copy).  The terminal observations of the envs that finished are
-read from that same copy (a second, dependent round trip for them cost more than the bytes).
+Host path (SURVEY.md §7 hard part 7).  The env writes obs / reward / terminated / truncated into
+ONE packed device buffer (``bind_outputs``) and its terminal observations into a device buffer of
+their own; ``adrp_compact_rows`` then gathers the finished envs' ids and terminal rows behind the
+flags in the packed buffer, so ``step_wait`` issues one asynchronous copy of about the obs size into
+pinned host memory and waits once (the whole terminal-obs batch no longer crosses PCIe); the
+actions go the other way through a pinned staging buffer (one asynchronous copy).
 ``infos`` is a lazy sequence: a finished env's dict is made when the caller first reads it; every
 other entry is one shared read-only empty mapping (SB3 reads infos and copies the dicts it
 annotates; writing into a shared entry raises).  Returned
@@ -32,6 +33,8 @@ from collections.abc import Sequence
 
 import numpy as np
 import torch
+
+from . import _lib
 
 _NO_INFO = types.MappingProxyType({})
 
@@ -94,21 +97,36 @@ class AviaryVecEnv(_VecEnvBase):
             _VecEnvBase.__init__(self, self.num_envs, self.observation_space, self.action_space)
 
     def _bind_packed(self, ring):
-        """[obs | terminal obs | reward | terminated | truncated] in one device buffer the env writes
-        into (bind_outputs), so a step's outputs reach the host in ONE asynchronous copy and one wait
-        (the terminal rows of the envs that finished are read from it; no second round trip)"""
+        """[obs | reward | terminated | truncated | done count | done env ids | terminal rows] in one
+        device buffer: the env writes the first four into it (bind_outputs) and its terminal
+        observations into a separate device buffer; after the step, adrp_compact_rows gathers the
+        finished envs' ids and terminal rows behind the flags, so a step's outputs reach the host in
+        ONE asynchronous copy of about the obs size and one wait (not the whole terminal-obs batch)"""
         env, E = self.env, self.num_envs
         obs_shape = tuple(env._obs.shape)
         dev = env._obs.device
-        nobs = int(np.prod(obs_shape)) * 4
-        self._off = (2 * nobs, 2 * nobs + 4 * E, 2 * nobs + 5 * E)
-        self._nbytes = (2 * nobs + 6 * E + 15) // 16 * 16
+        rf = int(np.prod(obs_shape[1:]))
+        nobs = E * rf * 4
+        self._rf = rf
+        self._cap = min(E, max(64, E // 32))   # terminal rows carried by the copy (more: a second copy)
+        a16 = lambda x: (x + 15) // 16 * 16   # noqa: E731
+        o_rew, o_term, o_trunc = nobs, nobs + 4 * E, nobs + 5 * E
+        o_cnt = a16(nobs + 6 * E)
+        o_idx = o_cnt + 16
+        o_rows = a16(o_idx + 4 * E)
+        self._nbytes = a16(o_rows + 4 * rf * self._cap)
         self._dev = torch.zeros(self._nbytes, dtype=torch.uint8, device=dev)
-        o_rew, o_term, o_trunc = self._off
+        self._tobs_dev = torch.zeros(obs_shape, dtype=torch.float32, device=dev)
         d = self._dev
         env.bind_outputs(d[:nobs].view(torch.float32).view(obs_shape), d[o_rew:o_term].view(torch.float32),
                          d[o_term:o_trunc].view(torch.bool), d[o_trunc:o_trunc + E].view(torch.bool),
-                         tobs=d[nobs:2 * nobs].view(torch.float32).view(obs_shape))
+                         tobs=self._tobs_dev)
+        base = d.data_ptr()
+        self._offs = (o_term, o_trunc, o_cnt, o_idx, o_rows)
+        lib = _lib.load() if dev.type == "cuda" else None
+        self._compact = getattr(lib, "adrp_compact_rows", None)
+        self._compact_args = (base + o_term, base + o_trunc, self._tobs_dev.data_ptr(), E, rf, self._cap,
+                              base + o_cnt, base + o_idx, base + o_rows)
         pin = dev.type == "cuda"
         self._host = [torch.zeros(self._nbytes, dtype=torch.uint8, pin_memory=pin) for _ in range(ring)]
         self._slot = 0
@@ -117,7 +135,8 @@ class AviaryVecEnv(_VecEnvBase):
             hn = h.numpy()
             self._views.append((hn[:nobs].view(np.float32).reshape(obs_shape), hn[o_rew:o_term].view(np.float32),
                                 hn[o_term:o_trunc].view(np.bool_), hn[o_trunc:o_trunc + E].view(np.bool_),
-                                hn[nobs:2 * nobs].view(np.float32).reshape(obs_shape)))
+                                hn[o_cnt:o_cnt + 4].view(np.int32), hn[o_idx:o_idx + 4 * E].view(np.int32),
+                                hn[o_rows:o_rows + 4 * rf * self._cap].view(np.float32).reshape((self._cap,) + obs_shape[1:])))
         act_shape = tuple(getattr(env, "_act_shape", (E,) + tuple(self.action_space.shape)))
         self._act_host = torch.zeros(act_shape, dtype=torch.float32, pin_memory=pin)
         self._act_dev = torch.zeros(act_shape, dtype=torch.float32, device=dev)
@@ -163,13 +182,38 @@ class AviaryVecEnv(_VecEnvBase):
         self._act_dev.copy_(self._act_host, non_blocking=True)
         return self._act_dev
 
+    def _gather_terminal(self):
+        """the finished envs' ids and terminal rows into the packed buffer (stream-ordered after the
+        step); a build without adrp_compact_rows (CPU stand-ins, old libraries) gathers with torch"""
+        if self._compact is not None and self._dev.is_cuda:
+            rc = self._compact(*self._compact_args, _lib._raw_stream(self._dev.device.index))
+            if rc != 0:
+                raise _lib.AdrpError(f"adrp_compact_rows: {_lib.load().adrp_last_error(None).decode()}")
+            return
+        E, rf, cap, d = self.num_envs, self._rf, self._cap, self._dev
+        o_term, o_trunc, o_cnt, o_idx, o_rows = self._offs
+        ids = torch.nonzero(d[o_term:o_term + E].bool() | d[o_trunc:o_trunc + E].bool()).flatten().to(torch.int32)
+        n = int(ids.numel())
+        d[o_cnt:o_cnt + 4].view(torch.int32)[0] = n
+        d[o_idx:o_idx + 4 * E].view(torch.int32)[:n] = ids
+        m = min(n, cap)
+        rows = d[o_rows:o_rows + 4 * rf * cap].view(torch.float32).view(cap, rf)
+        rows[:m] = self._tobs_dev.reshape(E, rf)[ids[:m].long()]
+
     def _step_wait_packed(self):
         self.env.step(self._act_in(self._actions))
-        obs, rew, term, trunc, tobs_all = self._copy_out()
+        self._gather_terminal()
+        obs, rew, term, trunc, cnt, idx_all, rows = self._copy_out()
+        n = int(cnt[0])
+        idx = idx_all[:n].copy()
+        if n <= self._cap:
+            tobs = rows[:n].copy()
+        else:   # more finished envs than the copy carries: the rest by a second (rare) copy
+            rest = torch.as_tensor(idx[self._cap:], dtype=torch.long, device=self._tobs_dev.device)
+            tobs = np.concatenate([rows.copy(), self._tobs_dev[rest].cpu().numpy()])
         done = term | trunc
-        idx = np.flatnonzero(done)
-        # terminal rows copied out of the (reused) pinned slot now; their dicts are built on demand
-        infos = _StepInfos(self.num_envs, idx, tobs_all[idx], (trunc & ~term)[idx])
+        # the dicts are built on demand from the copied terminal rows
+        infos = _StepInfos(self.num_envs, idx, tobs, (trunc & ~term)[idx])
         if not self.zero_copy:
             obs, rew = obs.copy(), rew.copy()
         return obs, rew, done, infos

@@ -337,6 +337,16 @@ int adrp_gae(const float* rewards, const float* values, const float* episode_sta
              const float* dones, int n_steps, int n_envs, double gamma, double gae_lambda, float* advantages,
              float* returns, void* stream);
 
+/* SB3 VecEnv host path: the terminal observations of the finished envs, compacted on the device
+ * behind the step's packed outputs so ONE device -> host copy returns them (replaces the per-env
+ * infos[e]["terminal_observation"] = obs that stable_baselines3 DummyVecEnv.step_wait fills from
+ * its sub-envs, vec_env/dummy_vec_env.py, 2.3.2).  term / trunc [n] uint8, rows [n][row_floats]
+ * (the env's terminal-obs buffer); writes count[0] = number of envs with term | trunc, idx[j] = the
+ * j-th such env (ascending, j < count, so idx holds up to n entries) and out_rows[j] = rows[idx[j]]
+ * for j < min(count, cap).  One workgroup; stream-ordered after the step. */
+int adrp_compact_rows(const uint8_t* term, const uint8_t* trunc, const float* rows, int n, int row_floats,
+                      int cap, int32_t* count, int32_t* idx, float* out_rows, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Parity mode noise (MultiRaceAviary).  The reference draws, per sub-step, the disturbance force
  * of every drone (np_random.<distrib>(low, high), MultiRaceAviary.py:532-537) and then the (N, 4)
@@ -378,6 +388,8 @@ int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_d
 #define ADRP_MATH_DIVC 18          /* in[i] / in[n + i] by the fp64 kernels' constant-divisor form */
 #define ADRP_MATH_SIN_FAST 19      /* octant-reduced sin / cos (gate yaws, reset attitudes) */
 #define ADRP_MATH_COS_FAST 20
+#define ADRP_MATH_EXP_TAB 21       /* exp(x), x <= 0, table form of the fp64 race downwash */
+#define ADRP_MATH_ATAN2_NC 22      /* atan2(in[i], in[n + i]) for finite operands (race Euler angles) */
 int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream);
 
 #ifdef __cplusplus

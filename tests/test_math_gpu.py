@@ -99,6 +99,27 @@ def test_exp():
     assert got[-1] == 0.0
 
 
+def test_exp_table_form():
+    """the race downwash's exp (2^(j/32) table + degree-6 Taylor on |r| <= ln2/64): the same 4-ulp bar
+    as exp() on x <= 0, underflow to 0 below the clamp"""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([-np.linspace(0, 40, 200001), -rng.exponential(3.0, 200000), [-700.0, -745.5, -1e4, -0.0]])
+    got = probe(abi.MATH_EXP_TAB, x)
+    ref = np.exp(x.astype(L))
+    ok = ref > L(1e-300)
+    assert rel_err(got[ok], ref[ok]).max() < ULP4
+    assert got[-2] == 0.0 and got[-1] == 1.0
+
+
+def test_atan2_finite_form_matches():
+    """the race Euler angles' atan2 without the non-finite fix-ups: bit-identical to atan2 on finite
+    operands (zeros included)"""
+    rng = np.random.default_rng(6)
+    y = np.concatenate([rng.normal(size=200000) * 10.0 ** rng.uniform(-3, 3, 200000), [0.0, 1.0, -1.0, 0.0, -0.0]])
+    x = np.concatenate([rng.normal(size=200000) * 10.0 ** rng.uniform(-3, 3, 200000), [1.0, 0.0, 0.0, 0.0, -1.0]])
+    np.testing.assert_array_equal(probe(abi.MATH_ATAN2_NC, y, x), probe(abi.MATH_ATAN2, y, x))
+
+
 def test_non_finite_inputs():
     """NaN in -> NaN out for atan2 (fmax / fmin drop a NaN), sqrt(+inf) = +inf"""
     nan, inf = np.nan, np.inf

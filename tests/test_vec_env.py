@@ -155,3 +155,31 @@ def test_packed_host_path_matches_legacy(kind):
             if x1 is not None:
                 np.testing.assert_array_equal(x1, x2)
     assert ndone > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rf,cap,p", [(4096, 72, 128, 0.004), (5000, 196, 64, 0.3), (1, 5, 1, 1.0), (3000, 7, 0, 0.5)])
+def test_compact_rows_kernel(n, rf, cap, p):
+    """adrp_compact_rows: count, ascending ids of term | trunc envs (several 1024-env chunks, more
+    done envs than cap rows) and their rows, against torch"""
+    import ctypes
+    from gym_pybullet_adrp_amd import _lib
+    g = torch.Generator().manual_seed(n)
+    term = (torch.rand(n, generator=g) < p / 2).to(torch.uint8).cuda()
+    trunc = (torch.rand(n, generator=g) < p / 2).to(torch.uint8).cuda()
+    rows = torch.randn(n, rf, generator=g).cuda()
+    cnt = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    idx = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    out = torch.zeros(max(cap, 1), rf, device="cuda")
+    V = ctypes.c_void_p
+    rc = _lib.load().adrp_compact_rows(V(term.data_ptr()), V(trunc.data_ptr()), V(rows.data_ptr()), n, rf, cap,
+                                       V(cnt.data_ptr()), V(idx.data_ptr()), V(out.data_ptr()),
+                                       V(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = torch.nonzero((term | trunc).bool()).flatten()
+    k = int(cnt.item())
+    assert k == ref.numel()
+    assert torch.equal(idx[:k].long().cpu(), ref.cpu())
+    m = min(k, cap)
+    assert torch.equal(out[:m].cpu(), rows[ref[:m]].cpu())

@@ -80,5 +80,18 @@ r["copy_out_us"] = per_call(lambda: v._copy_out(), 300)
 o = v._views[0][0]
 r["obs_numpy_copy_us"] = per_call(lambda: o.copy(), 300)
 out["E4096_vecenv_fp64"] = r
+if os.environ.get("HOST_PATH_PROFILE"):
+    import cProfile
+    import io
+    import pstats
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(300):
+        vstep()
+    torch.cuda.synchronize()
+    pr.disable()
+    sio = io.StringIO()
+    pstats.Stats(pr, stream=sio).sort_stats("tottime").print_stats(18)
+    print(sio.getvalue(), file=sys.stderr, flush=True)
 v.close()
 print(json.dumps(out), flush=True)

@@ -16,7 +16,7 @@ constexpr int kIters = 256;
         const uint64_t t0 = __builtin_amdgcn_s_memtime();                                            \
         _Pragma("unroll 16") for (int i = 0; i < kIters; ++i) { STEP(x); }                           \
         const uint64_t t1 = __builtin_amdgcn_s_memtime();                                            \
-        out[blockIdx.x * 64 + threadIdx.x] = x;                                                      \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = x;                                                      \
         if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;                                             \
     }                                                                                                \
     __global__ void NAME##_ind(T* out, uint64_t* cyc, T seed) {                                      \
@@ -26,7 +26,7 @@ constexpr int kIters = 256;
         const uint64_t t0 = __builtin_amdgcn_s_memtime();                                            \
         _Pragma("unroll 4") for (int i = 0; i < kIters / 4; ++i) { STEP(x); STEP(y); STEP(z); STEP(w); } \
         const uint64_t t1 = __builtin_amdgcn_s_memtime();                                            \
-        out[blockIdx.x * 64 + threadIdx.x] = x + y + z + w;                                          \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = x + y + z + w;                                          \
         if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;                                             \
     }
 
@@ -41,6 +41,9 @@ constexpr int kIters = 256;
 #define DIV32_STEP(x) x = b / x
 #define DIV64_STEP(x) x = b / x
 #define CVT_STEP(x) x = double(float(x)) * a
+// an SGPR constant materialised next to each FMA (the fp64 kernels' 64-bit literals)
+#define SMOV_STEP(x) do { int lo_, hi_; asm volatile("s_mov_b32 %0, 0x3ff00001" : "=s"(lo_)); \
+    asm volatile("s_mov_b32 %0, 0x3ff00000" : "=s"(hi_)); x = __builtin_fma(x, __hiloint2double(hi_, lo_), b); } while (0)
 
 CHAIN(fma64, double, 0, FMA_STEP)
 CHAIN(fma32, float, 0, FMAF_STEP)
@@ -53,25 +56,29 @@ CHAIN(dpp32, float, 0, DPP_STEP)
 CHAIN(div32, float, 0, DIV32_STEP)
 CHAIN(div64, double, 0, DIV64_STEP)
 CHAIN(cvt64, double, 0, CVT_STEP)
+CHAIN(smov64, double, 0, SMOV_STEP)
 
 template <typename T>
-static void run(const char* name, void (*dep)(T*, uint64_t*, T), void (*ind)(T*, uint64_t*, T), T seed) {
+static void run(const char* name, void (*dep)(T*, uint64_t*, T), void (*ind)(T*, uint64_t*, T), T seed,
+                int waves_per_block = 1) {
     const int blocks = 1024;
     T* out;
     uint64_t* cyc;
-    hipMalloc(&out, blocks * 64 * sizeof(T));
+    hipMalloc(&out, blocks * 64 * waves_per_block * sizeof(T));
     hipMalloc(&cyc, blocks * sizeof(uint64_t));
     uint64_t h[blocks];
     double r[2];
     for (int m = 0; m < 2; ++m) {
-        for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(m ? ind : dep, dim3(blocks), dim3(64), 0, 0, out, cyc, seed);
+        for (int rep = 0; rep < 3; ++rep)
+            hipLaunchKernelGGL(m ? ind : dep, dim3(blocks), dim3(64 * waves_per_block), 0, 0, out, cyc, seed);
         hipDeviceSynchronize();
         hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
         double s = 0;
         for (int i = 0; i < blocks; ++i) s += double(h[i]);
         r[m] = s / blocks / kIters;
     }
-    printf("{\"op\": \"%s\", \"dep_cycles_per_op\": %.2f, \"indep4_cycles_per_op\": %.2f}\n", name, r[0], r[1]);
+    printf("{\"op\": \"%s\", \"waves_per_block\": %d, \"dep_cycles_per_op\": %.2f, \"indep4_cycles_per_op\": %.2f}\n",
+           name, waves_per_block, r[0], r[1]);
     hipFree(out);
     hipFree(cyc);
 }
@@ -88,5 +95,12 @@ int main() {
     run<float>("ieee_div_f32", div32_dep, div32_ind, 1.0001f);
     run<double>("ieee_div_f64", div64_dep, div64_ind, 1.0001);
     run<double>("cvt_f32_f64+mul", cvt64_dep, cvt64_ind, 1.0001);
+    run<double>("2x s_mov_b32+v_fma_f64", smov64_dep, smov64_ind, 1.0001);
+    // several waves per SIMD: cycles per op of each wave (throughput per SIMD = waves / this)
+    run<double>("v_fma_f64", fma64_dep, fma64_ind, 1.0001, 4);
+    run<double>("v_fma_f64", fma64_dep, fma64_ind, 1.0001, 8);
+    run<float>("v_fma_f32", fma32_dep, fma32_ind, 1.0001f, 4);
+    run<float>("v_fma_f32", fma32_dep, fma32_ind, 1.0001f, 8);
+    run<double>("2x s_mov_b32+v_fma_f64", smov64_dep, smov64_ind, 1.0001, 8);
     return 0;
 }

@@ -2,6 +2,7 @@
 
 usage: python tools/pmc_summary.py OUT.json KEY FETCH_DIR WRITE_DIR [KEY FETCH_DIR WRITE_DIR ...]
        python tools/pmc_summary.py --valu OUT.json KEY FLOPS_DIR BUSY_DIR [...]
+       python tools/pmc_summary.py --alg OUT.json KEY FLOPS_DIR DRONES_PER_LAUNCH [...]
 
 --valu: the VALU roofline of a step kernel from two passes, FLOPS_DIR =
 SQ_INSTS_VALU_FLOPS_FP32, SQ_INSTS_VALU_FLOPS_FP32_TRANS, SQ_INSTS_VALU_FLOPS_FP64, SQ_INSTS_VALU and
@@ -84,7 +85,33 @@ def calib(out_path, fdir, wdir, bytes_per_launch):
     json.dump(rec, open(out_path, "w"), indent=1)
 
 
+def alg(out_path, rest):
+    """--alg OUT.json KEY FLOPS_DIR DRONES_PER_LAUNCH [...]: the flop model of a race workload from a
+    FLOPS pass of the one-lane fp32 kernel (ADRP_RACE_QUAD=0: one lane per drone, no redundant
+    lanes): algorithmic_flops_per_drone_step = its FLOPS counters x 64 / drones per launch, kept on
+    KEY (and on its fp64 twin) beside the four-lane kernel's executed counters"""
+    try:
+        rec = json.load(open(out_path))
+    except (OSError, ValueError):
+        rec = {}
+    for i in range(0, len(rest), 3):
+        key, fdir, drones = rest[i], rest[i + 1], int(rest[i + 2])
+        c = {n: counter(fdir, n, "race_step_kernel")[0] for n in (
+            "SQ_INSTS_VALU_FLOPS_FP32", "SQ_INSTS_VALU_FLOPS_FP32_TRANS", "SQ_INSTS_VALU_FLOPS_FP64")}
+        per = 64 * sum(c.values()) / drones
+        for k in (key, key.replace("_fp32_", "_fp64_")):
+            rec.setdefault(k, {})
+            rec[k]["algorithmic_flops_per_drone_step"] = per
+            rec[k]["algorithmic_source"] = ("SQ_INSTS_VALU_FLOPS_* of the one-lane race_step_kernel (one lane per "
+                                            "drone, no redundant lanes; ADRP_RACE_QUAD=0) on the same workload, fp32, "
+                                            "tools/pmc_r4.sh; the same algorithm in either precision")
+        print(key, per)
+    json.dump(rec, open(out_path, "w"), indent=1)
+
+
 def main():
+    if sys.argv[1] == "--alg":
+        return alg(sys.argv[2], sys.argv[3:])
     if sys.argv[1] == "--valu":
         return valu(sys.argv[2], sys.argv[3:])
     if sys.argv[1] == "--calib":
