@@ -44,16 +44,21 @@ class _StepInfos(Sequence):
     that finished get their own dict ({"terminal_observation", "TimeLimit.truncated"}) when first
     read, then the same (mutable) dict on every read; every other entry is the shared read-only
     empty mapping.  A step with hundreds of finished envs no longer builds hundreds of dicts that
-    the caller may never look at."""
-    __slots__ = ("_n", "_row", "_tobs", "_tl", "_made")
+    the caller may never look at; iteration walks the (ascending) finished ids alongside."""
+    __slots__ = ("_n", "_idx", "_row", "_tobs", "_tl", "_made")
 
     def __init__(self, n, idx, tobs, tl):
-        self._n = n
-        self._row = dict(zip(idx.tolist(), range(len(idx))))
+        self._n, self._idx, self._row = n, idx, None
         self._tobs, self._tl, self._made = tobs, tl, {}
 
     def __len__(self):
         return self._n
+
+    def _info(self, e, j):
+        d = self._made.get(e)
+        if d is None:
+            d = self._made[e] = {"terminal_observation": self._tobs[j], "TimeLimit.truncated": bool(self._tl[j])}
+        return d
 
     def __getitem__(self, e):
         if isinstance(e, slice):
@@ -62,13 +67,21 @@ class _StepInfos(Sequence):
             e += self._n
         if not 0 <= e < self._n:
             raise IndexError(e)
+        if self._row is None:
+            self._row = dict(zip(self._idx.tolist(), range(len(self._idx))))
         j = self._row.get(e)
-        if j is None:
-            return _NO_INFO
-        d = self._made.get(e)
-        if d is None:
-            d = self._made[e] = {"terminal_observation": self._tobs[j], "TimeLimit.truncated": bool(self._tl[j])}
-        return d
+        return _NO_INFO if j is None else self._info(e, j)
+
+    def __iter__(self):
+        ids = self._idx.tolist()
+        j, nxt = 0, (ids[0] if ids else -1)
+        for e in range(self._n):
+            if e == nxt:
+                yield self._info(e, j)
+                j += 1
+                nxt = ids[j] if j < len(ids) else -1
+            else:
+                yield _NO_INFO
 
 try:  # pragma: no cover - SB3 is not part of this image
     from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _VecEnvBase
@@ -79,7 +92,7 @@ except ImportError:  # pragma: no cover
 class AviaryVecEnv(_VecEnvBase):
     """SB3 VecEnv over one batched aviary (HoverAviary / MultiRaceAviary of this package)."""
 
-    def __init__(self, env, as_torch=False, zero_copy=False, ring=2, packed=None):
+    def __init__(self, env, as_torch=False, zero_copy=False, ring=2, packed=None, terminal_rows=None):
         self.env = env
         self.num_envs = env.num_envs
         self.observation_space = env.observation_space
@@ -91,6 +104,8 @@ class AviaryVecEnv(_VecEnvBase):
         self._seed = None
         # packed host path: numpy outputs of an env that can write into caller buffers (None: auto)
         self._packed = (not as_torch) and hasattr(env, "bind_outputs") and packed is not False
+        if terminal_rows is not None:   # initial terminal-row capacity of the packed copy (it grows)
+            self._cap_req = max(1, min(self.num_envs, int(terminal_rows)))
         if self._packed:
             self._bind_packed(max(1, int(ring)))
         if _VecEnvBase is not object:  # pragma: no cover
@@ -108,15 +123,20 @@ class AviaryVecEnv(_VecEnvBase):
         rf = int(np.prod(obs_shape[1:]))
         nobs = E * rf * 4
         self._rf = rf
-        self._cap = min(E, max(64, E // 32))   # terminal rows carried by the copy (more: a second copy)
+        # terminal rows the copy carries (more: a second copy that step, and the region grows)
+        self._cap = getattr(self, "_cap_req", min(E, max(64, E // 16)))
         a16 = lambda x: (x + 15) // 16 * 16   # noqa: E731
         o_rew, o_term, o_trunc = nobs, nobs + 4 * E, nobs + 5 * E
         o_cnt = a16(nobs + 6 * E)
         o_idx = o_cnt + 16
         o_rows = a16(o_idx + 4 * E)
         self._nbytes = a16(o_rows + 4 * rf * self._cap)
+        old = getattr(self, "_dev", None), getattr(self, "_tobs_dev", None)
         self._dev = torch.zeros(self._nbytes, dtype=torch.uint8, device=dev)
         self._tobs_dev = torch.zeros(obs_shape, dtype=torch.float32, device=dev)
+        if old[0] is not None:   # a re-bind (larger terminal-row region): the current outputs move over
+            self._dev[:o_cnt].copy_(old[0][:o_cnt])
+            self._tobs_dev.copy_(old[1])
         d = self._dev
         env.bind_outputs(d[:nobs].view(torch.float32).view(obs_shape), d[o_rew:o_term].view(torch.float32),
                          d[o_term:o_trunc].view(torch.bool), d[o_trunc:o_trunc + E].view(torch.bool),
@@ -139,6 +159,7 @@ class AviaryVecEnv(_VecEnvBase):
                                 hn[o_rows:o_rows + 4 * rf * self._cap].view(np.float32).reshape((self._cap,) + obs_shape[1:])))
         act_shape = tuple(getattr(env, "_act_shape", (E,) + tuple(self.action_space.shape)))
         self._act_host = torch.zeros(act_shape, dtype=torch.float32, pin_memory=pin)
+        self._act_np = self._act_host.numpy()
         self._act_dev = torch.zeros(act_shape, dtype=torch.float32, device=dev)
         # the copies and the step run on the env device's current stream, which need not be the current
         # device's: the event is created on and recorded into that stream
@@ -178,7 +199,7 @@ class AviaryVecEnv(_VecEnvBase):
         """numpy / host actions -> the persistent device action buffer through pinned staging"""
         if isinstance(actions, torch.Tensor) and actions.device == self._act_dev.device:
             return actions
-        self._act_host.numpy()[...] = np.asarray(actions, np.float32).reshape(self._act_host.shape)
+        self._act_np[...] = np.asarray(actions, np.float32).reshape(self._act_np.shape)
         self._act_dev.copy_(self._act_host, non_blocking=True)
         return self._act_dev
 
@@ -208,9 +229,12 @@ class AviaryVecEnv(_VecEnvBase):
         idx = idx_all[:n].copy()
         if n <= self._cap:
             tobs = rows[:n].copy()
-        else:   # more finished envs than the copy carries: the rest by a second (rare) copy
+        else:   # more finished envs than the copy carries: the rest by a second copy, and a larger
+            # terminal-row region from the next step on (the outputs are re-bound; the env state stays)
             rest = torch.as_tensor(idx[self._cap:], dtype=torch.long, device=self._tobs_dev.device)
             tobs = np.concatenate([rows.copy(), self._tobs_dev[rest].cpu().numpy()])
+            self._cap_req = min(self.num_envs, max(2 * self._cap, n + n // 4))
+            self._bind_packed(len(self._host))
         done = term | trunc
         # the dicts are built on demand from the copied terminal rows
         infos = _StepInfos(self.num_envs, idx, tobs, (trunc & ~term)[idx])

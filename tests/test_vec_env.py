@@ -127,7 +127,8 @@ def test_packed_host_path_matches_legacy(kind):
             v = HoverAviaryVec(n_envs=256, seed=3, initial_xyzs=[0, 0, 1.0], init_noise={"rpy": 0.3, "omega": 1.0})
         else:
             v = MultiRaceAviaryVec(n_envs=128, race_config="level3", num_drones=4, seed=3)
-        v = type(v)(v.env, packed=packed)
+        # packed: start with 2 terminal rows, so steps with more finished envs take the second copy
+        v = type(v)(v.env, packed=packed, terminal_rows=2 if packed else None)
         assert v._packed == packed
         obs = v.reset()
         rng = np.random.default_rng(0)
@@ -142,6 +143,8 @@ def test_packed_host_path_matches_legacy(kind):
             seq.append((obs.copy(), rew.copy(), done.copy(),
                         [(bool(i.get("TimeLimit.truncated")), i.get("terminal_observation")) for i in infos]))
         outs.append(seq)
+        if packed:
+            assert v._cap > 2   # more finished envs than terminal rows in some step: grown
         v.close()
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     ndone = 0
@@ -183,3 +186,18 @@ def test_compact_rows_kernel(n, rf, cap, p):
     assert torch.equal(idx[:k].long().cpu(), ref.cpu())
     m = min(k, cap)
     assert torch.equal(out[:m].cpu(), rows[ref[:m]].cpu())
+
+
+def test_step_infos_iteration_matches_indexing():
+    """_StepInfos: iterating (what SB3's info-buffer update does over all envs) yields what indexing
+    does, the same dict objects for finished envs and the shared empty mapping for the rest"""
+    from gym_pybullet_adrp_amd.vec_env import _StepInfos
+    idx = np.array([0, 3, 4, 9])
+    tobs = np.arange(4 * 2, dtype=np.float32).reshape(4, 2)
+    infos = _StepInfos(10, idx, tobs, np.array([True, False, True, False]))
+    it = list(infos)
+    assert len(it) == 10 and all(a is b for a, b in zip(it, [infos[i] for i in range(10)]))
+    assert it[3]["TimeLimit.truncated"] is False and it[4]["TimeLimit.truncated"] is True
+    np.testing.assert_array_equal(it[9]["terminal_observation"], [6.0, 7.0])
+    assert it[1] == {} and infos[-1] is it[9] and len(infos[2:5]) == 3
+    assert list(_StepInfos(3, np.array([], dtype=np.int64), tobs[:0], np.array([], bool))) == [{}, {}, {}]
