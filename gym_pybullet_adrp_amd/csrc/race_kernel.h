@@ -293,9 +293,12 @@ __device__ __forceinline__ V3<Real> tri_closest(V3<Real> a, V3<Real> b, V3<Real>
 // registers (no dynamic indexing -> no scratch). Every iterate v is a point of the
 // Minkowski difference, so |v| >= distance, and v.w / |v| <= distance for the support point
 // w: the loop stops as soon as either bound decides against `cut`, else on convergence.
+// v0 (optional): the first search direction, a point of A - B (e.g. A's centre minus B's point
+// closest to it, gjk_seed): near a long part it starts the iteration next to the closest features
+// instead of along the centre difference
 template <typename Real>
 __device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
-                                                bool* undecided = nullptr) {
+                                                bool* undecided = nullptr, const V3<Real>* v0 = nullptr) {
     // in A's centre frame: support points stay O(shape size), so the fp32 termination test
     // is not swamped by rounding of world coordinates (which stalled convergence)
     Shape<Real> A = A0, B = B0;
@@ -306,6 +309,7 @@ __device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Sha
     V3<Real> W0, W1, W2, W3;
     int n = 0;
     V3<Real> v = A.c - B.c;
+    if (v0 != nullptr) v = *v0;
     const Real cut2 = cut * cut;
     if (dot(v, v) < Real(1e-20)) v = v3(Real(1), Real(0), Real(0));
     Real vv_prev = Real(3.0e38);
@@ -431,16 +435,17 @@ __device__ __noinline__ bool gjk_within_f64_call(Shape<double> A, Shape<double> 
 }
 
 template <typename Real>
-__device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Real>& B0, Real cut) {
+__device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
+                                           const V3<Real>* v0 = nullptr) {
     if constexpr (sizeof(Real) == 4) {
         if (cut < Real(1e-3)) {
             bool undecided = false;
-            const bool r = gjk_within_impl<Real>(A0, B0, cut, &undecided);
+            const bool r = gjk_within_impl<Real>(A0, B0, cut, &undecided, v0);
             if (__builtin_expect(!undecided, 1)) return r;
             return gjk_within_f64_call(shape_f64(A0), shape_f64(B0), double(cut));
         }
     }
-    return gjk_within_impl<Real>(A0, B0, cut);
+    return gjk_within_impl<Real>(A0, B0, cut, nullptr, v0);
 }
 
 // entry fraction of the segment p0 -> p1 into a cylinder, > 1 on a miss
@@ -1048,6 +1053,14 @@ __device__ __forceinline__ V3<Real> part_closest(V3<Real> x, V3<Real> h, Real r,
     return v3(clampr_(x.x, -h.x, h.x), clampr_(x.y, -h.y, h.y), clampr_(x.z, -h.z, h.z));
 }
 
+// GJK seed for a (drone, part) query: the drone's centre minus the part point closest to it (world
+// frame), a point of drone - part
+template <typename Real>
+__device__ __forceinline__ V3<Real> gjk_seed(const Shape<Real>& drone, const Shape<Real>& part) {
+    const V3<Real> x = mulT(part.R, drone.c - part.c);
+    return mul(part.R, x - part_closest(x, part.h, part.r, part.cyl));
+}
+
 // Support-function bounds of one (drone cylinder, part) pair in the part's frame: lp = the centre of
 // the drone's collision cylinder, ax = its axis (unit), dr / dhh = its radius / half height.  With q
 // the part point closest to lp and n = (q - lp) / |q - lp|, the (convex) part lies beyond the plane
@@ -1293,7 +1306,12 @@ __device__ __forceinline__ bool track_gjk_pool(const RaceConst<Real>& C, const T
         dl.R.a22 = shfl_(ds.R.a22, L, kRaceBlock);
         if (j < total) {
             const Shape<Real> s = track_part_shape(C, T.lane(L, G, N, E), b);
+#ifdef ADRP_GJK_NOSEED
             if (gjk_within(dl, s, fc ? ccut : cut)) {
+#else
+            const V3<Real> v0 = gjk_seed(dl, s);
+            if (gjk_within(dl, s, fc ? ccut : cut, &v0)) {
+#endif
                 const uint32_t bit = fc ? 1u << 8
                                         : b < kObstBit0 ? 1u << (b / kGateParts)
                                                         : 1u << (4 + (b - kObstBit0) / kObstParts);
