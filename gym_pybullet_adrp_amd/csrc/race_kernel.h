@@ -1306,7 +1306,7 @@ __device__ __forceinline__ bool track_gjk_pool(const RaceConst<Real>& C, const T
         dl.R.a22 = shfl_(ds.R.a22, L, kRaceBlock);
         if (j < total) {
             const Shape<Real> s = track_part_shape(C, T.lane(L, G, N, E), b);
-#ifdef ADRP_GJK_NOSEED
+#ifndef ADRP_GJK_SEED   // (measurement switch: the warm-started form, tools/abn.sh)
             if (gjk_within(dl, s, fc ? ccut : cut)) {
 #else
             const V3<Real> v0 = gjk_seed(dl, s);
