@@ -275,31 +275,6 @@ __device__ __forceinline__ double atan2_t(double y, double x) {
 }
 __device__ __forceinline__ double atan2(double y, double x) { return atan2_t<false>(y, x); }
 __device__ __forceinline__ double atan2_nc(double y, double x) { return atan2_t<true>(y, x); }
-// atan2_nc with its 14 literals read from a constant block (k: kAtan2K, through a pointer the caller
-// makes opaque per use) by scalar loads: one s_load_dwordx16 + one x8 where the literal form issues
-// 28 s_mov_b32 on the chain of a lone wave (measurement switch ADRP_ATAN_SMEM, tools/abn.sh)
-static __device__ __constant__ double kAtan2K[16] = {
-    0.41421356237309504880, 0.021428368220326288, -0.04375458729368037, 0.05699267039194693,
-    -0.06642647883966969, 0.07690277001250925, -0.09090800003785938, 0.11111107550967636,
-    -0.14285714221246087, 0.19999999999459742, -0.3333333333333199, 0.78539816339744830962,
-    1.57079632679489661923, 3.14159265358979323846, 0.0, 0.0};
-typedef const __attribute__((address_space(4))) double* kconst_ptr;   // scalar-loadable constant memory
-__device__ __forceinline__ double atan2_k(double y, double x, kconst_ptr k) {
-    const double ax = __builtin_fabs(x), ay = __builtin_fabs(y);
-    const double mx = __builtin_fmax(ax, ay), mn = __builtin_fmin(ax, ay);
-    const bool big = mn > k[0] * mx;
-    const double num = big ? mn - mx : mn, den = big ? mn + mx : mx;
-    const double t = mx > 0.0 ? num * rcp_nc(den) : 0.0;
-    const double s = t * t;
-    double p = k[1];
-#pragma unroll
-    for (int i = 2; i <= 10; ++i) p = fma_(p, s, k[i]);
-    double r = fma_(t * s, p, t);
-    if (big) r += k[11];
-    if (ay > ax) r = k[12] - r;
-    if (x < 0.0) r = k[13] - r;
-    return __builtin_copysign(r, y);
-}
 // 2^(j/32), j = 0..31 (correctly rounded), the table of f64::exp_tab (the race kernel copies it to LDS)
 static __device__ __constant__ double kExp2Tab32[32] = {
     1.0, 1.0218971486541166, 1.0442737824274138, 1.0671404006768237, 1.0905077326652577, 1.1143867425958924,

@@ -116,13 +116,6 @@ __device__ __forceinline__ Real euler_axis_q4(Q4<Real> q, int a) {
     // fasin_(sarg); the argument is > 0 here (|sarg| < 0.99999), the operands finite
     const Real x1 = hsqrt_nn_((Real(1) - sarg) * (Real(1) + sarg));
     const Real yy = a == 0 ? y0 : (a == 1 ? sarg : y2), xx = a == 0 ? x0 : (a == 1 ? x1 : x2);
-#ifdef ADRP_ATAN_SMEM
-    if constexpr (sizeof(Real) == 8) {
-        f64::kconst_ptr k = (f64::kconst_ptr)f64::kAtan2K;
-        asm volatile("" : "+s"(k));   // a fresh (loop-variant) pointer: the block is loaded here
-        return f64::atan2_k(yy, xx, k);
-    }
-#endif
     return fatan2_nc_(yy, xx);
 }
 
