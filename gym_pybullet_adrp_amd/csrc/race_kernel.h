@@ -430,8 +430,8 @@ __device__ __forceinline__ Shape<double> shape_f64(const Shape<Real>& s) {
 // float.
 // out of line: one copy per code object for the rare rerun (inlined at the three query sites it
 // grew the fp32 kernels by ~10 % of code and made them no faster; tools/gpu_r3_t16.sh)
-__device__ __noinline__ bool gjk_within_f64_call(Shape<double> A, Shape<double> B, double cut) {
-    return gjk_within_impl<double>(A, B, cut);
+__device__ __noinline__ bool gjk_within_f64_call(Shape<double> A, Shape<double> B, double cut, V3<double> v0, bool seeded) {
+    return gjk_within_impl<double>(A, B, cut, nullptr, seeded ? &v0 : nullptr);
 }
 
 template <typename Real>
@@ -442,7 +442,8 @@ __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Re
             bool undecided = false;
             const bool r = gjk_within_impl<Real>(A0, B0, cut, &undecided, v0);
             if (__builtin_expect(!undecided, 1)) return r;
-            return gjk_within_f64_call(shape_f64(A0), shape_f64(B0), double(cut));
+            const V3<double> v0d = v0 ? v3(double(v0->x), double(v0->y), double(v0->z)) : v3(0.0, 0.0, 0.0);
+            return gjk_within_f64_call(shape_f64(A0), shape_f64(B0), double(cut), v0d, v0 != nullptr);
         }
     }
     return gjk_within_impl<Real>(A0, B0, cut, nullptr, v0);
