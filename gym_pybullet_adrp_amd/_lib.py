@@ -97,6 +97,11 @@ def load():
     if hasattr(lib, "adrp_compact_rows"):
         lib.adrp_compact_rows.argtypes = [P, P, P, I, I, I, P, P, P, P]
         lib.adrp_compact_rows.restype = I
+    if hasattr(lib, "adrp_memcpy_async"):
+        lib.adrp_memcpy_async.argtypes = [P, P, ctypes.c_size_t, I, P]
+        lib.adrp_memcpy_async.restype = I
+        lib.adrp_stream_synchronize.argtypes = [P]
+        lib.adrp_stream_synchronize.restype = I
     if hasattr(lib, "adrp_math_probe"):      # (A/B runs may load an older build without it)
         lib.adrp_math_probe.argtypes = [I, P, P, I, P]
         lib.adrp_math_probe.restype = I

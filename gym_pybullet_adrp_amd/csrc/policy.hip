@@ -350,3 +350,18 @@ extern "C" int adrp_compact_rows(const uint8_t* term, const uint8_t* trunc, cons
     if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("compact launch: ") + hipGetErrorString(e));
     return ADRP_OK;
 }
+
+// the host path's copies and wait without a framework dispatch in between (vec_env.py): kind 1 =
+// host -> device, 2 = device -> host (pinned host memory: asynchronous on the stream)
+extern "C" int adrp_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream) {
+    if (!dst || !src || (kind != 1 && kind != 2)) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_memcpy_async: arguments");
+    const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost,
+                                        (hipStream_t)stream);
+    if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("memcpy: ") + hipGetErrorString(e));
+    return ADRP_OK;
+}
+extern "C" int adrp_stream_synchronize(void* stream) {
+    const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("stream sync: ") + hipGetErrorString(e));
+    return ADRP_OK;
+}

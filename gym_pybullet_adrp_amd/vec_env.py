@@ -145,6 +145,8 @@ class AviaryVecEnv(_VecEnvBase):
         self._offs = (o_term, o_trunc, o_cnt, o_idx, o_rows)
         lib = _lib.load() if dev.type == "cuda" else None
         self._compact = getattr(lib, "adrp_compact_rows", None)
+        # raw stream-ordered copies + one stream wait (no framework dispatch per copy) when the library has them
+        self._raw = lib if getattr(lib, "adrp_memcpy_async", None) is not None else None
         self._compact_args = (base + o_term, base + o_trunc, self._tobs_dev.data_ptr(), E, rf, self._cap,
                               base + o_cnt, base + o_idx, base + o_rows)
         pin = dev.type == "cuda"
@@ -186,9 +188,15 @@ class AviaryVecEnv(_VecEnvBase):
         self._actions = actions
 
     def _copy_out(self):
-        """one async device -> pinned copy of the packed outputs, one wait"""
+        """one async device -> pinned copy of the packed outputs, one wait (on the env device's stream)"""
         self._slot = (self._slot + 1) % len(self._host)
         h = self._host[self._slot]
+        if self._raw is not None:
+            st = _lib._raw_stream(self._dev.device.index)
+            if self._raw.adrp_memcpy_async(h.data_ptr(), self._dev.data_ptr(), self._nbytes, 2, st) != 0 or \
+                    self._raw.adrp_stream_synchronize(st) != 0:
+                raise _lib.AdrpError(f"packed copy: {self._raw.adrp_last_error(None).decode()}")
+            return self._views[self._slot]
         h.copy_(self._dev, non_blocking=True)
         if self._event is not None:
             self._event.record(torch.cuda.current_stream(self._dev.device))
@@ -200,6 +208,11 @@ class AviaryVecEnv(_VecEnvBase):
         if isinstance(actions, torch.Tensor) and actions.device == self._act_dev.device:
             return actions
         self._act_np[...] = np.asarray(actions, np.float32).reshape(self._act_np.shape)
+        if self._raw is not None:
+            if self._raw.adrp_memcpy_async(self._act_dev.data_ptr(), self._act_host.data_ptr(), self._act_host.nbytes, 1,
+                                           _lib._raw_stream(self._act_dev.device.index)) != 0:
+                raise _lib.AdrpError(f"action copy: {self._raw.adrp_last_error(None).decode()}")
+            return self._act_dev
         self._act_dev.copy_(self._act_host, non_blocking=True)
         return self._act_dev
 

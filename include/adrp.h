@@ -30,6 +30,7 @@
 #ifndef ADRP_H
 #define ADRP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -346,6 +347,10 @@ int adrp_gae(const float* rewards, const float* values, const float* episode_sta
  * for j < min(count, cap).  One workgroup; stream-ordered after the step. */
 int adrp_compact_rows(const uint8_t* term, const uint8_t* trunc, const float* rows, int n, int row_floats,
                       int cap, int32_t* count, int32_t* idx, float* out_rows, void* stream);
+/* The same host path's copies (kind 1: host -> device, 2: device -> host; pinned host memory makes
+ * them asynchronous on the stream) and its one wait, without a framework dispatch in between. */
+int adrp_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream);
+int adrp_stream_synchronize(void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Parity mode noise (MultiRaceAviary).  The reference draws, per sub-step, the disturbance force
