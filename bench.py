@@ -245,6 +245,20 @@ def pmc_record(name, key):
     return rec.get(key)
 
 
+def pmc_record_any_envs(name, key):
+    """the flop-model record of the same race workload (level, drones, physics) at any env count"""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        rec = json.load(fh)
+    stem = "_".join(key.split("_")[:-2]) + "_"   # race_{level}_{drones}_{physics}_
+    for k in sorted(rec):
+        if k.startswith(stem) and k[len(stem):].count("_") == 1 and "algorithmic_flops_per_drone_step" in rec[k]:
+            return rec[k]
+    return None
+
+
 def hover_make(precision, physics, dev, **kw):
     from gym_pybullet_adrp_amd.envs.hover import HoverAviary
     from gym_pybullet_adrp_amd.utils.enums import Physics
@@ -329,12 +343,18 @@ def valu_roofline(env, step_ms, eager_ms, key, precision):
            "hbm": {"achieved_GBps": hbm["achieved"], "frac": hbm["frac"], "bytes_per_launch": hbm["bytes_per_launch"]}}
     rec.update(kt)
     alg = pmc_record("pmc_valu.json", key.replace("_fp64_", "_fp32_")) if pmc is None or "algorithmic_flops_per_drone_step" not in pmc else pmc
+    if alg is None or "algorithmic_flops_per_drone_step" not in alg:
+        # the flop model is per drone-step: the same workload at another env count carries it
+        # (config 5 strong: 32,768 envs on one GPU)
+        alg = pmc_record_any_envs("pmc_valu.json", key)
     if alg is not None and "algorithmic_flops_per_drone_step" in alg:
         per_drone = alg["algorithmic_flops_per_drone_step"]
         flops = per_drone * drones
         rec.update({"achieved": flops / avg_s / 1e12, "frac": flops / avg_s / 1e12 / peak,
                     "flops_per_launch": flops, "flops_per_drone_step": per_drone,
-                    "source": f"profiles/pmc_valu.json[{key if pmc is alg else key.replace('_fp64_', '_fp32_')}]"})
+                    "source": f"profiles/pmc_valu.json[{key if pmc is alg else key.replace('_fp64_', '_fp32_')}]"
+                              + ("" if pmc is alg or pmc_record("pmc_valu.json", key.replace("_fp64_", "_fp32_")) is alg
+                                 else " (the same workload's flop model at another env count)")})
     if pmc is not None:
         exe = pmc["flops_per_launch"]
         rec.update({"executed_flops_per_launch": exe, "executed_frac": exe / avg_s / 1e12 / peak,
