@@ -298,7 +298,8 @@ __device__ __forceinline__ V3<Real> tri_closest(V3<Real> a, V3<Real> b, V3<Real>
 // instead of along the centre difference
 template <typename Real>
 __device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
-                                                bool* undecided = nullptr, const V3<Real>* v0 = nullptr) {
+                                                bool* undecided = nullptr, const V3<Real>* v0 = nullptr,
+                                                int max_it = 48) {
     // in A's centre frame: support points stay O(shape size), so the fp32 termination test
     // is not swamped by rounding of world coordinates (which stalled convergence)
     Shape<Real> A = A0, B = B0;
@@ -313,7 +314,7 @@ __device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Sha
     const Real cut2 = cut * cut;
     if (dot(v, v) < Real(1e-20)) v = v3(Real(1), Real(0), Real(0));
     Real vv_prev = Real(3.0e38);
-    for (int it = 0; it < 48; ++it) {
+    for (int it = 0; it < max_it; ++it) {
         const V3<Real> w = support(A, Real(-1) * v) - support(B, v);
         const Real vv = dot(v, v), vw = dot(v, w);
         // cycling: the same |v| twice in a row is the same simplex again (fp32 near contact: a support
@@ -386,7 +387,7 @@ __device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Sha
         }
         if (dot(v, v) < cut2) { GJK_STAT(it + 1); return true; }   // upper bound
     }
-    GJK_STAT(48);
+    GJK_STAT(max_it);
     if (undecided) *undecided = true;
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
     {
@@ -434,13 +435,20 @@ __device__ __noinline__ bool gjk_within_f64_call(Shape<double> A, Shape<double> 
     return gjk_within_impl<double>(A, B, cut, nullptr, seeded ? &v0 : nullptr);
 }
 
+#ifndef ADRP_GJK_CAP_F32
+#define ADRP_GJK_CAP_F32 24
+#endif
+constexpr int kGjkContactCapF32 = ADRP_GJK_CAP_F32;
 template <typename Real>
 __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
                                            const V3<Real>* v0 = nullptr) {
     if constexpr (sizeof(Real) == 4) {
         if (cut < Real(1e-3)) {
+            // a float contact query still open after 24 iterations goes to the float64 rerun (which
+            // decides as the oracle does) instead of running the float iteration to 48: the actor-driven
+            // tail was one such query per few hundred launches (48 fp32 iterations + the rerun)
             bool undecided = false;
-            const bool r = gjk_within_impl<Real>(A0, B0, cut, &undecided, v0);
+            const bool r = gjk_within_impl<Real>(A0, B0, cut, &undecided, v0, kGjkContactCapF32);
             if (__builtin_expect(!undecided, 1)) return r;
             const V3<double> v0d = v0 ? v3(double(v0->x), double(v0->y), double(v0->z)) : v3(0.0, 0.0, 0.0);
             return gjk_within_f64_call(shape_f64(A0), shape_f64(B0), double(cut), v0d, v0 != nullptr);
