@@ -82,6 +82,10 @@ def parse():
     p.add_argument("--launch-check", action="store_true",
                    help="CPU-only check of the rank launch: every rank joins a gloo group, rank 0 prints the "
                         "record of the world it saw, no GPU work")
+    p.add_argument("--gather-leg", action="store_true",
+                   help="internal: run only config 5's world-1 RCCL step + all-gather record and print it "
+                        "(the parent bench runs this as a child process)")
+    p.add_argument("--gather-warmup", type=int, default=None, help="internal: --gather-leg warm-up steps")
     return p.parse_args()
 
 
@@ -183,6 +187,27 @@ def cpu_baseline(cfg, seconds, race=False):
 # ----------------------------------------------------------------------------------------------
 # GPU timing
 # ----------------------------------------------------------------------------------------------
+WATCHDOG_POLL_S = 0.25   # > ProcessGroupNCCL's watchdog sleep (100 ms): one poll retires finished works
+
+
+def quiesce_collectives():
+    """Nothing of ProcessGroupNCCL may be pending when a HIP graph capture begins.  Its watchdog
+    thread polls every issued Work with an event query; a query from another thread while a
+    GLOBAL-mode capture is open fails with hipErrorStreamCaptureUnsupported, the watchdog throws
+    and the process terminates (BENCH_r04.json, rc 134).  So: finish the device work, then give the
+    watchdog one poll to retire the (completed) works before the capture opens.  The capture itself
+    is thread-local (`capture_graph`), so a late poll is legal as well."""
+    torch.cuda.synchronize()
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        time.sleep(WATCHDOG_POLL_S)
+
+
+def capture_graph(graph):
+    """torch.cuda.graph in thread-local capture mode: only this thread's capture-unsafe calls are
+    refused, so the RCCL watchdog's event queries on its own thread stay legal during a capture"""
+    return torch.cuda.graph(graph, capture_error_mode="thread_local")
+
+
 def time_graph(stepper, acts, K, W, world, dev):
     """W eager warm-up steps, then exactly K steps replayed from captured HIP graphs, bracketed by
     barrier + synchronize; returns the max over ranks of the timed region (s) and the graph size."""
@@ -196,8 +221,9 @@ def time_graph(stepper, acts, K, W, world, dev):
     with torch.cuda.stream(side):
         stepper.step(acts[0])
     torch.cuda.current_stream(dev).wait_stream(side)
+    quiesce_collectives()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    with capture_graph(graph):
         for k in range(G):
             stepper.step(acts[k % nbuf])
     graph.replay()                                           # untimed: warms the graph
@@ -431,6 +457,45 @@ def gather_record_world1(dev, K, W, precision="fp64", E=ENVS_PER_GPU, refuse_cap
             dist.destroy_process_group()
 
 
+def gather_leg_child(K, W, timeout_s=300):
+    """config 5's world-1 RCCL step + all-gather leg in a FRESH child process (this script with
+    --gather-leg): it brings up its own RCCL communicator and HIP graph, and whatever happens to it
+    (an abort on a library thread cannot be caught in-process) the parent's record survives and
+    says what the child returned.  The parent has synchronised its device work first."""
+    torch.cuda.synchronize()
+    cmd = [sys.executable, os.path.abspath(__file__), "--gather-leg", "--race-steps", str(K),
+           "--gather-warmup", str(W)]
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT", "GROUP_RANK", "ROLE_RANK"):
+        env.pop(k, None)
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout_s, env=env)
+    except subprocess.TimeoutExpired as exc:
+        return {"child": "timeout", "timeout_s": timeout_s,
+                "stderr_tail": (exc.stderr or b"")[-1500:].decode(errors="replace") if isinstance(exc.stderr, bytes)
+                else str(exc.stderr or "")[-1500:]}
+    sys.stderr.write(p.stderr[-4000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"child": "failed", "rc": p.returncode, "stderr_tail": p.stderr[-1500:]}
+    rec = json.loads(lines[-1])
+    rec["child"] = {"rc": 0, "wall_s": round(time.perf_counter() - t0, 2),
+                    "note": "run in a fresh child process (own RCCL communicator), merged here"}
+    return rec
+
+
+def guarded(fn, *a, **kw):
+    """one sub-record: an exception in it is recorded in its place, the rest of the line survives"""
+    try:
+        return fn(*a, **kw)
+    except Exception as exc:   # noqa: BLE001 - the record says what failed
+        import traceback
+        traceback.print_exc()
+        torch.cuda.synchronize()
+        return {"error": repr(exc)[:500]}
+
+
 def bench_race(level, drones, physics, racemode, precision, E, K, W, world, rank, dev, seed,
                sharded_gather=False, policy_spec=None, graph_only=False, global_envs=None):
     """one MultiRaceAviary workload; E envs per GPU, or global_envs in total (strong scaling)"""
@@ -656,6 +721,11 @@ def main():
         sys.exit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPUs")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     torch.cuda.set_device(local)
+    if args.gather_leg:
+        W = args.gather_warmup if args.gather_warmup is not None else max(10, args.race_steps // 10)
+        rec = gather_record_world1(local, args.race_steps, W)
+        print(json.dumps(rec), file=record_out, flush=True)
+        return
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         assert dist.get_world_size() == world
@@ -697,44 +767,53 @@ def main():
         go = args.graph_only
         # config 5 at every N (at N = 1 it is BASELINE configs[3]): reference precision, then fp32;
         # `strong`: the 32,768 envs of config 5 in total over the N GPUs
-        cf["config5"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp64", 4096, RK, RW, world, rank, local, 4,
-                                   sharded_gather=gather, graph_only=go)
-        if world == 1 and not args.no_allgather:
-            # the RCCL step + all-gather path of an N-GPU job, on a world-1 group
-            cf["config5"]["with_obs_allgather"] = gather_record_world1(local, RK, RW)
+        # at N > 1 every rank must run the same sequence of collectives, so a sub-record failure is
+        # not contained there (guarded only at N = 1)
+        run = guarded if world == 1 else (lambda fn, *a, **kw: fn(*a, **kw))
+        cf["config5"] = run(bench_race, "level3", 4, "PYB_DW", "COMPETE", "fp64", 4096, RK, RW, world, rank, local, 4,
+                            sharded_gather=gather, graph_only=go)
         progress("config5")
-        cf["config5"]["strong"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp64", None, RK, RW, world, rank,
-                                             local, 4, graph_only=go, global_envs=8 * 4096)
+        cf["config5"]["strong"] = run(bench_race, "level3", 4, "PYB_DW", "COMPETE", "fp64", None, RK, RW, world, rank,
+                                      local, 4, graph_only=go, global_envs=8 * 4096)
         progress("config5 strong")
-        cf["config5_f32"] = bench_race("level3", 4, "PYB_DW", "COMPETE", "fp32", 4096, RK, RW, world, rank, local, 4,
-                                       sharded_gather=gather, graph_only=go)
+        cf["config5_f32"] = run(bench_race, "level3", 4, "PYB_DW", "COMPETE", "fp32", 4096, RK, RW, world, rank, local,
+                                4, sharded_gather=gather, graph_only=go)
         if world == 1:
             progress("config5_f32")
-            cf["config4_gnd_drag_dw"] = bench_race("level3", 4, "PYB_GND_DRAG_DW", "COMPETE", "fp64", 4096, RK, RW, 1,
-                                                   0, local, 4, graph_only=go)
+            cf["config4_gnd_drag_dw"] = run(bench_race, "level3", 4, "PYB_GND_DRAG_DW", "COMPETE", "fp64", 4096, RK, RW,
+                                            1, 0, local, 4, graph_only=go)
             progress("config4_gnd_drag_dw")
-            cf["config3"] = bench_race("level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2, graph_only=go)
+            cf["config3"] = run(bench_race, "level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2,
+                                graph_only=go)
             progress("config3")
-            cf["config3_f32"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
-                                           graph_only=go)
+            cf["config3_f32"] = run(bench_race, "level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
+                                    graph_only=go)
             progress("config3_f32")
-            cf["config3_policy"] = bench_race("level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2,
-                                              policy_spec="example", graph_only=go)
+            cf["config3_policy"] = run(bench_race, "level0", 2, "PYB", "COMPARE", "fp64", 2048, RK, RW, 1, 0, local, 2,
+                                       policy_spec="example", graph_only=go)
             progress("config3_policy")
-            cf["config3_policy_f32"] = bench_race("level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0, local, 2,
-                                                  policy_spec="example", graph_only=go)
+            cf["config3_policy_f32"] = run(bench_race, "level0", 2, "PYB", "COMPARE", "fp32", 2048, RK, RW, 1, 0,
+                                           local, 2, policy_spec="example", graph_only=go)
             progress("config3_policy_f32")
             other = "fp32" if args.precision == "fp64" else "fp64"
-            r2, _ = bench_hover(args, other, E, min(K, 1000), min(W, 100), 1, 0, local)
-            r2.update({"workload": f"the `value` workload with the {other} kernel", "unit": "env-steps/s",
-                       "dtype": "f32" if other == "fp32" else "f64"})
-            cf[f"config2_{'f32' if other == 'fp32' else 'f64'}"] = r2
+
+            def _other():
+                r2, _ = bench_hover(args, other, E, min(K, 1000), min(W, 100), 1, 0, local)
+                r2.update({"workload": f"the `value` workload with the {other} kernel", "unit": "env-steps/s",
+                           "dtype": "f32" if other == "fp32" else "f64"})
+                return r2
+            cf[f"config2_{'f32' if other == 'fp32' else 'f64'}"] = run(_other)
             progress("config2 other precision")
             if not go:
-                cf["config1"] = bench_config1(args, local, args.cpu_seconds, not args.no_cpu_baseline)
+                cf["config1"] = run(bench_config1, args, local, args.cpu_seconds, not args.no_cpu_baseline)
                 progress("config1")
-                cf["config2_sb3_vecenv"] = bench_sb3_loop(args, local)
+                cf["config2_sb3_vecenv"] = run(bench_sb3_loop, args, local)
                 progress("config2_sb3_vecenv")
+            if not args.no_allgather:
+                # the RCCL step + all-gather path of an N-GPU job on a world-1 group, last and in a
+                # child process: nothing it does can take the record with it
+                cf["config5"]["with_obs_allgather"] = gather_leg_child(RK, RW)
+                progress("config5 world-1 RCCL all-gather (child)")
         result["configs"] = cf
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -786,7 +865,10 @@ def summary(result):
     if "with_obs_allgather" in c5:
         g = c5["with_obs_allgather"]
         out["config5_allgather"] = {"v": _sig(g.get("value")), "ms": _sig(g.get("ms_per_step")), "dt": "f64",
-                                    "graph": "graph_capture_error" not in g, "world": g.get("world")}
+                                    "graph": g.get("value") is not None and "graph_capture_error" not in g,
+                                    "world": g.get("world"),
+                                    "child": g["child"] if isinstance(g.get("child"), str) else "ok" if "child" in g
+                                    else None}
     if "config1" in cf:
         c1 = cf["config1"]
         out["config1"] = {"sync_v": _sig(c1["gpu_sync_per_step"]["value"]), "graph_v": _sig(c1["gpu_graph"]["value"]),

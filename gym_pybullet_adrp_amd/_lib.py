@@ -79,29 +79,29 @@ def load():
     lib.adrp_set_diagnostics.restype = I
     lib.adrp_diagnostic_contact_count.argtypes = [P, I]
     lib.adrp_diagnostic_contact_count.restype = I
+    lib.adrp_race_moment_hash.argtypes = [P, P, ctypes.c_size_t]
+    lib.adrp_race_moment_hash.restype = I
     lib.adrp_policy_create.argtypes = [I, I, I, I, I, P, P, P, P, P, P, ctypes.POINTER(P)]
     lib.adrp_policy_create.restype = I
     lib.adrp_policy_act.argtypes = [P, P, I, I, I, P, P]
     lib.adrp_policy_act.restype = I
     lib.adrp_policy_destroy.argtypes = [P]
     lib.adrp_policy_destroy.restype = None
-    if hasattr(lib, "adrp_policy_sample"):   # (A/B runs may load an older build without it)
-        lib.adrp_policy_create2.argtypes = [I, I, I, I, I, I, P, P, P, P, P, P, ctypes.POINTER(P)]
-        lib.adrp_policy_create2.restype = I
-        lib.adrp_policy_set_critic.argtypes = [P] + [P] * 7
-        lib.adrp_policy_set_critic.restype = I
-        lib.adrp_policy_sample.argtypes = [P, P, I, I, I, ctypes.c_uint64, ctypes.c_uint32, P, P, P, P, P, P]
-        lib.adrp_policy_sample.restype = I
-        lib.adrp_gae.argtypes = [P, P, P, P, P, I, I, ctypes.c_double, ctypes.c_double, P, P, P]
-        lib.adrp_gae.restype = I
-    if hasattr(lib, "adrp_compact_rows"):
-        lib.adrp_compact_rows.argtypes = [P, P, P, I, I, I, P, P, P, P]
-        lib.adrp_compact_rows.restype = I
-    if hasattr(lib, "adrp_memcpy_async"):
-        lib.adrp_memcpy_async.argtypes = [P, P, ctypes.c_size_t, I, P]
-        lib.adrp_memcpy_async.restype = I
-        lib.adrp_stream_synchronize.argtypes = [P]
-        lib.adrp_stream_synchronize.restype = I
+    # (every entry point include/adrp.h declares is bound: a library without one fails here, loudly)
+    lib.adrp_policy_create2.argtypes = [I, I, I, I, I, I, P, P, P, P, P, P, ctypes.POINTER(P)]
+    lib.adrp_policy_create2.restype = I
+    lib.adrp_policy_set_critic.argtypes = [P] + [P] * 7
+    lib.adrp_policy_set_critic.restype = I
+    lib.adrp_policy_sample.argtypes = [P, P, I, I, I, ctypes.c_uint64, ctypes.c_uint32, P, P, P, P, P, P]
+    lib.adrp_policy_sample.restype = I
+    lib.adrp_gae.argtypes = [P, P, P, P, P, I, I, ctypes.c_double, ctypes.c_double, P, P, P]
+    lib.adrp_gae.restype = I
+    lib.adrp_compact_rows.argtypes = [P, P, P, I, I, I, P, P, P, P]
+    lib.adrp_compact_rows.restype = I
+    lib.adrp_memcpy_async.argtypes = [P, P, ctypes.c_size_t, I, P]
+    lib.adrp_memcpy_async.restype = I
+    lib.adrp_stream_synchronize.argtypes = [P]
+    lib.adrp_stream_synchronize.restype = I
     if hasattr(lib, "adrp_math_probe"):      # (A/B runs may load an older build without it)
         lib.adrp_math_probe.argtypes = [I, P, P, I, P]
         lib.adrp_math_probe.restype = I
@@ -276,6 +276,16 @@ class Handle:
     def contact_count(self, reset=True):
         """env-steps that touched the plane contact model since the last reset (diagnostics on)"""
         return self.lib.adrp_diagnostic_contact_count(self.h, 1 if reset else 0)
+
+    def moment_hash(self):
+        """race, diagnostics on: [E*N] uint32 per drone slot, the hash of the int16 (roll, pitch, yaw)
+        moments of every firmware call of the last env.step (the parity tests compare it with the CPU
+        restatement's)"""
+        import numpy as np
+        out = np.zeros(self.E * self.N, np.uint32)
+        self._check(self.lib.adrp_race_moment_hash(self.h, out.ctypes.data_as(ctypes.c_void_p), out.size),
+                    "adrp_race_moment_hash")
+        return out
 
     def profile_begin(self, n):
         self._check(self.lib.adrp_profile_begin(self.h, n), "adrp_profile_begin")

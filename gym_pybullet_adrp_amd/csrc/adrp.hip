@@ -436,7 +436,7 @@ extern "C" void adrp_destroy(adrp_t* h) {
     for (auto e : h->ev_start) hipEventDestroy(e);
     for (auto e : h->ev_stop) hipEventDestroy(e);
     hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters); hipFree(h->cblk);
-    hipFree(h->cmdf); hipFree(h->cmdi);
+    hipFree(h->cmdf); hipFree(h->cmdi); hipFree(h->mom_hash);
     delete h;
 }
 
@@ -726,7 +726,29 @@ extern "C" int adrp_profile_end(adrp_t* h, float* kernel_ms, int cap) {
 
 extern "C" int adrp_set_diagnostics(adrp_t* h, int enable) {
     if (!h) return ADRP_ERR_INVALID;
+    if (enable && h->cfg.task == ADRP_TASK_RACE && !h->mom_hash) {
+        DeviceGuard g(h->device);
+        const size_t bytes = size_t(h->E) * h->N * sizeof(uint32_t);
+        if (hipMalloc((void**)&h->mom_hash, bytes) != hipSuccess) {
+            h->mom_hash = nullptr;
+            return seterr(h, ADRP_ERR_OOM, "adrp_set_diagnostics: hipMalloc failed");
+        }
+        if (hipMemset(h->mom_hash, 0, bytes) != hipSuccess) return seterr(h, ADRP_ERR_DEVICE, "adrp_set_diagnostics");
+    }
     h->diagnostics = enable ? 1 : 0;
+    return ADRP_OK;
+}
+
+// race diagnostics: the per-drone hash of the int16 firmware moments of the last env.step
+// (race_kernel.h fw_moment_hash), copied to host memory after the handle's device finishes
+extern "C" int adrp_race_moment_hash(adrp_t* h, uint32_t* out, size_t n) {
+    if (!h || !out) return seterr(h, ADRP_ERR_INVALID, "adrp_race_moment_hash: NULL argument");
+    if (h->cfg.task != ADRP_TASK_RACE || !h->mom_hash)
+        return seterr(h, ADRP_ERR_INVALID, "adrp_race_moment_hash: a race handle with diagnostics on");
+    if (n != size_t(h->E) * h->N) return seterr(h, ADRP_ERR_INVALID, "adrp_race_moment_hash: n != E * N");
+    DeviceGuard g(h->device);
+    HIPCHK(h, hipDeviceSynchronize());
+    HIPCHK(h, hipMemcpy(out, h->mom_hash, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return ADRP_OK;
 }
 
@@ -766,6 +788,7 @@ extern "C" int adrp_gjk_dump_read(double* out, int max, int f64, int reset) {
 
 extern "C" int adrp_diagnostic_contact_count(adrp_t* h, int reset) {
     if (!h) return ADRP_ERR_INVALID;
+    DeviceGuard g(h->device);
     int32_t v = 0;
     if (hipMemcpy(&v, h->counters, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return ADRP_ERR_DEVICE;
     if (reset && hipMemset(h->counters, 0, sizeof(int32_t)) != hipSuccess) return ADRP_ERR_DEVICE;

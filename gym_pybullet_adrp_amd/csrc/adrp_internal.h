@@ -45,6 +45,7 @@ struct adrp_handle {
     const double* inj_act = nullptr;    // adrp_set_noise (parity mode): caller's device arrays
     const double* inj_force = nullptr;
     int diagnostics = 0;
+    uint32_t* mom_hash = nullptr; // race diagnostics: [E*N] firmware int16-moment hash of the last step
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;
     int prof_cap = 0, prof_n = 0;
@@ -107,6 +108,7 @@ inline RaceArgs<Real> race_args(const adrp_t* h) {
     a.ci = h->cmdi;
     a.inj_act = h->inj_act;
     a.inj_force = h->inj_force;
+    a.mom_hash = h->diagnostics ? h->mom_hash : nullptr;
     return a;
 }
 

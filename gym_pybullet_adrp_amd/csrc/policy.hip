@@ -285,6 +285,7 @@ extern "C" int adrp_gae(const float* rewards, const float* values, const float* 
         return seterr(nullptr, ADRP_ERR_INVALID, "adrp_gae: NULL argument");
     if (n_steps < 0 || n_envs < 0) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_gae: sizes");
     if (n_steps == 0 || n_envs == 0) return ADRP_OK;
+    StreamDeviceGuard g((hipStream_t)stream);
     hipLaunchKernelGGL(gae_kernel, dim3((n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, values,
                        episode_starts, last_values, dones, n_steps, n_envs, float(gamma), float(gamma * gae_lambda), advantages,
                        returns);
@@ -344,6 +345,7 @@ extern "C" int adrp_compact_rows(const uint8_t* term, const uint8_t* trunc, cons
     if (!term || !trunc || !rows || !count || !idx || (cap > 0 && !out_rows))
         return seterr(nullptr, ADRP_ERR_INVALID, "adrp_compact_rows: NULL argument");
     if (n < 0 || row_floats <= 0 || cap < 0) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_compact_rows: sizes");
+    StreamDeviceGuard g((hipStream_t)stream);
     hipLaunchKernelGGL(compact_rows_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, term, trunc, rows, n, row_floats,
                        cap, count, idx, out_rows);
     const hipError_t e = hipGetLastError();
@@ -355,12 +357,14 @@ extern "C" int adrp_compact_rows(const uint8_t* term, const uint8_t* trunc, cons
 // host -> device, 2 = device -> host (pinned host memory: asynchronous on the stream)
 extern "C" int adrp_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream) {
     if (!dst || !src || (kind != 1 && kind != 2)) return seterr(nullptr, ADRP_ERR_INVALID, "adrp_memcpy_async: arguments");
+    StreamDeviceGuard g((hipStream_t)stream);
     const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost,
                                         (hipStream_t)stream);
     if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("memcpy: ") + hipGetErrorString(e));
     return ADRP_OK;
 }
 extern "C" int adrp_stream_synchronize(void* stream) {
+    StreamDeviceGuard g((hipStream_t)stream);
     const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
     if (e != hipSuccess) return seterr(nullptr, ADRP_ERR_DEVICE, std::string("stream sync: ") + hipGetErrorString(e));
     return ADRP_OK;

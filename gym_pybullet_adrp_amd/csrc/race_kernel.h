@@ -98,6 +98,7 @@ struct RaceArgs {
     uint64_t seed;
     int64_t env_offset;
     int E;
+    uint32_t* mom_hash;  // diagnostics (adrp_set_diagnostics): [E*N] fw_moment_hash of the step, or null
 };
 
 // The physical constants of the reference's race drone (cf2x.urdf at PYB_FREQ 500, BaseAviary.py:
@@ -529,6 +530,17 @@ __device__ __forceinline__ Shape<Real> drone_shape(const RaceConst<Real>& C, V3<
 // ---------------------------------------------------------------------------------------
 // lane state
 // ---------------------------------------------------------------------------------------
+// Diagnostics (the causal fp64 closed-loop bar, tests/test_race_gpu.py): an FNV-1a style hash of the
+// int16 (roll, pitch, yaw) moments of every firmware call of one env.step, in call order.  The
+// oracle computes the same hash (oracle/race.c fw_moment_hash), so equal hashes mean the kernel and
+// the oracle truncated every moment of the step to the same integers.
+constexpr uint32_t kMomHashSeed = 2166136261u;
+__device__ __forceinline__ uint32_t fw_moment_hash(uint32_t h, float r, float p, float y) {
+    h = (h ^ uint32_t(int32_t(r))) * 16777619u;
+    h = (h ^ uint32_t(int32_t(p))) * 16777619u;
+    return (h ^ uint32_t(int32_t(y))) * 16777619u;
+}
+
 template <typename Real>
 struct RDrone {
     V3<Real> pos, vel, w, angv, lpos, kpos;
@@ -543,6 +555,7 @@ struct RDrone {
     int tick, last_att, last_pos, tumble, gate, flags;   // last_*: the ticks of last_{att,pos}_pid_call
     int tick_base;                  // tick of bit 0 of the tick-schedule windows
     uint32_t att_bits, pos_bits;    // tick_window(tick_base)
+    uint32_t mh;                    // fw_moment_hash over this env.step's firmware calls (diagnostics)
 };
 
 template <typename Real>
@@ -575,6 +588,7 @@ __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, s
     d.pw_roll = float(L_(RF_PREV_OMEGA_ROLL)); d.pw_pitch = float(L_(RF_PREV_OMEGA_PITCH));
     d.psp_roll = float(L_(RF_PREV_SP_ROLL)); d.psp_pitch = float(L_(RF_PREV_SP_PITCH));
     d.mass = L_(RF_MASS);
+    d.mh = kMomHashSeed;
 #undef L_
     const int32_t* ist = a.ist;
     d.tick = ist[RI_TICK * EN + slot]; d.last_att = ist[RI_LAST_ATT * EN + slot];
@@ -618,6 +632,7 @@ __device__ __forceinline__ void store_drone_body(const RaceArgs<Real>& a, size_t
     int32_t* ist = a.ist;
     ist[RI_TICK * EN + slot] = d.tick; ist[RI_LAST_ATT * EN + slot] = d.last_att;
     ist[RI_LAST_POS * EN + slot] = d.last_pos; ist[RI_TUMBLE * EN + slot] = d.tumble;
+    if (a.mom_hash) a.mom_hash[slot] = d.mh;
 }
 template <typename Real>
 __device__ __forceinline__ void store_drone_flags(const RaceArgs<Real>& a, size_t EN, size_t slot, const RDrone<Real>& d) {
@@ -650,6 +665,8 @@ __device__ __forceinline__ void store_drone(const RaceArgs<Real>& a, size_t EN, 
     if (params) {   // mass / inertia: written by the reset only
         S_(RF_MASS, d.mass);
         S_(RF_INERTIA, d.inertia[0]); S_(RF_INERTIA + 1, d.inertia[1]); S_(RF_INERTIA + 2, d.inertia[2]);
+    } else if (a.mom_hash) {   // the step's store (not a reset's): the firmware-output hash
+        a.mom_hash[slot] = d.mh;
     }
 #undef S_
     int32_t* ist = a.ist;
@@ -768,6 +785,7 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
     d.ctl[0] = on ? float(int16_t(clampf_(Mx, -32000.0f, 32000.0f))) : 0.0f;
     d.ctl[1] = on ? float(int16_t(clampf_(My, -32000.0f, 32000.0f))) : 0.0f;
     d.ctl[2] = on ? float(int16_t(clampf_(-Mz, -32000.0f, 32000.0f))) : 0.0f;
+    d.mh = fw_moment_hash(d.mh, d.ctl[0], d.ctl[1], d.ctl[2]);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         d.ierr[k] = on ? d.ierr[k] : 0.0f;

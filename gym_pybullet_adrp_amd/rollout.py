@@ -74,6 +74,12 @@ class RolloutCollector:
     def collect(self):
         """one rollout of n_steps env.steps -> fills the buffer and runs GAE (SB3 collect_rollouts +
         compute_returns_and_advantage); every tensor stays on the device"""
+        # the env's device is the current one for the whole rollout: the launches take that device's
+        # current stream (a null stream is the current device's, ADVICE r4)
+        with torch.cuda.device(self.obs.device):
+            return self._collect()
+
+    def _collect(self):
         env, pol, E = self.env, self.policy, self.E
         base = self.rollouts * self.T
         env_act = self._env_act.view(E, -1)
@@ -86,11 +92,12 @@ class RolloutCollector:
             self.rewards[t].copy_(rew)
             self._term[t].copy_(term)
             self._trunc[t].copy_(trunc)
-            # time-limit bootstrap (collect_rollouts): reward += gamma * V(terminal obs) where the
-            # episode was truncated and not terminated
+            # time-limit bootstrap (collect_rollouts): reward += gamma * V(terminal obs) only where the
+            # episode was truncated and not terminated; a select, so a stale terminal row of an env
+            # that did not finish (even a non-finite one) never reaches its reward
             self._values_of(info["terminal_observation"].reshape(E, -1), self._tv)
-            boot = (trunc & ~term).to(torch.float32)
-            self.rewards[t].add_(boot * self.gamma * self._tv)
+            boot = trunc & ~term
+            torch.where(boot, self.rewards[t] + self.gamma * self._tv, self.rewards[t], out=self.rewards[t])
             self._last_obs.copy_(obs.reshape(E, -1))
             self._last_start.copy_((term | trunc).to(torch.float32))
         # values of the observations after the last step (SB3: policy.predict_values(new_obs))

@@ -28,6 +28,7 @@ annotates; writing into a shared entry raises).  Returned
 arrays are fresh copies (DummyVecEnv semantics) unless ``zero_copy=True``: then they are views
 of a ring of ``ring`` pinned buffers, valid until ``ring`` more steps have been taken.
 """
+import contextlib
 import types
 from collections.abc import Sequence
 
@@ -180,7 +181,8 @@ class AviaryVecEnv(_VecEnvBase):
         seed, self._seed = self._seed, None
         obs, _ = self.env.reset(seed=seed)
         if self._packed:
-            o = self._copy_out()[0]
+            with self._on_device():
+                o = self._copy_out()[0]
             return o if self.zero_copy else o.copy()
         return self._out(obs).copy() if not self.as_torch else obs.clone()
 
@@ -255,9 +257,15 @@ class AviaryVecEnv(_VecEnvBase):
             obs, rew = obs.copy(), rew.copy()
         return obs, rew, done, infos
 
+    def _on_device(self):
+        """the env's device current while the raw C-ABI copies / compaction run: a null (default)
+        stream names the current device's, so the work then lands on the env's"""
+        return torch.cuda.device(self._dev.device) if self._dev.is_cuda else contextlib.nullcontext()
+
     def step_wait(self):
         if self._packed:
-            return self._step_wait_packed()
+            with self._on_device():
+                return self._step_wait_packed()
         obs, rew, term, trunc, info = self.env.step(self._actions)
         done = term | trunc
         if self.as_torch:

@@ -277,6 +277,12 @@ int adrp_profile_end(adrp_t* h, float* kernel_ms, int cap);
  * count env-steps whose sub-steps touched the plane contact model. */
 int adrp_set_diagnostics(adrp_t* h, int enable);
 int adrp_diagnostic_contact_count(adrp_t* h, int reset);
+/* Race handles: with diagnostics on, each env.step also records per drone a hash of the int16
+ * (roll, pitch, yaw) moments of every firmware controllerMellinger call of the step, in call order
+ * (FNV-1a over the int32 values, seed 2166136261, prime 16777619; oracle/race.c computes the same).
+ * Parity tests use it as the causal witness of an int16 truncation difference.  Copies E * N values
+ * of the last step to `out` (host memory); n must be E * N.  Replaces nothing in the reference. */
+int adrp_race_moment_hash(adrp_t* h, uint32_t* out, size_t n);
 
 /* ---------------------------------------------------------------------------------------
  * On-device policy forward: the actor of an SB3 PPO MlpPolicy

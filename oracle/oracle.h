@@ -47,6 +47,7 @@ int orc_race_command(orc_t* o, const int32_t* cmd, const double* args);
    (kept by pointer) instead of the Philox draws; NULL, NULL returns to Philox */
 int orc_set_noise(orc_t* o, const double* act_noise, const double* force);
 int orc_race_moment_margin(const orc_t* o, float* out);
+int orc_race_moment_hash(const orc_t* o, uint32_t* out);   /* fw_moment_hash of the last step, per drone */
 int orc_normal_pair(uint32_t x0, uint32_t x1, float* z);
 int orc_get_command_state(const orc_t* o, float* f, int32_t* i);
 int orc_set_command_state(orc_t* o, const float* f, const int32_t* i);

@@ -77,6 +77,7 @@ def _load():
     lib.orc_race_command.argtypes = [P, P, P]
     lib.orc_set_noise.argtypes = [P, P, P]
     lib.orc_race_moment_margin.argtypes = [P, P]
+    lib.orc_race_moment_hash.argtypes = [P, P]
     lib.orc_normal_pair.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P]
     lib.orc_get_command_state.argtypes = [P, P, P]
     lib.orc_set_command_state.argtypes = [P, P, P]
@@ -197,6 +198,13 @@ class Oracle:
         firmware calls; inf if no call produced moments"""
         out = np.zeros(self.E * self.N, np.float32)
         assert lib().orc_race_moment_margin(self.h, _ptr(out)) == 0
+        return out
+
+    def moment_hash(self):
+        """[E*N] uint32 per drone slot: the hash of the int16 (roll, pitch, yaw) moments of every
+        firmware call of the last env.step, in call order (the kernel's adrp_race_moment_hash)"""
+        out = np.zeros(self.E * self.N, np.uint32)
+        assert lib().orc_race_moment_hash(self.h, _ptr(out)) == 0
         return out
 
     def contact_count(self):

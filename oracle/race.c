@@ -74,6 +74,8 @@ typedef struct rdrone_s {
     float mom_margin;                /* diagnostic, not state: over this env.step's firmware calls, the
                                         smallest distance of a clamped moment to a point where its int16
                                         truncation changes (a nonzero integer) */
+    uint32_t mom_hash;               /* diagnostic, not state: fw_moment_hash over this env.step's firmware
+                                        calls (the kernel's adrp_race_moment_hash) */
     /* race progress */
     int gate, elim, fin;
     /* command state (adrp.h ADRP_CMD_NF / ADRP_CMD_NI order): setpoint_t fields the controller
@@ -130,6 +132,15 @@ static f3 f3cross(f3 a, f3 b) { return F3(a.y * b.z - a.z * b.y, a.z * b.x - a.x
 static f3 f3norm(f3 a) {
     float m = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
     return F3(a.x / m, a.y / m, a.z / m);
+}
+
+/* the int16 moments of one firmware call folded into the step's hash (FNV-1a over the int32 values;
+   include/adrp.h adrp_race_moment_hash, race_kernel.h fw_moment_hash) */
+#define MOM_HASH_SEED 2166136261u
+static uint32_t fw_moment_hash(uint32_t h, float r, float p, float y) {
+    h = (h ^ (uint32_t)(int32_t)r) * 16777619u;
+    h = (h ^ (uint32_t)(int32_t)p) * 16777619u;
+    return (h ^ (uint32_t)(int32_t)y) * 16777619u;
 }
 
 static void mellinger_reset(rdrone_t* d) {   /* controllerMellingerReset */
@@ -234,6 +245,7 @@ static void mellinger_fw(rdrone_t* d, const float gyro[3], const float st_pos[3]
         d->ctl[0] = d->ctl[1] = d->ctl[2] = 0;
         mellinger_reset(d);
     }
+    d->mom_hash = fw_moment_hash(d->mom_hash, d->ctl[0], d->ctl[1], d->ctl[2]);
 }
 
 /* ---------------------------------------------------------------------------------- */
@@ -1120,7 +1132,7 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
     body_t* bs = &o->b[(size_t)e * N];
     rdrone_t* ds = &o->rd[(size_t)e * N];
     int touched = 0;
-    for (int i = 0; i < N; ++i) ds[i].mom_margin = INFINITY;
+    for (int i = 0; i < N; ++i) { ds[i].mom_margin = INFINITY; ds[i].mom_hash = MOM_HASH_SEED; }
     /* the command message per drone (190-210): FULLSTATE (act[:3], 0, 0, act[3], 0, step_counter)
        from an ndarray action (act = NULL: the commands adrp_race_command / orc_race_command sent);
        eliminated drones get STOP [step_counter] */
@@ -1316,6 +1328,11 @@ static void race_set_row(orc_t* o, size_t slot, int e, int first, const double* 
 int orc_race_moment_margin(const orc_t* o, float* out) {
     if (!o->rd) return ADRP_ERR_INVALID;
     for (size_t k = 0; k < (size_t)o->E * o->N; ++k) out[k] = o->rd[k].mom_margin;
+    return 0;
+}
+int orc_race_moment_hash(const orc_t* o, uint32_t* out) {
+    if (!o || !o->rd) return -1;
+    for (size_t k = 0; k < (size_t)o->E * o->N; ++k) out[k] = o->rd[k].mom_hash;
     return 0;
 }
 

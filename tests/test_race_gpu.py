@@ -16,8 +16,9 @@ So the north-star bound, 1e-4 per physics step on identical RPM inputs, is teste
 1e-6), and full 20-sub-step closed-loop env.steps are held to rtol 2e-3 in fp32.  The fp64
 kernel draws the oracle's action noise bit for bit and runs the float firmware with the C
 operations, so its closed loop is held to 1e-6, and a drone may exceed that only in a step where
-one of its firmware moments sat within ATTR_TAU of an int16 truncation point (the oracle reports
-the margin per drone, Oracle.moment_margin: check_closed_loop).
+the kernel's int16 firmware moments differ from the oracle's: both record a hash of every firmware
+call's int16 (roll, pitch, yaw) triple in call order (adrp_race_moment_hash / Oracle.moment_hash),
+and a drone whose hash equals the oracle's is held to 1e-6 with no exemption (check_closed_loop).
 Discrete outputs (current gate, elimination, terminated, truncated, in-range flags) must
 match exactly.
 """
@@ -44,16 +45,15 @@ FLOORS = {"pos": 1e-3, "quat": 1e-3, "vel": 1e-3, "omega": 1e-3, "rpm": 1.0}
 
 
 RTOL = {"fp32": 2e-3, "fp64": 2e-3}    # the cap every drone stays under
-FP64_BAR = 1e-6                          # fp64 closed loop: the bar for every drone not attributed
-ATTR_TAU = 0.0125                        # int16 units: a float-ulp change of a firmware input moves a
-                                         # moment by ~1e-2 at the 7e4 / 2e4 attitude gains; the drones
-                                         # over FP64_BAR measured margins <= 0.0093 (r4b: 97 of 4,224)
+FP64_BAR = 1e-6                          # fp64 closed loop: every drone whose int16 firmware moments
+                                         # all equal the oracle's (same moment hash) stays within it
 
 
 def pair(level, N, physics, mode, reward, E, **kw):
     kw.setdefault("precision", "fp32")
     env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=11,
                           autoreset=False, reward=reward, **kw)
+    env.h.set_diagnostics(True)          # the firmware moment hash of every step (check_closed_loop)
     return env, O.Oracle(env.cfg.copy())
 
 
@@ -149,29 +149,36 @@ def state_errors(env, orc, floors=None):
     return out
 
 
+def moment_witness(hash_gpu, hash_cpu, err, flags_same, stats=None, where=""):
+    """the causal fp64 bar: a drone may exceed FP64_BAR only if some firmware call of the step
+    truncated a moment to a different int16 than the oracle's (the two moment hashes differ).
+    stats accumulates drones compared / drones with an int16 difference / exceedances / the largest
+    error among the drones whose int16 sequences match"""
+    differ = hash_gpu != hash_cpu
+    over = (err > FP64_BAR) & flags_same
+    bad = np.flatnonzero(over & ~differ)
+    assert len(bad) == 0, (f"{where}{len(bad)} drones over {FP64_BAR:g} whose int16 firmware moments all equal the "
+                           f"oracle's: slots {bad[:8]}, errors {err[bad[:8]]}")
+    if stats is not None:
+        stats["drones"] = stats.get("drones", 0) + err.size
+        stats["int16_differ"] = stats.get("int16_differ", 0) + int(differ.sum())
+        stats["over"] = stats.get("over", 0) + int(over.sum())
+        same = flags_same & ~differ
+        stats["max_err_same_int16"] = max(stats.get("max_err_same_int16", 0.0), float(err[same].max(initial=0)))
+    return differ
+
+
 def check_closed_loop(env, orc, precision, stats=None, floors=None):
-    """one closed-loop env.step: fp32 at RTOL; fp64 every drone within FP64_BAR unless the oracle's
-    firmware moment margin of this step is below ATTR_TAU (an int16 truncation within rounding),
-    and every drone within RTOL.  stats (dict) accumulates drones / exceeding / near-boundary counts."""
+    """one closed-loop env.step: fp32 at RTOL; fp64 every drone within FP64_BAR unless its int16
+    firmware moments differ from the oracle's in this step (moment_witness), and every drone within
+    RTOL.  stats (dict) accumulates the counts moment_witness reports."""
     worst = check_state(env, orc, RTOL[precision], floors=floors)
     if precision == "fp64":
         err = np.max(np.stack(list(state_errors(env, orc, floors).values())), axis=0)
-        margin = orc.moment_margin()
         _, io = orc.get_state()
         _, inames = orc.field_names()
         flags_same = env.get_state()[1].cpu().numpy()[inames.index("flags")] == io[inames.index("flags")]
-        over = (err > FP64_BAR) & flags_same
-        bad = np.flatnonzero(over & ~(margin < ATTR_TAU))
-        assert len(bad) == 0, (f"{len(bad)} drones over {FP64_BAR:g} with no int16 moment within {ATTR_TAU} of a "
-                               f"truncation point: slots {bad[:8]}, errors {err[bad[:8]]}, margins {margin[bad[:8]]}")
-        if stats is not None:
-            stats["drones"] = stats.get("drones", 0) + err.size
-            stats["over"] = stats.get("over", 0) + int(over.sum())
-            stats["near"] = stats.get("near", 0) + int((margin < ATTR_TAU).sum())
-            stats["max_unattributed"] = max(stats.get("max_unattributed", 0.0), float(err[~(margin < ATTR_TAU)].max(initial=0)))
-            stats["over_margin_max"] = max(stats.get("over_margin_max", 0.0), float(margin[over].max(initial=0)))
-            for t in (1e-3, 1e-4):
-                stats[f"margin<{t:g}"] = stats.get(f"margin<{t:g}", 0) + int((margin < t).sum())
+        moment_witness(env.h.moment_hash(), orc.moment_hash(), err, flags_same, stats)
     return worst
 
 
@@ -565,6 +572,7 @@ def test_full_size_subset_vs_oracle(E, N, level, physics, mode, precision):
     rng = np.random.default_rng(17)
     env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=7, autoreset=False,
                           precision=precision)
+    env.h.set_diagnostics(True)
     assert env.kernel_name == f"race_step<{'f64' if precision == 'fp64' else 'f32'},{physics.name},G{N},Q4>"
     obs, _ = env.reset()
     act = targets(rng, obs.cpu().numpy(), E, N)
@@ -592,32 +600,28 @@ def test_full_size_subset_vs_oracle(E, N, level, physics, mode, precision):
     # the firmware's int16 moment truncation carries O(1e-4) rad/s differences through the step (module
     # docstring); over 192 sampled drones some hover with |omega| ~ 1e-2, so omega gets a 0.1 rad/s floor
     floors = dict(FLOORS, omega=0.1)
-    over = near = 0
+    hash_g = env.h.moment_hash()
+    stats = {}
     for o, e in zip(orcs, sub):
         fo, io = o.get_state()
         sl = slice(e * N, (e + 1) * N)
-        margin = o.moment_margin()
         kf = inames.index("flags")
         flags_same = ig[kf, sl] == io[kf]
+        errs = []
         for g, fields in GROUPS.items():
             rows = [idx[n] for n in fields]
             err = np.linalg.norm(fg[rows, sl] - fo[rows], axis=0) / np.maximum(np.linalg.norm(fo[rows], axis=0), floors[g])
             assert err.max() <= RTOL["fp32"], (f"env {e} {g}: {err.max():.3e}; flags {io[inames.index('flags')]} "
                                                f"gpu {fg[rows, sl].T} cpu {fo[rows].T} z {fo[idx['pos_z']]}")
-            if precision == "fp64":
-                bad = (err > FP64_BAR) & flags_same & ~(margin < ATTR_TAU)
-                assert not bad.any(), (f"env {e} {g}: {err.max():.3e} over {FP64_BAR:g}, moment margins {margin}")
-                over += int(((err > FP64_BAR) & flags_same).sum())
-                if ((err > FP64_BAR) & flags_same).any():
-                    print(f"env {e} {g}: over-bar margins {margin[(err > FP64_BAR) & flags_same]}")
-        near += int((margin < ATTR_TAU).sum())
+            errs.append(err)
+        if precision == "fp64":
+            moment_witness(hash_g[sl], o.moment_hash(), np.max(np.stack(errs), axis=0), flags_same, stats,
+                           where=f"env {e}: ")
         for k in ("step_counter", "episode", "gate", "tick", "last_att_tick", "last_pos_tick"):
             np.testing.assert_array_equal(ig[inames.index(k), sl], io[inames.index(k)], err_msg=f"env {e} {k}")
-        kf = inames.index("flags")
         for n in np.flatnonzero(ig[kf, sl] != io[kf]):
             assert abs(contact_margin(o.cfg, fo, names, n)) < 1e-4, f"env {e} drone {n}: flags differ"
-    print(f"{level} {physics.name} {precision}: {48 * N} drones, {over} (drone, group) over {FP64_BAR:g}, "
-          f"{near} with a moment within {ATTR_TAU} of an int16 truncation point")
+    print(f"{level} {physics.name} {precision}: {48 * N} drones, int16 witness {stats}")
     env.close()
 
 

@@ -164,8 +164,12 @@ def test_packed_gather_rccl_graph():
         torch.cuda.current_stream().wait_stream(side)
         ref.step(acts[0])
         a_buf = acts[1].clone()
+        # no RCCL work pending and a thread-local capture: the ProcessGroupNCCL watchdog's event
+        # queries must not meet a global-mode capture (BENCH_r04's abort, bench.quiesce_collectives)
+        import bench
+        bench.quiesce_collectives()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with bench.capture_graph(g):
             out = sh.step_gather(a_buf)
         done = 0
         for k in range(1, 21):
