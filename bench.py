@@ -22,7 +22,8 @@ The same JSON line carries sub-records (`configs`), each timed the same way:
   config3_policy  N = 1: config 3 (float64) driven by the reference's PPO actor on the device
   config4_gnd_drag_dw  N = 1: config 4 with Physics.PYB_GND_DRAG_DW (float64)
   config2_f32  N = 1: the `value` workload with the float32 kernel
-  config1      N = 1: one HoverAviary env (E = 1), per-step latency, GPU and CPU oracle
+  config1      N = 1: one HoverAviary env (E = 1), per-step latency: a launch per step, graph-replayed,
+               and the persistent step kernel (numpy in / out, synchronous); the CPU oracle
 Rooflines: the hover kernel is HBM-bound (bytes per launch / kernel time vs 8 TB/s); the race
 kernel is VALU/issue-bound (PMC-counted flops per launch / kernel time vs the vector peak;
 HBM fraction kept as information).  Kernel time = HIP events on the launching stream around
@@ -649,6 +650,22 @@ def bench_config1(args, dev, cpu_seconds, with_cpu):
                                  "note": "Python env.step + torch.cuda.synchronize each step"},
            "gpu_graph": {"value": 1000 / elapsed, "unit": "env-steps/s", "us_per_step": elapsed / 1000 * 1e6},
            "kernel_us": graph_kernel_us, "eager_dispatch_us": float(np.mean(kern)) * 1e3}
+    # the same loop without a launch per step: a resident step kernel polling a host-mapped mailbox
+    # (HoverAviary.persistent, include/adrp.h adrp_persistent_*); numpy action in, numpy obs out,
+    # the step finished when step() returns
+    acts_np = acts.cpu().numpy()
+    with env.persistent() as p:
+        for k in range(200):
+            p.step(acts_np[k % acts_np.shape[0]])
+        n_p = 5000
+        t0 = time.perf_counter()
+        for k in range(n_p):
+            p.step(acts_np[k % acts_np.shape[0]])
+        ps = (time.perf_counter() - t0) / n_p
+    rec["gpu_persistent_sync_per_step"] = {
+        "value": 1 / ps, "unit": "env-steps/s", "us_per_step": ps * 1e6, "steps": n_p,
+        "note": "HoverAviary.persistent(): numpy action written to host-mapped memory, one resident step kernel "
+                "(no launch per step), numpy obs / reward / flags read from host-mapped memory when step() returns"}
     if with_cpu:
         v, steps, dt = _oracle_leg(env.cfg, 1, _hover_acts, min(cpu_seconds, 3.0), 1)
         rec["cpu_oracle_1env"] = {"value": v, "unit": "env-steps/s", "cores": 1,
@@ -871,8 +888,11 @@ def summary(result):
                                     else None}
     if "config1" in cf:
         c1 = cf["config1"]
-        out["config1"] = {"sync_v": _sig(c1["gpu_sync_per_step"]["value"]), "graph_v": _sig(c1["gpu_graph"]["value"]),
-                          "cpu_1core_v": _sig((c1.get("cpu_oracle_1env") or {}).get("value"))}
+        out["config1"] = {"sync_v": _sig((c1.get("gpu_persistent_sync_per_step") or {}).get("value")),
+                          "launch_sync_v": _sig((c1.get("gpu_sync_per_step") or {}).get("value")),
+                          "graph_v": _sig((c1.get("gpu_graph") or {}).get("value")),
+                          "cpu_1core_v": _sig((c1.get("cpu_oracle_1env") or {}).get("value"))} if "error" not in c1 \
+            else {"error": c1["error"]}
     if "config2_sb3_vecenv" in cf:
         out["sb3_packed_us"] = _sig(cf["config2_sb3_vecenv"]["packed"]["us_per_step"])
     if result.get("cpu_baseline"):

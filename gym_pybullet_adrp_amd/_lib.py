@@ -79,6 +79,12 @@ def load():
     lib.adrp_set_diagnostics.restype = I
     lib.adrp_diagnostic_contact_count.argtypes = [P, I]
     lib.adrp_diagnostic_contact_count.restype = I
+    lib.adrp_persistent_begin.argtypes = [P] + [ctypes.POINTER(P)] * 6
+    lib.adrp_persistent_begin.restype = I
+    lib.adrp_persistent_step.argtypes = [P]
+    lib.adrp_persistent_step.restype = I
+    lib.adrp_persistent_end.argtypes = [P]
+    lib.adrp_persistent_end.restype = I
     lib.adrp_race_moment_hash.argtypes = [P, P, ctypes.c_size_t]
     lib.adrp_race_moment_hash.restype = I
     lib.adrp_policy_create.argtypes = [I, I, I, I, I, P, P, P, P, P, P, ctypes.POINTER(P)]

@@ -12,10 +12,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
 #include "adrp_internal.h"
+#include "hover_persist.h"
 
 static thread_local std::string g_err;
 
@@ -431,6 +433,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
 
 extern "C" void adrp_destroy(adrp_t* h) {
     if (!h) return;
+    if (h->pbox) adrp_persistent_end(h);
     DeviceGuard g(h->device);
     hipDeviceSynchronize();
     for (auto e : h->ev_start) hipEventDestroy(e);
@@ -477,6 +480,7 @@ extern "C" int adrp_act_dim(const adrp_t* h) { return h ? h->A : ADRP_ERR_INVALI
 
 extern "C" int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev, void* stream) {
     if (!h || !obs_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_reset: NULL argument");
+    if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_reset: persistent mode is active (adrp_persistent_end first)");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     if (h->cfg.task == ADRP_TASK_RACE)
@@ -490,6 +494,7 @@ extern "C" int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float*
                          uint8_t* trunc_dev, float* terminal_obs_dev, void* stream) {
     if (!h || (!act_dev && !h->cmdf) || !obs_dev || !rew_dev || !term_dev || !trunc_dev)
         return seterr(h, ADRP_ERR_INVALID, "adrp_step: NULL argument");
+    if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_step: persistent mode is active (adrp_persistent_step)");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     if (h->cfg.task == ADRP_TASK_RACE)
@@ -636,6 +641,7 @@ extern "C" const char* adrp_state_field(const adrp_t* h, int is_int, int index) 
 
 extern "C" int adrp_get_state(adrp_t* h, void* f_dev, int32_t* i_dev, void* stream) {
     if (!h || !f_dev || !i_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_get_state: NULL argument");
+    if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_get_state: persistent mode is active (adrp_persistent_end first)");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t EN = size_t(h->E) * h->N, nb = h->nf_base * EN, nr = size_t(h->B) * h->A * h->E;
@@ -651,6 +657,7 @@ extern "C" int adrp_get_state(adrp_t* h, void* f_dev, int32_t* i_dev, void* stre
 
 extern "C" int adrp_set_state(adrp_t* h, const void* f_dev, const int32_t* i_dev, void* stream) {
     if (!h || !f_dev || !i_dev) return seterr(h, ADRP_ERR_INVALID, "adrp_set_state: NULL argument");
+    if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_set_state: persistent mode is active (adrp_persistent_end first)");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t EN = size_t(h->E) * h->N, nb = h->nf_base * EN, nr = size_t(h->B) * h->A * h->E;
@@ -691,6 +698,124 @@ extern "C" int64_t adrp_step_bytes(const adrp_t* h) {
                             + int64_t(h->D) * 4                   // obs write
                             + 4 + 2;                              // reward, terminated, truncated
     return per_env * h->E;
+}
+
+// ---------------------------------------------------------------------------------------------
+// persistent step (hover_persist.h): BASELINE config 1, one env stepped synchronously from Python
+// ---------------------------------------------------------------------------------------------
+static size_t a64(size_t n) { return (n + 63) & ~size_t(63); }
+
+extern "C" int adrp_persistent_begin(adrp_t* h, void** act, void** obs, void** rew, void** term, void** trunc,
+                                     void** tobs) {
+    if (!h) return seterr(h, ADRP_ERR_INVALID, "adrp_persistent_begin: NULL handle");
+    if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_persistent_begin: already active");
+    if (h->cfg.task != ADRP_TASK_HOVER || hover_has_pid(h->cfg.act_type))
+        return seterr(h, ADRP_ERR_INVALID, "adrp_persistent_begin: HoverAviary with RPM / ONE_D_RPM actions only");
+    if (h->E > kPersistMaxBlocks * kStepBlock)
+        return seterr(h, ADRP_ERR_INVALID, "adrp_persistent_begin: at most 1024 envs (one resident workgroup per 64)");
+    DeviceGuard g(h->device);
+    HIPCHK(h, hipDeviceSynchronize());   // every step / reset / set_state issued before is in the state
+    const size_t E = size_t(h->E), D = size_t(h->D), A = size_t(h->A);
+    size_t off = a64(sizeof(PersistCtl));
+    const size_t sizes[6] = {E * A * 4, E * D * 4, E * 4, E, E, E * D * 4};
+    for (int k = 0; k < 6; ++k) {
+        h->poff[k] = off;
+        off += a64(sizes[k]);
+    }
+    void* box = nullptr;
+    HIPCHK(h, hipHostMalloc(&box, off, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(box, 0, off);
+    char* dbox = nullptr;
+    if (hipHostGetDevicePointer((void**)&dbox, box, 0) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking) != hipSuccess) {
+        hipHostFree(box);
+        h->pstream = nullptr;
+        return seterr(h, ADRP_ERR_DEVICE, "adrp_persistent_begin: mapping / stream");
+    }
+    const int rc = h->real_size == 8 ? [&] {
+        HoverArgs<double> a = hover_args<double>(h);
+        a.act = (const float*)(dbox + h->poff[0]); a.obs = (float*)(dbox + h->poff[1]); a.rew = (float*)(dbox + h->poff[2]);
+        a.term = (uint8_t*)(dbox + h->poff[3]); a.trunc = (uint8_t*)(dbox + h->poff[4]);
+        a.tobs = h->cfg.autoreset ? (float*)(dbox + h->poff[5]) : nullptr;
+        a.contact_count = nullptr;
+        return hover_persist_launch<double>(h, a, dbox, h->pstream);
+    }() : [&] {
+        HoverArgs<float> a = hover_args<float>(h);
+        a.act = (const float*)(dbox + h->poff[0]); a.obs = (float*)(dbox + h->poff[1]); a.rew = (float*)(dbox + h->poff[2]);
+        a.term = (uint8_t*)(dbox + h->poff[3]); a.trunc = (uint8_t*)(dbox + h->poff[4]);
+        a.tobs = h->cfg.autoreset ? (float*)(dbox + h->poff[5]) : nullptr;
+        a.contact_count = nullptr;
+        return hover_persist_launch<float>(h, a, dbox, h->pstream);
+    }();
+    if (rc != ADRP_OK) {
+        hipStreamDestroy(h->pstream);
+        h->pstream = nullptr;
+        hipHostFree(box);
+        return rc;
+    }
+    PersistCtl* ctl = (PersistCtl*)box;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&ctl->status, __ATOMIC_ACQUIRE) != 1u) {   // resident before the first request
+        if (hipStreamQuery(h->pstream) != hipErrorNotReady ||
+            std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
+            __atomic_store_n(&ctl->req, kPersistStop, __ATOMIC_RELEASE);
+            hipStreamSynchronize(h->pstream);
+            hipStreamDestroy(h->pstream);
+            h->pstream = nullptr;
+            hipHostFree(box);
+            return seterr(h, ADRP_ERR_DEVICE, "adrp_persistent_begin: the persistent kernel did not start");
+        }
+    }
+    h->pbox = box;
+    h->pseq = 0;
+    char* hb = (char*)box;
+    if (act) *act = hb + h->poff[0];
+    if (obs) *obs = hb + h->poff[1];
+    if (rew) *rew = hb + h->poff[2];
+    if (term) *term = hb + h->poff[3];
+    if (trunc) *trunc = hb + h->poff[4];
+    if (tobs) *tobs = hb + h->poff[5];
+    return ADRP_OK;
+}
+
+extern "C" int adrp_persistent_step(adrp_t* h) {
+    if (!h || !h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_persistent_step: persistent mode is not active");
+    PersistCtl* ctl = (PersistCtl*)h->pbox;
+    uint32_t seq = h->pseq + 1;
+    if (seq == kPersistStop) seq = 1;
+    h->pseq = seq;
+    __atomic_store_n(&ctl->req, seq, __ATOMIC_RELEASE);   // the action bytes written before it are visible first
+    const int nb = (h->E + kStepBlock - 1) / kStepBlock;
+    for (int b = 0; b < nb; ++b) {
+        unsigned spins = 0;
+        auto t0 = std::chrono::steady_clock::time_point{};
+        while (__atomic_load_n(&ctl->done[b], __ATOMIC_ACQUIRE) != seq) {
+            __builtin_ia32_pause();
+            if ((++spins & 4095u) == 0) {
+                if (t0 == decltype(t0){}) t0 = std::chrono::steady_clock::now();
+                if (__atomic_load_n(&ctl->status, __ATOMIC_ACQUIRE) == 2u)
+                    return seterr(h, ADRP_ERR_DEVICE, "adrp_persistent_step: the persistent kernel has exited "
+                                                      "(idle timeout); adrp_persistent_end, then begin again");
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                    return seterr(h, ADRP_ERR_DEVICE, "adrp_persistent_step: no completion within 10 s");
+            }
+        }
+    }
+    return ADRP_OK;
+}
+
+extern "C" int adrp_persistent_end(adrp_t* h) {
+    if (!h || !h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_persistent_end: persistent mode is not active");
+    DeviceGuard g(h->device);
+    PersistCtl* ctl = (PersistCtl*)h->pbox;
+    __atomic_store_n(&ctl->req, kPersistStop, __ATOMIC_RELEASE);
+    const hipError_t e = hipStreamSynchronize(h->pstream);
+    hipStreamDestroy(h->pstream);
+    hipHostFree(h->pbox);
+    h->pstream = nullptr;
+    h->pbox = nullptr;
+    if (e != hipSuccess) return seterr(h, ADRP_ERR_DEVICE, std::string("adrp_persistent_end: ") + hipGetErrorString(e));
+    return ADRP_OK;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -46,6 +46,11 @@ struct adrp_handle {
     const double* inj_force = nullptr;
     int diagnostics = 0;
     uint32_t* mom_hash = nullptr; // race diagnostics: [E*N] firmware int16-moment hash of the last step
+    // persistent step (adrp_persistent_*, hover_persist.h): host-mapped mailbox and its own stream
+    void* pbox = nullptr;         // host address of the mapped mailbox (PersistCtl + buffers), or null
+    hipStream_t pstream = nullptr;
+    uint32_t pseq = 0;
+    size_t poff[6] = {0, 0, 0, 0, 0, 0};   // act, obs, rew, term, trunc, tobs byte offsets in pbox
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;
     int prof_cap = 0, prof_n = 0;
@@ -118,6 +123,9 @@ int hover_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* ter
                hipStream_t s);
 template <typename Real>
 int hover_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s);
+template <typename Real>
+int hover_persist_launch(adrp_t* h, const HoverArgs<Real>& a, void* ctl, hipStream_t s);
+bool hover_persist_def(const adrp_t* h);
 template <typename Real>
 int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc, float* tobs,
               hipStream_t s);

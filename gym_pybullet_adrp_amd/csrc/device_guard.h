@@ -14,7 +14,7 @@ struct DeviceGuard {
         if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
     }
     ~DeviceGuard() {
-        if (prev >= 0) hipSetDevice(prev);
+        if (prev >= 0) (void)hipSetDevice(prev);
     }
     DeviceGuard(const DeviceGuard&) = delete;
     DeviceGuard& operator=(const DeviceGuard&) = delete;
@@ -32,7 +32,7 @@ struct StreamDeviceGuard {
         if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
     }
     ~StreamDeviceGuard() {
-        if (prev >= 0) hipSetDevice(prev);
+        if (prev >= 0) (void)hipSetDevice(prev);
     }
     StreamDeviceGuard(const StreamDeviceGuard&) = delete;
     StreamDeviceGuard& operator=(const StreamDeviceGuard&) = delete;

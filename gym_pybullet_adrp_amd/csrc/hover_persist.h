@@ -1,0 +1,81 @@
+// hover_persist.h — persistent HoverAviary step for small E (BASELINE config 1: one env stepped
+// synchronously from Python, examples/pid.py:101-147 driving envs/BaseAviary.py:262-387).
+//
+// A launch per env.step costs the host a kernel launch (~5 us), the kernel a cold start (the
+// agent-scope acquire at kernel start invalidates L2, so the first loads go to HBM) and the host a
+// completion wait.  Here ONE launch stays resident on one CU per 64 envs and polls a host-mapped
+// mailbox: the host writes the action into mapped memory and bumps `req`; the kernel runs the same
+// hover_step_body as hover_step_kernel (the env state stays hot in L2 between steps), writes obs /
+// reward / flags straight into mapped memory and publishes `done`.  The host spins on `done` in its
+// own memory, so one env.step is two PCIe crossings and the step itself.
+//
+// Exit: the host's stop request, or no request for kPersistIdleTicks (s_memrealtime, 100 MHz): every
+// wave reaches one of the two, so the grid always drains (a host that died leaves a kernel that
+// ends by itself).
+#pragma once
+
+#include "hover_kernel.h"
+
+namespace adrp {
+
+constexpr uint32_t kPersistStop = 0xFFFFFFFFu;
+constexpr int kPersistMaxBlocks = 16;                     // E <= 16 * 64 envs
+constexpr uint64_t kPersistIdleTicks = 1000000000ull;     // 10 s without a request ends the kernel
+
+// the control block at the head of the mapped mailbox
+struct PersistCtl {
+    uint32_t req;                        // host: sequence number of the requested step, kPersistStop
+    uint32_t status;                     // device: 1 running, 2 exited
+    uint32_t pad[14];
+    uint32_t done[kPersistMaxBlocks];    // device: per workgroup, the last request it finished
+};
+
+// a: HoverArgs whose act / obs / rew / term / trunc / tobs point into the mapped mailbox (device
+// addresses of host memory); f / ring / ist / c / r are the handle's device buffers
+template <typename Real, int PH, int A, int B, bool DEF>
+__global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Real> a, PersistCtl* ctl) {
+    __shared__ uint32_t cmd;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&ctl->status, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t last = 0;
+    uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint32_t r;
+            for (;;) {
+                r = __hip_atomic_load(&ctl->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (r != last) break;
+                if (__builtin_amdgcn_s_memrealtime() - t_idle > kPersistIdleTicks) {
+                    r = kPersistStop;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            cmd = r;
+        }
+        __syncthreads();
+        const uint32_t r = cmd;
+        __syncthreads();   // cmd is rewritten by the next poll
+        if (r == kPersistStop) break;
+        // the action the host wrote before it published req: every lane's view of mapped memory fresh
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if constexpr (DEF) {
+            constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
+            hover_step_body<Real, PH, A, B, C.S>(a, C);
+        } else {
+            hover_step_body<Real, PH, A, B, 0>(a, *a.c);
+        }
+        // obs / reward / flags (mapped memory) visible to the host before done
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(&ctl->done[blockIdx.x], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = r;
+        t_idle = __builtin_amdgcn_s_memrealtime();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // the env state the next launch / get_state reads
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&ctl->status, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace adrp

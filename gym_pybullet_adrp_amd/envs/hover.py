@@ -174,6 +174,14 @@ class HoverAviary(AviaryEnv):
             self._info["terminal_observation"] = tobs
         self.h.bind(self._obs, self._rew, self._term, self._trunc, self._tobs)
 
+    # ---- persistent stepping (BASELINE config 1: a Python loop stepping a few envs synchronously) ----
+    def persistent(self):
+        """A resident step kernel for this env (include/adrp.h adrp_persistent_*): ``step(action)``
+        takes a numpy action, returns numpy views of host-mapped outputs, with no kernel launch per
+        step.  Use as a context manager; ``step`` / ``reset`` / ``get_state`` of the env itself are
+        refused until it is closed."""
+        return PersistentStepper(self)
+
     # ---- introspection (tests / teacher forcing) ----
     def get_state(self):
         return self.h.get_state()
@@ -191,3 +199,60 @@ class HoverAviary(AviaryEnv):
     def kernel_name(self):
         """the step-kernel instantiation this env launches now (include/adrp.h adrp_handle_kernel_name)"""
         return self.h.kernel_name()
+
+
+class PersistentStepper:
+    """HoverAviary.persistent(): the env.step of a resident kernel polling a host-mapped mailbox.
+
+    ``step(action)`` writes the action (numpy, [E,1,A]) into mapped memory and returns when the
+    step is done: (obs [E,1,D], reward [E], terminated [E], truncated [E], info) as numpy views of
+    mapped memory that the next step overwrites (``info["terminal_observation"]`` likewise, for the
+    auto-reset envs).  Results are those of ``HoverAviary.step`` on the same state and action."""
+
+    def __init__(self, env):
+        import ctypes
+        self.env = env
+        h = env.h
+        ptrs = [ctypes.c_void_p() for _ in range(6)]
+        rc = h.lib.adrp_persistent_begin(h.h, *[ctypes.byref(p) for p in ptrs])
+        if rc != 0:
+            raise _lib.AdrpError(f"adrp_persistent_begin: {h.lib.adrp_last_error(h.h).decode()}")
+        E, D, A = env.num_envs, h.D, h.A
+
+        def view(p, ctype, shape):
+            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctype)), shape=shape)
+        self.act = view(ptrs[0], ctypes.c_float, (E, 1, A))
+        self.obs = view(ptrs[1], ctypes.c_float, (E, 1, D))
+        self.rew = view(ptrs[2], ctypes.c_float, (E,))
+        self.term = view(ptrs[3], ctypes.c_uint8, (E,)).view(np.bool_)
+        self.trunc = view(ptrs[4], ctypes.c_uint8, (E,)).view(np.bool_)
+        self.tobs = view(ptrs[5], ctypes.c_float, (E, 1, D))
+        self.info = {"answer": 42, "terminal_observation": self.tobs}
+        self._step, self._h, self._lib = h.lib.adrp_persistent_step, h.h, h.lib
+        self.active = True
+
+    def step(self, action):
+        self.act[...] = action
+        if self._step(self._h) != 0:
+            raise _lib.AdrpError(f"adrp_persistent_step: {self._lib.adrp_last_error(self._h).decode()}")
+        return self.obs, self.rew, self.term, self.trunc, self.info
+
+    def close(self):
+        if self.active:
+            self.active = False
+            if getattr(self.env.h, "h", None) is None:   # the env was closed first: adrp_destroy ended it
+                return
+            if self._lib.adrp_persistent_end(self._h) != 0:
+                raise _lib.AdrpError(f"adrp_persistent_end: {self._lib.adrp_last_error(self._h).decode()}")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

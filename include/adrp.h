@@ -273,6 +273,22 @@ int64_t adrp_step_bytes(const adrp_t* h);
 int adrp_profile_begin(adrp_t* h, int max_launches);
 int adrp_profile_end(adrp_t* h, float* kernel_ms, int cap);
 
+/* ---------------------------------------------------------------------------------------
+ * Persistent step (HoverAviary, RPM / ONE_D_RPM actions, E <= 1024): BASELINE config 1, the
+ * reference's one-env loop (examples/pid.py:101-147 calling BaseAviary.step, envs/BaseAviary.py:
+ * 262-387) with no kernel launch per step.  begin launches one resident kernel (a workgroup per 64
+ * envs) on its own stream and returns HOST pointers into a host-mapped mailbox: act [E][A] float,
+ * obs [E][D] float, reward [E] float, terminated / truncated [E] uint8, terminal obs [E][D] float
+ * (auto-reset envs).  step: the caller writes act, calls adrp_persistent_step, which returns when
+ * the env.step is done and the outputs are in the mailbox (same results as adrp_step on the same
+ * state).  While active, adrp_step / adrp_reset / adrp_get_state / adrp_set_state are refused.
+ * end stops the kernel (destroy ends it too); the kernel also ends by itself after 10 s without a
+ * request, after which step fails and end + begin restart it. */
+int adrp_persistent_begin(adrp_t* h, void** act, void** obs, void** reward, void** terminated, void** truncated,
+                          void** terminal_obs);
+int adrp_persistent_step(adrp_t* h);
+int adrp_persistent_end(adrp_t* h);
+
 /* Diagnostics (off by default, costs a same-address atomic per touching wave):
  * count env-steps whose sub-steps touched the plane contact model. */
 int adrp_set_diagnostics(adrp_t* h, int enable);

@@ -104,7 +104,7 @@ def alg(out_path, rest):
             rec[k]["algorithmic_flops_per_drone_step"] = per
             rec[k]["algorithmic_source"] = ("SQ_INSTS_VALU_FLOPS_* of the one-lane race_step_kernel (one lane per "
                                             "drone, no redundant lanes; ADRP_RACE_QUAD=0) on the same workload, fp32, "
-                                            "tools/pmc_r4.sh; the same algorithm in either precision")
+                                            "tools/gpu.sh pmc; the same algorithm in either precision")
         print(key, per)
     json.dump(rec, open(out_path, "w"), indent=1)
 
