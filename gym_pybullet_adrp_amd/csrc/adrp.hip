@@ -723,7 +723,8 @@ extern "C" int adrp_persistent_begin(adrp_t* h, void** act, void** obs, void** r
         off += a64(sizes[k]);
     }
     void* box = nullptr;
-    HIPCHK(h, hipHostMalloc(&box, off, hipHostMallocMapped | hipHostMallocCoherent));
+    if (hipHostMalloc(&box, off, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return seterr(h, ADRP_ERR_OOM, "adrp_persistent_begin: hipHostMalloc");
     memset(box, 0, off);
     char* dbox = nullptr;
     if (hipHostGetDevicePointer((void**)&dbox, box, 0) != hipSuccess ||

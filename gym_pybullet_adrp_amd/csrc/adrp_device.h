@@ -273,6 +273,12 @@ __device__ __forceinline__ double atan2_t(double y, double x) {
     if constexpr (NC) return __builtin_copysign(r, y);
     return __builtin_isunordered(x, y) ? x + y : __builtin_copysign(r, y);
 }
+// Correctly rounded float x / y from a float64 reciprocal of y: f64::rcp is within 2 ulp, so
+// x * rcp(y) is the quotient to 1.25 * 2^-51 relative, while an exact quotient of two floats keeps at
+// least 2^-49 relative from every float rounding boundary (significands X, Y < 2^24: |X 2^n -
+// (2k + 1) Y| is a nonzero integer), so rounding that double to float IS the IEEE float x / y.  A
+// divisor shared by several quotients pays one reciprocal (the race firmware's normalisations).
+__device__ __forceinline__ float fdiv_rcp(float x, double ry) { return float(double(x) * ry); }
 __device__ __forceinline__ double atan2(double y, double x) { return atan2_t<false>(y, x); }
 __device__ __forceinline__ double atan2_nc(double y, double x) { return atan2_t<true>(y, x); }
 // 2^(j/32), j = 0..31 (correctly rounded), the table of f64::exp_tab (the race kernel copies it to LDS)

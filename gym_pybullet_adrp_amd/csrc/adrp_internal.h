@@ -125,7 +125,6 @@ template <typename Real>
 int hover_reset(adrp_t* h, const uint8_t* mask, float* obs, hipStream_t s);
 template <typename Real>
 int hover_persist_launch(adrp_t* h, const HoverArgs<Real>& a, void* ctl, hipStream_t s);
-bool hover_persist_def(const adrp_t* h);
 template <typename Real>
 int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc, float* tobs,
               hipStream_t s);

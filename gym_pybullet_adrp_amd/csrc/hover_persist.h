@@ -31,19 +31,27 @@ struct PersistCtl {
 };
 
 // a: HoverArgs whose act / obs / rew / term / trunc / tobs point into the mapped mailbox (device
-// addresses of host memory); f / ring / ist / c / r are the handle's device buffers
+// addresses of host memory); f / ring / ist / c / r are the handle's device buffers.
+// Memory traffic with the host, per step and without a cache-wide fence (a system-scope acquire
+// would invalidate the L2 the env state lives in, a system-scope release would write it back):
+//   - the request word is read with a system-scope atomic load (it bypasses the GPU caches); the
+//     action loads of the step body are issued after the load that saw req, together with the state
+//     loads, from the coherent mapping (not cached on the GPU), where the host stored the action
+//     before it published req;
+//   - the outputs are plain stores into the same mapping; the wave waits for their completion
+//     before the done word is stored, and the host reads the outputs after it sees done.
 template <typename Real, int PH, int A, int B, bool DEF>
 __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Real> a, PersistCtl* ctl) {
     __shared__ uint32_t cmd;
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(&ctl->status, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&ctl->status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t last = 0;
     uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (threadIdx.x == 0) {
             uint32_t r;
             for (;;) {
-                r = __hip_atomic_load(&ctl->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                r = __hip_atomic_load(&ctl->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (r != last) break;
                 if (__builtin_amdgcn_s_memrealtime() - t_idle > kPersistIdleTicks) {
                     r = kPersistStop;
@@ -57,25 +65,24 @@ __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Rea
         const uint32_t r = cmd;
         __syncthreads();   // cmd is rewritten by the next poll
         if (r == kPersistStop) break;
-        // the action the host wrote before it published req: every lane's view of mapped memory fresh
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         if constexpr (DEF) {
             constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
             hover_step_body<Real, PH, A, B, C.S>(a, C);
         } else {
             hover_step_body<Real, PH, A, B, 0>(a, *a.c);
         }
-        // obs / reward / flags (mapped memory) visible to the host before done
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        // every output store of this wave completed before the block publishes done
+        __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(&ctl->done[blockIdx.x], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0) __hip_atomic_store(&ctl->done[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         last = r;
         t_idle = __builtin_amdgcn_s_memrealtime();
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // the env state the next launch / get_state reads
+    // the env state the next launch / get_state reads (kernel end releases it too)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(&ctl->status, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&ctl->status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace adrp

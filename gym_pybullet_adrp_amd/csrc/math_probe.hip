@@ -36,6 +36,7 @@ __global__ void __launch_bounds__(256) math_probe_kernel(int fn, const double* _
         case ADRP_MATH_COS_FAST: adrp::f64::sincos_fast(x, &c, &r); break;
         case ADRP_MATH_EXP_TAB: r = adrp::f64::exp_tab(x, adrp::f64::kExp2Tab32); break;
         case ADRP_MATH_ATAN2_NC: r = adrp::f64::atan2_nc(x, in[n + i]); break;
+        case ADRP_MATH_FDIV_RCP: r = adrp::f64::fdiv_rcp(float(x), adrp::f64::rcp(double(float(in[n + i])))); break;
         case ADRP_MATH_NORMAL_Z0:
         case ADRP_MATH_NORMAL_Z1: {
             const unsigned long long b = (unsigned long long)__double_as_longlong(x);
@@ -51,7 +52,7 @@ __global__ void __launch_bounds__(256) math_probe_kernel(int fn, const double* _
 }  // namespace
 
 extern "C" int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream) {
-    if (fn < ADRP_MATH_RCP || fn > ADRP_MATH_ATAN2_NC || n < 0 || (n > 0 && (!in_dev || !out_dev))) return ADRP_ERR_INVALID;
+    if (fn < ADRP_MATH_RCP || fn > ADRP_MATH_FDIV_RCP || n < 0 || (n > 0 && (!in_dev || !out_dev))) return ADRP_ERR_INVALID;
     if (n == 0) return ADRP_OK;
     hipLaunchKernelGGL(math_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, in_dev, out_dev, n);
     return hipGetLastError() == hipSuccess ? ADRP_OK : ADRP_ERR_DEVICE;

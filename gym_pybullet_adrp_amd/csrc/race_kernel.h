@@ -744,7 +744,16 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
     const float current_thrust = tx * Rz0 + ty * Rz1 + tz * Rz2;
     const float tn = FAST ? __builtin_amdgcn_sqrtf(tx * tx + ty * ty + tz * tz) : sqrtf(tx * tx + ty * ty + tz * tz);
     const float itn = FAST ? __builtin_amdgcn_rcpf(tn) : 0.0f;
-    const float zd0 = FAST ? tx * itn : tx / tn, zd1 = FAST ? ty * itn : ty / tn, zd2 = FAST ? tz * itn : tz / tn;
+    // !FAST: the C float divisions, correctly rounded through one float64 reciprocal per divisor
+    // (f64::fdiv_rcp: the same bits as x / y, a third of the instructions for three quotients)
+#ifdef ADRP_EXP_FDIV_IEEE   // measurement-only: the plain IEEE float divisions (A/B of fdiv_rcp)
+#define FDIV_(x, ry, y) ((x) / (y))
+#else
+#define FDIV_(x, ry, y) f64::fdiv_rcp((x), (ry))
+#endif
+    const double rtn = FAST ? 0.0 : f64::rcp(double(tn));
+    const float zd0 = FAST ? tx * itn : FDIV_(tx, rtn, tn), zd1 = FAST ? ty * itn : FDIV_(ty, rtn, tn),
+                zd2 = FAST ? tz * itn : FDIV_(tz, rtn, tn);
     // y_des = normalize(z_des x x_c), x_c = (cos yaw, sin yaw, 0)
     float yd0 = zd1 * 0.0f - zd2 * xc_y, yd1 = zd2 * xc_x - zd0 * 0.0f, yd2 = zd0 * xc_y - zd1 * xc_x;
     const float yn = FAST ? __builtin_amdgcn_sqrtf(yd0 * yd0 + yd1 * yd1 + yd2 * yd2) : sqrtf(yd0 * yd0 + yd1 * yd1 + yd2 * yd2);
@@ -752,7 +761,8 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
         const float iyn = __builtin_amdgcn_rcpf(yn);
         yd0 *= iyn; yd1 *= iyn; yd2 *= iyn;
     } else {
-        yd0 /= yn; yd1 /= yn; yd2 /= yn;
+        const double ryn = f64::rcp(double(yn));
+        yd0 = FDIV_(yd0, ryn, yn); yd1 = FDIV_(yd1, ryn, yn); yd2 = FDIV_(yd2, ryn, yn);
     }
     const float xd0 = yd1 * zd2 - yd2 * zd1, xd1 = yd2 * zd0 - yd0 * zd2, xd2 = yd0 * zd1 - yd1 * zd0;
     const float eRx = (zd0 * Ry0 + zd1 * Ry1 + zd2 * Ry2) - (Rz0 * yd0 + Rz1 * yd1 + Rz2 * yd2);
@@ -762,10 +772,12 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
     const float ewx = radf_(spr) - rate_roll, ewy = -radf_(spp) - rate_pitch, ewz = radf_(spy) - rate_yaw;
     float err_d_roll = 0, err_d_pitch = 0;
     if (d.pw_roll == d.pw_roll) {
+        // !FAST: x / dt as fdiv_rcp by the correctly rounded float64 1 / dt (2^-52 relative: exact too)
+        constexpr double kInvDt = 1.0 / double(float(1.0f / 500));
         err_d_roll = FAST ? ((radf_(spr) - d.psp_roll) - (rate_roll - d.pw_roll)) * 500.0f
-                          : ((radf_(spr) - d.psp_roll) - (rate_roll - d.pw_roll)) / dt;
+                          : FDIV_((radf_(spr) - d.psp_roll) - (rate_roll - d.pw_roll), kInvDt, dt);
         err_d_pitch = FAST ? (-(radf_(spp) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) * 500.0f
-                           : (-(radf_(spp) - d.psp_pitch) - (rate_pitch - d.pw_pitch)) / dt;
+                           : FDIV_(-(radf_(spp) - d.psp_pitch) - (rate_pitch - d.pw_pitch), kInvDt, dt);
     }
     d.pw_roll = rate_roll;
     d.pw_pitch = rate_pitch;
@@ -792,6 +804,7 @@ __device__ __forceinline__ void mellinger_fw(RDrone<Real>& d, const float sp[3],
         d.ierrm[k] = on ? d.ierrm[k] : 0.0f;
     }
 }
+#undef FDIV_
 
 // MellingerControl.computeControl (154-262) -> rpm (float64 wrapper arithmetic in Real)
 // CMD: command mode (commander.h) — _update_state into cs->st_*, and while the commander drives

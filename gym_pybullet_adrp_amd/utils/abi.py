@@ -19,7 +19,7 @@ MATH_RCP, MATH_RSQ, MATH_SQRT, MATH_SIN_SMALL, MATH_COS_SMALL, MATH_ATAN2, MATH_
 MATH_SQRT_NN, MATH_RCP_NC, MATH_RSQ_NC, MATH_SIN_TINY, MATH_COS_TINY = 8, 9, 10, 11, 12
 MATH_EXPMAP_SINC, MATH_EXPMAP_COS, MATH_QUAT_INV_NORM, MATH_NORMAL_Z0, MATH_NORMAL_Z1 = 13, 14, 15, 16, 17
 MATH_DIVC, MATH_SIN_FAST, MATH_COS_FAST = 18, 19, 20
-MATH_EXP_TAB, MATH_ATAN2_NC = 21, 22
+MATH_EXP_TAB, MATH_ATAN2_NC, MATH_FDIV_RCP = 21, 22, 23
 RACE_COMPARE, RACE_COMPETE = 0, 1
 POLICY_TANH, POLICY_RELU = 0, 1
 POLICY_RAW, POLICY_RELATIVE, POLICY_ABSOLUTE = 0, 1, 2

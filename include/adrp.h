@@ -417,6 +417,7 @@ int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_d
 #define ADRP_MATH_COS_FAST 20
 #define ADRP_MATH_EXP_TAB 21       /* exp(x), x <= 0, table form of the fp64 race downwash */
 #define ADRP_MATH_ATAN2_NC 22      /* atan2(in[i], in[n + i]) for finite operands (race Euler angles) */
+#define ADRP_MATH_FDIV_RCP 23      /* float(in[i]) / float(in[n + i]) as the fp64 race firmware divides (f64::fdiv_rcp) */
 int adrp_math_probe(int fn, const double* in_dev, double* out_dev, int n, void* stream);
 
 #ifdef __cplusplus

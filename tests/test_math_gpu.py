@@ -209,3 +209,34 @@ def test_sincos_fast():
         err = np.abs(got.astype(L) - ref)
         assert (err <= np.maximum(np.abs(ref) * L(2.0 ** -51), L(2.0 ** -52))).all(), float(err.max())
     assert s[-6] == 0.0 and c[-6] == 1.0
+
+
+def test_fdiv_rcp_is_ieee_float_division():
+    """f64::fdiv_rcp (the fp64 race firmware's float divisions, race_kernel.h mellinger_fw): rounding
+    x * rcp(y) to float is the IEEE float x / y bit for bit.  4M quotients: random bit patterns over
+    the whole normal range (both signs), quotients near float rounding boundaries (y a float just off
+    a power of two, x with all-ones / alternating significands), the firmware's own scales (norms of
+    target / y_des vectors, D terms by dt = 0.002f)"""
+    rng = np.random.default_rng(23)
+    n = 1 << 20
+
+    def rand_f32(k, lo_exp=-60, hi_exp=60):
+        m = rng.integers(0, 1 << 23, k, dtype=np.uint32)
+        e = rng.integers(127 + lo_exp, 127 + hi_exp, k).astype(np.uint32)
+        s = rng.integers(0, 2, k, dtype=np.uint32) << 31
+        return (s | (e << 23) | m).view(np.float32)
+    xs = [rand_f32(n), rand_f32(n, -3, 3), rng.uniform(-3, 3, n).astype(np.float32)]
+    ys = [rand_f32(n), rand_f32(n, -3, 3), rng.uniform(0.05, 3, n).astype(np.float32)]
+    # adversarial: y = 2^k (1 + j ulp) with small j, x with long runs of ones in the significand
+    j = rng.integers(1, 64, n).astype(np.uint32)
+    y_adv = ((np.uint32(127) << 23) + j).view(np.float32) * np.float32(2.0) ** rng.integers(-4, 4, n).astype(np.float32)
+    x_adv = ((np.uint32(127) << 23) | (np.uint32((1 << 23) - 1) ^ rng.integers(0, 8, n, dtype=np.uint32))).view(np.float32)
+    xs.append(x_adv)
+    ys.append(y_adv)
+    xs.append(rng.uniform(-50, 50, n).astype(np.float32))
+    ys.append(np.full(n, np.float32(1.0) / np.float32(500), np.float32))
+    for x, y in zip(xs, ys):
+        got = probe(abi.MATH_FDIV_RCP, x.astype(np.float64), y.astype(np.float64)).astype(np.float32)
+        ref = x / y
+        bad = np.flatnonzero(got.view(np.uint32) != ref.view(np.uint32))
+        assert len(bad) == 0, f"{len(bad)} quotients differ, e.g. {x[bad[:4]]} / {y[bad[:4]]}: {got[bad[:4]]} vs {ref[bad[:4]]}"

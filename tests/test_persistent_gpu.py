@@ -16,9 +16,13 @@ from gym_pybullet_adrp_amd.envs.hover import HoverAviary  # noqa: E402
 from gym_pybullet_adrp_amd.utils.enums import ActionType, Physics  # noqa: E402
 
 
-def _pair(E, precision, physics=Physics.PYB, act=ActionType.RPM):
+def _pair(E, precision, physics=Physics.PYB, act=ActionType.RPM, monkeypatch=None):
+    """the launched env on the row-store step kernel (the template the persistent kernel runs: the
+    LDS-staged variant, chosen at E % 64 == 0, may contract a * b + c differently, 1-ulp differences,
+    test_hover_gpu.test_reset_helper_same_results), and its persistent twin"""
     kw = dict(num_envs=E, physics=physics, act=act, precision=precision, seed=31, initial_xyzs=[0, 0, 1.0],
               init_noise={"xyz": 0.1, "rpy": 0.2, "vel": 0.3, "omega": 1.0})
+    monkeypatch.setenv("ADRP_STAGE_ROWS", "0")   # (both: b also steps by launch after its persistent run)
     return HoverAviary(**kw), HoverAviary(**kw)
 
 
@@ -27,8 +31,8 @@ def _pair(E, precision, physics=Physics.PYB, act=ActionType.RPM):
                                            (128, Physics.PYB, ActionType.RPM),
                                            (70, Physics.PYB_GND_DRAG_DW, ActionType.ONE_D_RPM),
                                            (3, Physics.DYN, ActionType.RPM)])
-def test_persistent_bit_identical_to_launched(E, physics, act, precision):
-    a, b = _pair(E, precision, physics, act)
+def test_persistent_bit_identical_to_launched(monkeypatch, E, physics, act, precision):
+    a, b = _pair(E, precision, physics, act, monkeypatch)
     a.reset()
     b.reset()
     A = a.h.A
