@@ -280,7 +280,7 @@ static bool race_is_cf2x(const RaceConst<Real>& rt) {
     ADRP_SAME(gnd_kf); ADRP_SAME(prop_r4); ADRP_SAME(gnd_clip); ADRP_SAME(drag);
     ADRP_SAME(dw1); ADRP_SAME(dw2); ADRP_SAME(dw3); ADRP_SAME(prop_r);
     ADRP_SAME(dyn_mass); ADRP_SAME(dyn_inv_mass); ADRP_SAME(dyn_i); ADRP_SAME(dyn_inv_i); ADRP_SAME(dyn_arm);
-    ADRP_SAME(coll_hh); ADRP_SAME(coll_r); ADRP_SAME(coll_zoff); ADRP_SAME(ang_max);
+    ADRP_SAME(coll_hh); ADRP_SAME(coll_r); ADRP_SAME(coll_zoff); ADRP_SAME(ang_max); ADRP_SAME(link_lag);
 #undef ADRP_SAME
     return same;
 }
@@ -313,7 +313,10 @@ extern "C" const char* adrp_kernel_name(const adrp_config* cfg) {
     if (cfg->task == ADRP_TASK_RACE) {
         const char* q = getenv("ADRP_RACE_QUAD");
         const bool cf2x = cfg->precision ? race_is_cf2x(race_const<double>(*cfg)) : race_is_cf2x(race_const<float>(*cfg));
-        const bool quad = !(q && atoi(q) == 0) && (cf2x || !cfg->precision);
+        const char* pd = getenv("ADRP_RACE_PREDRAW");
+        const int S = cfg->ctrl_freq > 0 ? cfg->pyb_freq / cfg->ctrl_freq : 0;
+        const bool quad = !(q && atoi(q) == 0) && (cf2x || !cfg->precision) &&
+                          !(cfg->track.disturbances && (S > kRacePreS || (pd && atoi(pd) == 0)));
         snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s>", cfg->precision ? "f64" : "f32", ph[p],
                  race_group(cfg->num_drones), quad ? ",Q4" : "");
         return buf;
@@ -347,7 +350,7 @@ extern "C" const char* adrp_handle_kernel_name(const adrp_t* h) {
     const char* prec = h->real_size == 8 ? "f64" : "f32";
     if (h->cmdf) snprintf(buf, sizeof buf, "race_step<%s,%s,G8,CMD>", prec, ph[p]);
     else snprintf(buf, sizeof buf, "race_step<%s,%s,G%d%s>", prec, ph[p], race_group(h->N),
-                  h->race_quad && (h->race_cf2x || h->real_size == 4) ? ",Q4" : "");
+                  race_quad_ok(h) ? ",Q4" : "");
     return buf;
 }
 

@@ -70,6 +70,16 @@ constexpr int kBlock = kStepBlock;
 
 inline int race_group(int n) { return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : 8; }
 
+// the four-lane race kernel (race_quad.h) runs a handle when: it is not switched off
+// (ADRP_RACE_QUAD=0); fp64 only for the reference drone (compiled-in constants, race_is_cf2x);
+// disturbances, if on, drawn up front (S <= kRacePreS, ADRP_RACE_PREDRAW not 0); no parity-mode
+// injection (adrp_set_noise).  Every other handle runs the one-lane kernel (race_kernel.h), which
+// covers all of these with the same arithmetic (test_quad_matches_lane).
+inline bool race_quad_ok(const adrp_t* h) {
+    return h->race_quad && (h->race_cf2x || h->real_size == 4) && !h->inj_force &&
+           !(h->cfg.track.disturbances && (h->S > kRacePreS || !h->race_predraw));
+}
+
 // HoverAviary action width (BaseRLAviary._actionSpace, BaseRLAviary.py:141-147) and whether the
 // action type runs the fused DSLPIDControl
 inline bool hover_has_pid(int t) { return t == ADRP_ACT_PID || t == ADRP_ACT_VEL || t == ADRP_ACT_ONE_D_PID; }

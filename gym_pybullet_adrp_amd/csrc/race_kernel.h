@@ -120,6 +120,7 @@ __host__ __device__ constexpr void race_cf2x_phys(RaceConst<Real>& k) {
     k.dyn_arm = Real(0.028072139213105935);
     k.coll_hh = Real(0.5 * 0.025); k.coll_r = Real(0.06); k.coll_zoff = Real(0);
     k.ang_max = Real(0.5 * (3.14159265358979323846 / 2) * 500);
+    k.link_lag = 1;   // link_frame_lag: the reference's cached link basis (deviation 2)
 }
 
 // nominal attitude of drone k (RaceConst::nom_q / nom_rpy)
@@ -563,8 +564,10 @@ __device__ __forceinline__ Real ld(const Real* f, int field, size_t EN, size_t s
 template <typename Real>
 __device__ __forceinline__ void st(Real* f, int field, size_t EN, size_t slot, Real v) { f[size_t(field) * EN + slot] = v; }
 
-// TW: also load the tick-schedule window (a caller that issued it early passes false and sets it)
-template <typename Real, bool TW = true>
+// TW: also load the tick-schedule window (a caller that issued it early passes false and sets it);
+// ANGV: load the DYN world angular velocity (the other physics modes never change it: the four-lane
+// kernel then neither loads nor stores it, so it holds no registers through the sub-steps)
+template <typename Real, bool TW = true, bool ANGV = true>
 __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, size_t slot, RDrone<Real>& d) {
     const Real* f = a.f;
 #define L_(k) ld(f, (k), EN, slot)
@@ -572,7 +575,8 @@ __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, s
     d.q = {L_(RF_QUAT), L_(RF_QUAT + 1), L_(RF_QUAT + 2), L_(RF_QUAT + 3)};
     d.vel = v3(L_(RF_VEL), L_(RF_VEL + 1), L_(RF_VEL + 2));
     d.w = v3(L_(RF_OMEGA), L_(RF_OMEGA + 1), L_(RF_OMEGA + 2));
-    d.angv = v3(L_(RF_ANGV), L_(RF_ANGV + 1), L_(RF_ANGV + 2));
+    if constexpr (ANGV) d.angv = v3(L_(RF_ANGV), L_(RF_ANGV + 1), L_(RF_ANGV + 2));
+    else d.angv = v3(Real(0), Real(0), Real(0));
     d.ql = {L_(RF_LINK_QUAT), L_(RF_LINK_QUAT + 1), L_(RF_LINK_QUAT + 2), L_(RF_LINK_QUAT + 3)};
     d.lpos = v3(L_(RF_LINK_POS), L_(RF_LINK_POS + 1), L_(RF_LINK_POS + 2));
     d.kpos = v3(L_(RF_KIN_POS), L_(RF_KIN_POS + 1), L_(RF_KIN_POS + 2));
@@ -606,7 +610,7 @@ __device__ __forceinline__ void load_drone(const RaceArgs<Real>& a, size_t EN, s
 // store_drone split in two for the four-lane kernel: everything the sub-step loop leaves final
 // (stored right after the loop, so those registers are free for the post-loop queries), then the
 // gate / flags the post-loop phases still change
-template <typename Real>
+template <typename Real, bool ANGV = true>
 __device__ __forceinline__ void store_drone_body(const RaceArgs<Real>& a, size_t EN, size_t slot, const RDrone<Real>& d) {
     Real* f = a.f;
 #define S_(k, v) st(f, (k), EN, slot, Real(v))
@@ -614,7 +618,7 @@ __device__ __forceinline__ void store_drone_body(const RaceArgs<Real>& a, size_t
     S_(RF_QUAT, d.q.x); S_(RF_QUAT + 1, d.q.y); S_(RF_QUAT + 2, d.q.z); S_(RF_QUAT + 3, d.q.w);
     S_(RF_VEL, d.vel.x); S_(RF_VEL + 1, d.vel.y); S_(RF_VEL + 2, d.vel.z);
     S_(RF_OMEGA, d.w.x); S_(RF_OMEGA + 1, d.w.y); S_(RF_OMEGA + 2, d.w.z);
-    S_(RF_ANGV, d.angv.x); S_(RF_ANGV + 1, d.angv.y); S_(RF_ANGV + 2, d.angv.z);
+    if constexpr (ANGV) { S_(RF_ANGV, d.angv.x); S_(RF_ANGV + 1, d.angv.y); S_(RF_ANGV + 2, d.angv.z); }
     S_(RF_LINK_QUAT, d.ql.x); S_(RF_LINK_QUAT + 1, d.ql.y); S_(RF_LINK_QUAT + 2, d.ql.z); S_(RF_LINK_QUAT + 3, d.ql.w);
     S_(RF_LINK_POS, d.lpos.x); S_(RF_LINK_POS + 1, d.lpos.y); S_(RF_LINK_POS + 2, d.lpos.z);
     S_(RF_KIN_POS, d.kpos.x); S_(RF_KIN_POS + 1, d.kpos.y); S_(RF_KIN_POS + 2, d.kpos.z);

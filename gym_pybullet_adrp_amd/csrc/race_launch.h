@@ -11,7 +11,7 @@ constexpr bool kQuadDef = sizeof(Real) == 8;
 // four lanes per drone (race_quad.h): 16 drones per 64-lane block
 template <typename Real, int PH>
 static void launch_race_q4(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
-    const bool draws = h->cfg.track.disturbances && h->S <= kRacePreS && h->race_predraw;
+    const bool draws = h->cfg.track.disturbances;   // (race_quad_ok: then drawn up front)
     const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G * 4 + kRaceBlock - 1) / kRaceBlock));
     auto go = [&](auto kernel) {
         if (h->prof_n < h->prof_cap) {
@@ -56,7 +56,7 @@ static void launch_race_g(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t*
     if (h->cmdf) return launch_race_cmd<Real, PH>(a, s, h);
     // the fp64 four-lane kernel has the reference drone's physical constants compiled in: another
     // drone (or PYB_FREQ) runs the one-lane kernel there
-    if (h->race_quad && (h->race_cf2x || !kQuadDef<Real>)) return launch_race_q4<Real, PH>(a, G, s, h);
+    if (race_quad_ok(h)) return launch_race_q4<Real, PH>(a, G, s, h);
     // kRaceBlock drone lanes, + kRaceHelpers helper waves per block in the fp32 kernel (the track
     // copy into LDS, and the sub-step draws with disturbances on; race_kernel.h)
     const int helpers = sizeof(Real) != 4 || !h->race_helpers ? 0

@@ -213,6 +213,8 @@ __device__ __forceinline__ void mellinger_q4(RDrone<Real>& d, const Lpf& lpf, co
         CP_ADD(2, m2 - m1);
         d.tick += 1;
         // _compute_pwms (423-442), motor ql of [t-r+p+y, t-r-p-y, t+r-p+y, t+r+p-y]
+        // (reusing the thrust between firmware calls, where control_t is unchanged, measured slower:
+        // config 4 fp64 69.5 -> 73.8 us, config 3 47.1 -> 49.8 us, A/B round 5)
         const Real r = Real(d.ctl[0]) / Real(2), p = Real(d.ctl[1]) / Real(2), y = Real(d.ctl[2]), th = Real(d.ctl[3]);
         const Real m = ((th + (ql < 2 ? -r : r)) + ((ql == 0 || ql == 3) ? p : -p)) + ((ql & 1) ? -y : y);
         const Real x = F32 ? clampr_(m, Real(0), Real(65535)) * Real(60.0 / 65535)
@@ -470,28 +472,46 @@ struct ResetToHBM {
             st(a->f, RF_WR_PREV + k, EN, slot, prv[k]);
         }
     }
-    __device__ __forceinline__ void drone(size_t EN, size_t slot, const RDrone<Real>& d, int episode) const {
-        store_drone(*a, EN, slot, d, true);
-        a->ist[RI_STEP * EN + slot] = 0;
-        a->ist[RI_EPISODE * EN + slot] = episode + 1;
-        a->ist[RI_WR_GATE * EN + slot] = 0;
+    // the reset drone's state (store_drone(params = true) of the RDrone race_reset_lane builds), field
+    // by field from its values: an RDrone aggregate here went to scratch memory (~500 B per lane stored
+    // and reloaded on the resetting wave)
+    __device__ __forceinline__ void drone(size_t EN, size_t slot, V3<Real> pos, Q4<Real> q, V3<Real> vel, V3<Real> w,
+                                          V3<Real> angv, V3<Real> kpos, V3<Real> prpy, Real mass, const Real inertia[3],
+                                          int episode) const {
+        Real* f = a->f;
+#define S_(k, v) st(f, (k), EN, slot, Real(v))
+        S_(RF_POS, pos.x); S_(RF_POS + 1, pos.y); S_(RF_POS + 2, pos.z);
+        S_(RF_QUAT, q.x); S_(RF_QUAT + 1, q.y); S_(RF_QUAT + 2, q.z); S_(RF_QUAT + 3, q.w);
+        S_(RF_VEL, vel.x); S_(RF_VEL + 1, vel.y); S_(RF_VEL + 2, vel.z);
+        S_(RF_OMEGA, w.x); S_(RF_OMEGA + 1, w.y); S_(RF_OMEGA + 2, w.z);
+        S_(RF_ANGV, angv.x); S_(RF_ANGV + 1, angv.y); S_(RF_ANGV + 2, angv.z);
+        S_(RF_LINK_QUAT, q.x); S_(RF_LINK_QUAT + 1, q.y); S_(RF_LINK_QUAT + 2, q.z); S_(RF_LINK_QUAT + 3, q.w);
+        S_(RF_LINK_POS, pos.x); S_(RF_LINK_POS + 1, pos.y); S_(RF_LINK_POS + 2, pos.z);
+        S_(RF_KIN_POS, kpos.x); S_(RF_KIN_POS + 1, kpos.y); S_(RF_KIN_POS + 2, kpos.z);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { S_(RF_RPM + k, 0); S_(RF_PREV_RPM + k, 0); S_(RF_CTL + k, 0); }
+        const Real pr[3] = {prpy.x, prpy.y, prpy.z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            S_(RF_PREV_RPY + k, pr[k]); S_(RF_PREV_VEL + k, 0);
+            S_(RF_LPF_D1 + k, 0); S_(RF_LPF_D2 + k, 0);
+            S_(RF_I_ERR + k, 0); S_(RF_I_ERR_M + k, 0);
+        }
+        const Real nan = Real(__builtin_nanf(""));   // D-term memory: no D term on the first call
+        S_(RF_PREV_OMEGA_ROLL, nan); S_(RF_PREV_OMEGA_PITCH, nan);
+        S_(RF_PREV_SP_ROLL, 0); S_(RF_PREV_SP_PITCH, 0);
+        S_(RF_MASS, mass);
+        S_(RF_INERTIA, inertia[0]); S_(RF_INERTIA + 1, inertia[1]); S_(RF_INERTIA + 2, inertia[2]);
+#undef S_
+        int32_t* ist = a->ist;
+        ist[RI_TICK * EN + slot] = 0; ist[RI_LAST_ATT * EN + slot] = 0;
+        ist[RI_LAST_POS * EN + slot] = 0; ist[RI_TUMBLE * EN + slot] = 0;
+        ist[RI_GATE * EN + slot] = 0; ist[RI_FLAGS * EN + slot] = 0;
+        ist[RI_STEP * EN + slot] = 0;
+        ist[RI_EPISODE * EN + slot] = episode + 1;
+        ist[RI_WR_GATE * EN + slot] = 0;
     }
 };
-
-// the reset state a race_reset_q4 leaves in an RDrone besides its non-constant values
-template <typename Real>
-__device__ __forceinline__ void reset_drone_constants(RDrone<Real>& d) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        d.prev_vel[k] = Real(0); d.lpf1[k] = d.lpf2[k] = 0.0f; d.ierr[k] = d.ierrm[k] = 0.0f;
-    }
-    d.tick = d.last_att = d.last_pos = d.tumble = 0;
-    d.pw_roll = d.pw_pitch = __builtin_nanf("");
-    d.psp_roll = d.psp_pitch = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { d.ctl[k] = 0.0f; d.rpm[k] = d.prev[k] = Real(0); }
-    d.gate = 0; d.flags = 0;
-}
 
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RESET_PHASES)
 // measurement-only (tools/race_phases.py with a -DADRP_RESET_PHASES timing build): s_memtime marks
@@ -616,19 +636,16 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
         }
         out.wrapper(EN, slot, tgt, prv);
     }
-    RDrone<Real> d;
-    d.prev_rpy[0] = nrpy.x; d.prev_rpy[1] = nrpy.y; d.prev_rpy[2] = nrpy.z;
-    reset_drone_constants(d);
-    d.mass = C.race_mass;
-    d.inertia[0] = C.race_inertia[0]; d.inertia[1] = C.race_inertia[1]; d.inertia[2] = C.race_inertia[2];
+    Real mass = C.race_mass;
+    Real inertia[3] = {C.race_inertia[0], C.race_inertia[1], C.race_inertia[2]};
     if (C.random_inertia) {
-        Real v[4] = {d.mass, d.inertia[0], d.inertia[1], d.inertia[2]};
+        Real v[4] = {mass, inertia[0], inertia[1], inertia[2]};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const Real lo = C.inertia_off[k][0], hi = C.inertia_off[k][1];
             v[k] = clampr_(v[k] + lo + (hi - lo) * uq[2][k], Real(0), Real(100));
         }
-        d.mass = v[0]; d.inertia[0] = v[1]; d.inertia[1] = v[2]; d.inertia[2] = v[3];
+        mass = v[0]; inertia[0] = v[1]; inertia[1] = v[2]; inertia[2] = v[3];
     }
     Real po[3] = {0, 0, 0}, ro[3] = {0, 0, 0};
     if (C.random_state) {
@@ -638,16 +655,13 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
             ro[k] = C.rot_off[k][0] + (C.rot_off[k][1] - C.rot_off[k][0]) * uq[1][k];
         }
     }
-    d.pos = v3(npos.x + po[0], npos.y + po[1], npos.z + po[2]);
-    d.q = quat_from_euler_fast(C.init_rpy[dn][0] + ro[0], C.init_rpy[dn][1] + ro[1], C.init_rpy[dn][2] + ro[2]);
-    d.vel = v3(C.init_vel[dn][0], C.init_vel[dn][1], C.init_vel[dn][2]);
-    d.w = v3(C.init_pqr[dn][0], C.init_pqr[dn][1], C.init_pqr[dn][2]);
-    d.angv = d.w;
-    if (C.physics == ADRP_PHYS_DYN) d.w = v3(Real(0), Real(0), Real(0));   // rpy_rates zeroed by _housekeeping
-    d.ql = d.q;
-    d.lpos = d.pos;
-    d.kpos = C.physics == ADRP_PHYS_PYB ? npos : d.pos;   // self.pos: nominal until the first read
-    out.drone(EN, slot, d, episode);
+    const V3<Real> pos = v3(npos.x + po[0], npos.y + po[1], npos.z + po[2]);
+    const Q4<Real> q = quat_from_euler_fast(C.init_rpy[dn][0] + ro[0], C.init_rpy[dn][1] + ro[1], C.init_rpy[dn][2] + ro[2]);
+    const V3<Real> w0 = v3(C.init_pqr[dn][0], C.init_pqr[dn][1], C.init_pqr[dn][2]);
+    const V3<Real> w = C.physics == ADRP_PHYS_DYN ? v3(Real(0), Real(0), Real(0)) : w0;   // rpy_rates zeroed by _housekeeping
+    const V3<Real> kpos = C.physics == ADRP_PHYS_PYB ? npos : pos;   // self.pos: nominal until the first read
+    out.drone(EN, slot, pos, q, v3(C.init_vel[dn][0], C.init_vel[dn][1], C.init_vel[dn][2]), w, w0, kpos, nrpy, mass,
+              inertia, episode);
     RESET_MARK(8);
 }
 
@@ -761,7 +775,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         if (k < kTrackFields) trk_lds[k * kQuadDrones + qd] = ld(a.f, RF_GATE + k, EN, slot);
     }
     RDrone<Real> d;
-    load_drone<Real, false>(a, EN, slot, d);
+    load_drone<Real, false, PH == ADRP_PHYS_DYN>(a, EN, slot, d);   // (angv: only DYN changes it)
     d.tick_base = tick0;
     d.att_bits = att0;
     d.pos_bits = pos0;
@@ -778,19 +792,18 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
         xc_y = sinf(radf_(yaw_deg));
     }
     const Lpf lpf = {CG.lpf[0], CG.lpf[1], CG.lpf[2], CG.lpf[3], CG.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
-    const bool inj = a.inj_force != nullptr;   // parity mode: the caller's draws, read in the loop
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
     if (threadIdx.x == 0) g_gjk_wave_iters = 0;
 #endif
     if constexpr (!DRAWS && kDwF64) __syncthreads();   // the exp table (DRAWS: the barrier below)
     if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
-        if (!inj) quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
+        quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
         __syncthreads();
 #ifdef ADRP_EXP_DUP_DRAWS
         {
             uint32_t ep2 = ep;
             exp_dep(ep2, pre_draws[tl]);
-            if (!inj) quad_draws<Real>(H, pre_draws, a.seed, gid, ep2, dn, sc0, ql, qd, H.S);
+            quad_draws<Real>(H, pre_draws, a.seed, gid, ep2, dn, sc0, ql, qd, H.S);
             __syncthreads();
         }
 #endif
@@ -816,7 +829,6 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
 #ifdef ADRP_RACE_TIMING
         RACE_MARK(ta);
 #endif
-        const uint32_t idx = uint32_t(sc0 + s);
         if (PH != ADRP_PHYS_PYB) d.kpos = d.pos;
         Real noise_m = Real(0);
         if constexpr (PH == ADRP_PHYS_DYN) {
@@ -860,37 +872,20 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
                 Fx = fz * col2(Rs);
               }
             }
-#ifdef ADRP_EXP_NODIST
-            if (false) {
-#else
-            if (H.disturbances) {
-#endif
+            // disturbances: compile-time (the host runs this kernel with DRAWS = disturbances on and
+            // the draws made up front; parity-mode injection and in-loop draws go to the one-lane
+            // kernel), so no uniform branch splits the sub-step
+            if constexpr (DRAWS) {
                 V3<Real> fd;
-                if (inj) {
-                    Real f3[3], nz[4];
-                    injected_draws(a, slot, H.S, s, f3, nz);
-                    fd = v3(f3[0], f3[1], f3[2]);
-                    noise_m = nz[0];
-#pragma unroll
-                    for (int k = 1; k < 4; ++k) noise_m = ql == k ? nz[k] : noise_m;
-                } else if constexpr (DRAWS) {
-                    const float* src = pre_draws + s * 7 * kQuadDrones + qd;
-                    if constexpr (F32) {
-                        fd = v3(src[0], src[kQuadDrones], src[2 * kQuadDrones]);
-                        noise_m = src[(3 + ql) * kQuadDrones];
-                    } else {   // race_substep_draws' arithmetic on the stored uniforms / samples
-                        fd = v3(H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * Real(src[0]),
-                                H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * Real(src[kQuadDrones]),
-                                H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * Real(src[2 * kQuadDrones]));
-                        noise_m = Real(src[(3 + ql) * kQuadDrones]) * H.noise_std;
-                    }
-                } else {
-                    Real f3[3], nz[4];
-                    race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, nz);
-                    fd = v3(f3[0], f3[1], f3[2]);
-                    noise_m = nz[0];
-#pragma unroll
-                    for (int k = 1; k < 4; ++k) noise_m = ql == k ? nz[k] : noise_m;
+                const float* src = pre_draws + s * 7 * kQuadDrones + qd;
+                if constexpr (F32) {
+                    fd = v3(src[0], src[kQuadDrones], src[2 * kQuadDrones]);
+                    noise_m = src[(3 + ql) * kQuadDrones];
+                } else {   // race_substep_draws' arithmetic on the stored uniforms / samples
+                    fd = v3(H.dist_lo[0] + (H.dist_hi[0] - H.dist_lo[0]) * Real(src[0]),
+                            H.dist_lo[1] + (H.dist_hi[1] - H.dist_lo[1]) * Real(src[kQuadDrones]),
+                            H.dist_lo[2] + (H.dist_hi[2] - H.dist_lo[2]) * Real(src[2 * kQuadDrones]));
+                    noise_m = Real(src[(3 + ql) * kQuadDrones]) * H.noise_std;
                 }
                 const V3<Real> lo = (PH == ADRP_PHYS_PYB_GND || PH == ADRP_PHYS_PYB_GND_DRAG_DW) ? d.pos : d.lpos;
                 Fx = Fx + fd;
@@ -954,7 +949,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     // tools/gpu_r3_t21.sh)
     constexpr bool kEarlyStore = !F32;   // (fp32 early store re-measured round 4: +0.3 us)
     if constexpr (kEarlyStore) {
-        if (owner) store_drone_body(a, EN, slot, d);
+        if (owner) store_drone_body<Real, PH == ADRP_PHYS_DYN>(a, EN, slot, d);
     }
     __syncthreads();
     const TrackSrcQ<Real> T{trk_lds, qd};
@@ -1121,7 +1116,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
             a.trunc[e] = tr;
         }
         if (!reset) {
-            if constexpr (!kEarlyStore) store_drone_body(a, EN, slot, d);
+            if constexpr (!kEarlyStore) store_drone_body<Real, PH == ADRP_PHYS_DYN>(a, EN, slot, d);
             store_drone_flags(a, EN, slot, d);
             a.ist[RI_STEP * EN + slot] = sc0 + C.S;
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
