@@ -541,7 +541,9 @@ __device__ __forceinline__ void stage_row(float4* lds_row, const float o12[12], 
 // of the first wave's envs (3 Philox draws, quaternion, Euler obs: ~1/4 of a wave's instruction
 // stream at E = 4096, where nearly every wave has a done lane) on another SIMD, into LDS; the
 // chain wave, issue-bound at one instruction per 4 cycles, only copies it for its done lanes.
-template <typename Real, int PH, int A, int B, int SC, bool STG = false, int CTL = 0, bool HELP = false>
+// SYS: the action rows live in host-mapped memory written by the host while the kernel runs
+// (hover_persist.h): they are read with system-scope loads, which no GPU cache serves.
+template <typename Real, int PH, int A, int B, int SC, bool STG = false, int CTL = 0, bool HELP = false, bool SYS = false>
 __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const HoverConst<Real>& C) {
     constexpr int BR = B > 0 ? B : 1;
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
@@ -618,7 +620,12 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     RACE_MARK(t0);
     // ---- issue every load up front: action, the whole ring, ints, state ----
     float act[A];
-    if constexpr (A == 4) {
+    if constexpr (SYS) {
+        uint32_t* sa = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(a.act)) + size_t(e) * A;
+#pragma unroll
+        for (int j = 0; j < A; ++j)
+            act[j] = __uint_as_float(__hip_atomic_load(sa + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    } else if constexpr (A == 4) {
         const float4 v = reinterpret_cast<const float4*>(a.act)[e];
         act[0] = v.x; act[1] = v.y; act[2] = v.z; act[3] = v.w;
     } else {

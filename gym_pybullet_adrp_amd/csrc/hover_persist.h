@@ -34,12 +34,14 @@ struct PersistCtl {
 // addresses of host memory); f / ring / ist / c / r are the handle's device buffers.
 // Memory traffic with the host, per step and without a cache-wide fence (a system-scope acquire
 // would invalidate the L2 the env state lives in, a system-scope release would write it back):
-//   - the request word is read with a system-scope atomic load (it bypasses the GPU caches); the
-//     action loads of the step body are issued after the load that saw req, together with the state
-//     loads, from the coherent mapping (not cached on the GPU), where the host stored the action
-//     before it published req;
-//   - the outputs are plain stores into the same mapping; the wave waits for their completion
-//     before the done word is stored, and the host reads the outputs after it sees done.
+//   - the request word and the action rows are read with system-scope atomic loads (no GPU cache
+//     serves them); the action loads are issued after the load that saw req, and the host stored
+//     the action before it published req;
+//   - the outputs are plain stores into the same mapping; every wave waits for their completion,
+//     then one lane per block runs a system-scope release (an L2 write-back: the env state lines
+//     become clean, they are not evicted) and stores done; the host reads the outputs after it
+//     sees done.  Without the release the done word could reach host memory before the last
+//     output rows (seen once in the E = 70 bit-identity test: 69 stale obs words at step 1).
 template <typename Real, int PH, int A, int B, bool DEF>
 __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Real> a, PersistCtl* ctl) {
     __shared__ uint32_t cmd;
@@ -67,14 +69,21 @@ __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Rea
         if (r == kPersistStop) break;
         if constexpr (DEF) {
             constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
-            hover_step_body<Real, PH, A, B, C.S>(a, C);
+            hover_step_body<Real, PH, A, B, C.S, false, 0, false, true>(a, C);
         } else {
-            hover_step_body<Real, PH, A, B, 0>(a, *a.c);
+            hover_step_body<Real, PH, A, B, 0, false, 0, false, true>(a, *a.c);
         }
-        // every output store of this wave completed before the block publishes done
-        __builtin_amdgcn_s_waitcnt(0);
+        // every output store of every wave has completed, then ONE system-scope release makes them
+        // visible to the host before done: a completed store is not yet a visible one (the flag can
+        // overtake plain stores on their way to host memory).  The inline waits are invisible to
+        // the compiler, which otherwise drops the wait after the release's write-back.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(&ctl->done[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&ctl->done[blockIdx.x], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         last = r;
         t_idle = __builtin_amdgcn_s_memrealtime();
     }
