@@ -87,6 +87,8 @@ def load():
     lib.adrp_persistent_end.restype = I
     lib.adrp_race_moment_hash.argtypes = [P, P, ctypes.c_size_t]
     lib.adrp_race_moment_hash.restype = I
+    lib.adrp_race_reset_counts.argtypes = [P, P, I]
+    lib.adrp_race_reset_counts.restype = I
     lib.adrp_policy_create.argtypes = [I, I, I, I, I, P, P, P, P, P, P, ctypes.POINTER(P)]
     lib.adrp_policy_create.restype = I
     lib.adrp_policy_act.argtypes = [P, P, I, I, I, P, P]
@@ -292,6 +294,15 @@ class Handle:
         self._check(self.lib.adrp_race_moment_hash(self.h, out.ctypes.data_as(ctypes.c_void_p), out.size),
                     "adrp_race_moment_hash")
         return out
+
+    def reset_counts(self, reset=True):
+        """race, diagnostics on: (auto-resets copied from a next-reset image, auto-resets computed
+        inline) by the four-lane kernel since the last read"""
+        import numpy as np
+        out = np.zeros(2, np.int32)
+        self._check(self.lib.adrp_race_reset_counts(self.h, out.ctypes.data_as(ctypes.c_void_p), 1 if reset else 0),
+                    "adrp_race_reset_counts")
+        return int(out[0]), int(out[1])
 
     def profile_begin(self, n):
         self._check(self.lib.adrp_profile_begin(self.h, n), "adrp_profile_begin")

@@ -405,6 +405,7 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     const size_t EN = size_t(h->E) * h->N;
     auto cleanup = [&](int rc) {
         hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters); hipFree(h->cblk);
+        hipFree(h->img_f); hipFree(h->img_i); hipFree(h->img_row); hipFree(h->img_ep);
         g_err = h->err;
         delete h;
         return rc;
@@ -430,6 +431,17 @@ extern "C" int adrp_create(const adrp_config* cfg, int device, adrp_t** out) {
     const int rc = race ? (h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h))
                         : (h->real_size == 8 ? upload_const<double>(h) : upload_const<float>(h));
     if (rc != ADRP_OK) return cleanup(seterr(h, rc, "constant block upload failed"));
+    if (const char* env = getenv("ADRP_RESET_IMAGES")) h->img_period = atoi(env);
+    if (race && c.autoreset && h->img_period > 0) {   // next-reset images (race_quad.h)
+        if (hipMalloc(&h->img_f, size_t(RF_N) * EN * h->real_size) != hipSuccess ||
+            hipMalloc((void**)&h->img_i, size_t(RI_N) * EN * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc((void**)&h->img_row, EN * size_t(h->D) * sizeof(float)) != hipSuccess ||
+            hipMalloc((void**)&h->img_ep, size_t(h->E) * sizeof(int32_t)) != hipSuccess)
+            return cleanup(seterr(h, ADRP_ERR_OOM, "hipMalloc failed (reset images)"));
+        if (hipMemset(h->img_ep, 0xff, size_t(h->E) * sizeof(int32_t)) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess)
+            return cleanup(seterr(h, ADRP_ERR_DEVICE, "initialisation failed (reset images)"));
+    }
     *out = h;
     return ADRP_OK;
 }
@@ -443,7 +455,16 @@ extern "C" void adrp_destroy(adrp_t* h) {
     for (auto e : h->ev_stop) hipEventDestroy(e);
     hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters); hipFree(h->cblk);
     hipFree(h->cmdf); hipFree(h->cmdi); hipFree(h->mom_hash);
+    hipFree(h->img_f); hipFree(h->img_i); hipFree(h->img_row); hipFree(h->img_ep);
     delete h;
+}
+
+// next-reset images are keyed by the episode; a new seed or constant block makes them all stale
+static int images_invalidate(adrp_t* h, hipStream_t s) {
+    if (!h->img_ep) return ADRP_OK;
+    HIPCHK(h, hipMemsetAsync(h->img_ep, 0xff, size_t(h->E) * sizeof(int32_t), s));
+    h->img_ctr = 0;   // the next step refills
+    return ADRP_OK;
 }
 
 extern "C" int adrp_reseed(adrp_t* h, uint64_t seed, void* stream) {
@@ -453,7 +474,7 @@ extern "C" int adrp_reseed(adrp_t* h, uint64_t seed, void* stream) {
     const size_t EN = size_t(h->E) * h->N;
     static_assert(RI_EPISODE == 1 && HI_EPISODE == 1, "episode counters are int row 1 in both tasks");
     HIPCHK(h, hipMemsetAsync(h->ist + EN, 0, EN * sizeof(int32_t), (hipStream_t)stream));
-    return ADRP_OK;
+    return images_invalidate(h, (hipStream_t)stream);
 }
 
 extern "C" int adrp_set_wrappers(adrp_t* h, int reward_wrapper, int obs_wrapper) {
@@ -465,7 +486,8 @@ extern "C" int adrp_set_wrappers(adrp_t* h, int reward_wrapper, int obs_wrapper)
     h->cfg.track.reward_wrapper = reward_wrapper ? 1 : 0;
     h->cfg.track.obs_wrapper = obs_wrapper;
     const int rc = h->real_size == 8 ? upload_race_const<double>(h) : upload_race_const<float>(h);
-    return rc == ADRP_OK ? rc : seterr(h, rc, "constant block upload failed");
+    if (rc != ADRP_OK) return seterr(h, rc, "constant block upload failed");
+    return images_invalidate(h, nullptr);
 }
 
 extern "C" int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_dev) {
@@ -486,9 +508,11 @@ extern "C" int adrp_reset(adrp_t* h, const uint8_t* env_mask_dev, float* obs_dev
     if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_reset: persistent mode is active (adrp_persistent_end first)");
     DeviceGuard g(h->device);
     hipStream_t s = (hipStream_t)stream;
-    if (h->cfg.task == ADRP_TASK_RACE)
+    if (h->cfg.task == ADRP_TASK_RACE) {
+        h->img_ctr = 0;   // the next step refills the next-reset images of the new episodes
         return h->real_size == 8 ? race_reset<double>(h, env_mask_dev, obs_dev, s)
                                  : race_reset<float>(h, env_mask_dev, obs_dev, s);
+    }
     return h->real_size == 8 ? hover_reset<double>(h, env_mask_dev, obs_dev, s)
                              : hover_reset<float>(h, env_mask_dev, obs_dev, s);
 }
@@ -914,6 +938,14 @@ extern "C" int adrp_gjk_dump_read(double* out, int max, int f64, int reset) {
 }
 #endif
 #endif
+
+extern "C" int adrp_race_reset_counts(adrp_t* h, int32_t* out, int reset) {
+    if (!h || !out) return seterr(h, ADRP_ERR_INVALID, "adrp_race_reset_counts: NULL argument");
+    DeviceGuard g(h->device);
+    HIPCHK(h, hipMemcpy(out, h->counters + 1, 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(h, hipMemset(h->counters + 1, 0, 2 * sizeof(int32_t)));
+    return ADRP_OK;
+}
 
 extern "C" int adrp_diagnostic_contact_count(adrp_t* h, int reset) {
     if (!h) return ADRP_ERR_INVALID;

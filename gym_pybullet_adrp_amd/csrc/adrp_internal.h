@@ -46,6 +46,14 @@ struct adrp_handle {
     const double* inj_force = nullptr;
     int diagnostics = 0;
     uint32_t* mom_hash = nullptr; // race diagnostics: [E*N] firmware int16-moment hash of the last step
+    // race next-reset images (race_quad.h race_refill_q4; four-lane kernel with auto-reset): refilled
+    // by a launch every img_period steps (ADRP_RESET_IMAGES=K, 0 = off)
+    void* img_f = nullptr;        // Real [RF_N][E*N]
+    int32_t* img_i = nullptr;     // [RI_N][E*N]
+    float* img_row = nullptr;     // [E*N][D]
+    int32_t* img_ep = nullptr;    // [E], -1 = none
+    int img_period = 32;
+    unsigned img_ctr = 0;
     // persistent step (adrp_persistent_*, hover_persist.h): host-mapped mailbox and its own stream
     void* pbox = nullptr;         // host address of the mapped mailbox (PersistCtl + buffers), or null
     hipStream_t pstream = nullptr;
@@ -124,6 +132,11 @@ inline RaceArgs<Real> race_args(const adrp_t* h) {
     a.inj_act = h->inj_act;
     a.inj_force = h->inj_force;
     a.mom_hash = h->diagnostics ? h->mom_hash : nullptr;
+    a.img_f = (Real*)h->img_f;
+    a.img_i = h->img_i;
+    a.img_row = h->img_row;
+    a.img_ep = h->img_ep;
+    a.reset_count = h->diagnostics ? h->counters + 1 : nullptr;
     return a;
 }
 

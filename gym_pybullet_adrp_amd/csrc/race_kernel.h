@@ -99,6 +99,13 @@ struct RaceArgs {
     int64_t env_offset;
     int E;
     uint32_t* mom_hash;  // diagnostics (adrp_set_diagnostics): [E*N] fw_moment_hash of the step, or null
+    // next-reset images (race_quad.h, race_refill_q4): what the auto-reset at the end of episode
+    // img_ep[e] writes for env e, computed ahead of time; null when off
+    Real* img_f;         // [RF_N][E*N]
+    int32_t* img_i;      // [RI_N][E*N]
+    float* img_row;      // [E*N][D] the reset obs rows
+    int32_t* img_ep;     // [E] the episode the image is for, -1 none
+    int32_t* reset_count;  // diagnostics: [2] auto-resets from an image / computed inline (four-lane kernel)
 };
 
 // The physical constants of the reference's race drone (cf2x.urdf at PYB_FREQ 500, BaseAviary.py:

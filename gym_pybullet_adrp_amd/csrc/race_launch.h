@@ -98,12 +98,32 @@ int race_step_ph(adrp_t* h, const RaceArgs<Real>& a, int G, hipStream_t s) {
 }
 #define ADRP_RACE_STEP_PH(R, PH) int race_step_ph<R, PH>(adrp_t*, const RaceArgs<R>&, int, hipStream_t)
 
+// the next-reset image refill (race_quad.h), in the step's lane layout
+template <typename Real>
+static void launch_race_refill(const RaceArgs<Real>& a, int G, hipStream_t s, adrp_t* h) {
+    const dim3 blk(kRaceBlock), grid((unsigned)((size_t(h->E) * G * 4 + kRaceBlock - 1) / kRaceBlock));
+    switch (G) {
+#ifndef ADRP_DEV_FAST
+        case 1: hipLaunchKernelGGL((race_refill_q4<Real, 1>), grid, blk, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((race_refill_q4<Real, 8>), grid, blk, 0, s, a); break;
+#endif
+        case 2: hipLaunchKernelGGL((race_refill_q4<Real, 2>), grid, blk, 0, s, a); break;
+        default: hipLaunchKernelGGL((race_refill_q4<Real, 4>), grid, blk, 0, s, a); break;
+    }
+}
+
 template <typename Real>
 int race_step(adrp_t* h, const float* act, float* obs, float* rew, uint8_t* term, uint8_t* trunc,
                      float* tobs, hipStream_t s) {
     RaceArgs<Real> a = race_args<Real>(h);
     a.act = act; a.obs = obs; a.rew = rew; a.term = term; a.trunc = trunc; a.tobs = tobs;
     const int G = race_group(h->N);
+    // next-reset images: the four-lane kernel's auto-reset copies them; refilled every img_period steps
+    if (h->img_ep && !h->cmdf && race_quad_ok(h)) {
+        if (h->img_ctr++ % unsigned(h->img_period) == 0) launch_race_refill<Real>(a, G, s, h);
+    } else {
+        a.img_f = nullptr; a.img_i = nullptr; a.img_row = nullptr; a.img_ep = nullptr;
+    }
 #ifdef ADRP_DEV_FAST   // experiment build (make dev): the benched race instantiations only
     if ((h->cfg.physics != ADRP_PHYS_PYB && h->cfg.physics != ADRP_PHYS_PYB_DW) || (G != 2 && G != 4))
         return seterr(h, ADRP_ERR_INVALID, "dev build: race config not instantiated");

@@ -665,6 +665,118 @@ __device__ __forceinline__ void race_reset_q4(const RaceArgs<Real>& a, const Rac
     RESET_MARK(8);
 }
 
+// Next-reset images.  Everything an auto-reset writes (the drone slot's 98 state fields and 9 ints,
+// its reset obs row) is a function of (seed, env, episode) and the constant block only: the track and
+// drone-init draws are keyed by the episode, the range tests and the obs row are taken at the nominal
+// pose.  race_refill_q4 computes it ahead, with race_reset_q4 itself (the same code, so the same bits),
+// into image buffers tagged with the episode it is for; the step kernel's auto-reset of an env whose
+// image is for its current episode then copies it (loads and stores, no arithmetic) instead of running
+// the reset's ~5 us chain on the wave that the whole launch waits for.  An env whose image is not ready
+// (reset twice between refills, or images off) resets inline as before.
+// n floats from LDS to global memory by the wave's 64 lanes (all reads, then the stores)
+template <int MAXN>
+__device__ __forceinline__ void wave_copy_rows(const float* src, float* dst, int n, int tl) {
+    constexpr int K = (MAXN + kRaceBlock - 1) / kRaceBlock;
+    float v[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const int k = tl + kRaceBlock * i;
+        v[i] = k < n ? src[k] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const int k = tl + kRaceBlock * i;
+        if (k < n) dst[k] = v[i];
+    }
+}
+
+// one env's image (its N drone slots from slot0: 98 fields and 9 ints each, and its N obs rows) into
+// the state and the block's LDS rows, by the wave's 64 lanes: every load in flight, then the stores
+template <typename Real, int G, int ROWF>
+__device__ __forceinline__ void reset_from_image(const RaceArgs<Real>& a, size_t EN, size_t slot0, int N, float* rows,
+                                                 int D, int tl) {
+    constexpr int KF = (RF_N * G + kRaceBlock - 1) / kRaceBlock, KI = (RI_N * G + kRaceBlock - 1) / kRaceBlock;
+    constexpr int KR = (ROWF * G + kRaceBlock - 1) / kRaceBlock;
+    const int nf = RF_N * N, ni = RI_N * N, nr = N * D;
+    Real v[KF];
+    int32_t iv[KI];
+    float rv[KR];
+    size_t fo[KF], io[KI];
+#pragma unroll
+    for (int i = 0; i < KF; ++i) {   // field k of drone slot0 + j: idx = k * N + j
+        const int idx = tl + kRaceBlock * i;
+        const int k = idx / N, j = idx - k * N;
+        fo[i] = size_t(k) * EN + slot0 + j;
+        v[i] = idx < nf ? a.img_f[fo[i]] : Real(0);
+    }
+#pragma unroll
+    for (int i = 0; i < KI; ++i) {
+        const int idx = tl + kRaceBlock * i;
+        const int k = idx / N, j = idx - k * N;
+        io[i] = size_t(k) * EN + slot0 + j;
+        iv[i] = idx < ni ? a.img_i[io[i]] : 0;
+    }
+    const float* src = a.img_row + slot0 * size_t(D);
+#pragma unroll
+    for (int i = 0; i < KR; ++i) {
+        const int k = tl + kRaceBlock * i;
+        rv[i] = k < nr ? src[k] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < KF; ++i)
+        if (tl + kRaceBlock * i < nf) a.f[fo[i]] = v[i];
+#pragma unroll
+    for (int i = 0; i < KI; ++i)
+        if (tl + kRaceBlock * i < ni) a.ist[io[i]] = iv[i];
+#pragma unroll
+    for (int i = 0; i < KR; ++i) {
+        const int k = tl + kRaceBlock * i;
+        if (k < nr) rows[k] = rv[i];
+    }
+}
+
+// The refill: the step's lane layout (a quad per drone, 4G lanes per env); an env whose image is not
+// for its current episode gets one.  Waves with nothing to refill end after two loads.
+template <typename Real, int G>
+__global__ void __launch_bounds__(kRaceBlock) race_refill_q4(RaceArgs<Real> a) {
+    const int tl = threadIdx.x;
+    const int ql = tl & 3, qd = tl >> 2;
+    const int dl = blockIdx.x * kQuadDrones + qd;
+    const RaceConst<Real>& CG = *a.c;
+    const int N = CG.N;
+    const int e_raw = dl / G, d_raw = dl % G;
+    const bool active = e_raw < a.E && d_raw < N;
+    const int e = e_raw < a.E ? e_raw : a.E - 1;
+    const int dn = d_raw < N ? d_raw : 0;
+    const size_t EN = size_t(a.E) * N;
+    const size_t slot = size_t(e) * N + dn;
+    const int episode = a.ist[RI_EPISODE * EN + slot];
+    const bool need = a.img_ep[e] != episode;   // env-uniform: the env's drones share the episode
+    if (!__any(need)) return;                   // wave-uniform exit
+    __shared__ __attribute__((aligned(16))) RaceConst<Real> c_lds;
+    __shared__ float rows[kQuadDrones * (49 + 6 * (G - 1))];
+    // (the wave that reaches here is the whole block: kRaceBlock = one wave)
+    {
+        constexpr int nw = int(sizeof(RaceConst<Real>) / 4);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.c);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&c_lds);
+        for (int i = tl; i < nw; i += kRaceBlock) dst[i] = src[i];
+    }
+    __syncthreads();
+    const RaceConst<Real>& C = c_lds;
+    RaceArgs<Real> b = a;   // the reset's sink writes the image instead of the state
+    b.f = a.img_f;
+    b.ist = a.img_i;
+    float* row = rows + qd * C.D;
+    if (need) race_reset_q4<Real, G>(b, C, e, dn, ql, active, EN, slot, episode, row, ResetToHBM<Real>{&b});
+    __syncthreads();   // the owner lane's row
+    if (need && active) {   // the quad's lanes copy the row out
+        float* dst = a.img_row + slot * size_t(C.D);
+        for (int k = ql; k < C.D; k += 4) dst[k] = row[k];
+        if (ql == 0 && dn == 0) a.img_ep[e] = episode;
+    }
+}
+
 // the sub-step draws of drone qd's sub-steps s = ql, ql + 4, ... into the LDS table [s][7][drone]:
 // fp32 the 3 force components and the 4 motor noises; fp64 the 3 force uniforms (exact in float;
 // the force is formed in Real at use) and the 4 noise samples (normal_pair_f, float, scaled at use)
@@ -951,6 +1063,9 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     if constexpr (kEarlyStore) {
         if (owner) store_drone_body<Real, PH == ADRP_PHYS_DYN>(a, EN, slot, d);
     }
+    // the episode this env's next-reset image is for, loaded here so that its latency hides behind
+    // the post-loop phases (the barrier keeps the load from sinking to its use in the auto-reset)
+    const int img_for = a.img_ep != nullptr ? a.img_ep[e] : -2;
     __syncthreads();
     const TrackSrcQ<Real> T{trk_lds, qd};
     // ---- _gate_progress (471-506) ----
@@ -1122,14 +1237,22 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
             if (dn == 0) a.ist[RI_WR_GATE * EN + slot] = wr_gate;
         }
     }
-    if (reset && a.tobs && e_raw < a.E) {   // terminal obs: the env's N rows, copied by its 4G lanes
-        const int nl = 4 * G, li = tl & (nl - 1);
-        const float* src = rows + (qd / G) * N * C.D;
-        float* dst = a.tobs + size_t(e) * N * C.D;
-        const int n = N * C.D;
-        for (int k = li; k < n; k += nl) dst[k] = src[k];
+    // terminal obs, then the resets: a done env's work is dealt over the wave's 64 lanes (the
+    // other envs' lanes are idle here), one resetting env at a time (rarely more than one per wave)
+    const bool img = reset && img_for == episode;          // (env-uniform)
+    const bool env_lead = reset && owner && dn == 0;        // one lane per resetting env
+    for (uint64_t rm = __ballot(env_lead && a.tobs != nullptr); rm; rm &= rm - 1) {
+        const int L = __builtin_ctzll(rm);
+        const int er = __builtin_amdgcn_readlane(e, L), eb = __builtin_amdgcn_readlane(qd, L) / G;
+        wave_copy_rows<G * kRowF>(rows + eb * N * C.D, a.tobs + size_t(er) * N * C.D, N * C.D, tl);
     }
-    if (reset) race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, row, ResetToHBM<Real>{&a});
+    for (uint64_t rm = __ballot(env_lead && img); rm; rm &= rm - 1) {
+        const int L = __builtin_ctzll(rm);
+        const int er = __builtin_amdgcn_readlane(e, L), eb = __builtin_amdgcn_readlane(qd, L) / G;
+        reset_from_image<Real, G, kRowF>(a, EN, size_t(er) * N, N, rows + eb * N * C.D, C.D, tl);
+    }
+    if (reset && !img) race_reset_q4<Real, G>(a, C, e, dn, ql, active, EN, slot, episode, row, ResetToHBM<Real>{&a});
+    if (a.reset_count && env_lead) atomicAdd(a.reset_count + (img ? 0 : 1), 1);
 #ifdef ADRP_RACE_TIMING
     RACE_MARK(t6);   // tail: reward, flags, stores and the auto-reset of done envs
     if (threadIdx.x == 0) {

@@ -299,6 +299,10 @@ int adrp_diagnostic_contact_count(adrp_t* h, int reset);
  * Parity tests use it as the causal witness of an int16 truncation difference.  Copies E * N values
  * of the last step to `out` (host memory); n must be E * N.  Replaces nothing in the reference. */
 int adrp_race_moment_hash(adrp_t* h, uint32_t* out, size_t n);
+/* Race handles, diagnostics on: auto-resets of the four-lane kernel since the last read, out[0]
+ * copied from a next-reset image (computed ahead by the refill launch every ADRP_RESET_IMAGES
+ * steps, default 32, 0 = off), out[1] computed inline.  Replaces nothing in the reference. */
+int adrp_race_reset_counts(adrp_t* h, int32_t* out, int reset);
 
 /* ---------------------------------------------------------------------------------------
  * On-device policy forward: the actor of an SB3 PPO MlpPolicy

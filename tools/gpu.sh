@@ -139,6 +139,11 @@ r = d["roofline"]
 print(f"{sys.argv[1]:60s} kernel_us {r['kernel_us']:8.3f} eager {r.get('eager_dispatch_us', float('nan')):8.3f} "
       f"step_us {d['ms_per_step'] * 1e3:8.3f} value {d['value']:.4e}", flush=True)
 PY
+        python3 - "$ARM" "$O/ab_last.log" >> "$O/ab_results.txt" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
+print(sys.argv[1], d["roofline"]["kernel_us"], d["ms_per_step"] * 1e3)
+PY
       done
     done ;;
   *) sed -n 2,17p "$0"; exit 2 ;;
