@@ -189,18 +189,26 @@ __device__ __forceinline__ void tick_window(const uint32_t* tab, int n, uint32_t
     pos = __builtin_amdgcn_alignbit(tab[kTickWords + w + 1], tab[kTickWords + w], sh);
 }
 
-// clamps: v_med3_f32 (one instruction; the select form is four).  Equal to the reference's
-// `v < lo ? lo : (v > hi ? hi : v)` for every non-NaN v; fp64 keeps the selects
+// clamps: v_med3_f32 (one instruction; the select form is four), in fp64 v_max_f64 + v_min_f64 (the
+// double select form is a compare and two v_cndmask per side).  Equal to the reference's
+// `v < lo ? lo : (v > hi ? hi : v)` for every non-NaN v, up to the sign of a zero v at a zero bound
+// (the max returns +0 where the select keeps -0; every fp64 call site clamps the thrust chain,
+// whose later clamp to [20000, 65535] or sqrt makes the two zeros the same value)
 __device__ __forceinline__ float clampf_(float v, float lo, float hi) { return __builtin_amdgcn_fmed3f(v, lo, hi); }
 __device__ __forceinline__ float clampr_(float v, float lo, float hi) { return __builtin_amdgcn_fmed3f(v, lo, hi); }
-__device__ __forceinline__ double clampr_(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ double clampr_(double v, double lo, double hi) { return __builtin_fmin(__builtin_fmax(v, lo), hi); }
 // one-sided clamps (`x > hi ? hi : x`, `x < lo ? lo : x`) as v_min/v_max for non-NaN x
 __device__ __forceinline__ float minr_(float x, float hi) { return __builtin_fminf(x, hi); }
-__device__ __forceinline__ double minr_(double x, double hi) { return x > hi ? hi : x; }
+__device__ __forceinline__ double minr_(double x, double hi) { return __builtin_fmin(x, hi); }
 __device__ __forceinline__ float maxr_(float x, float lo) { return __builtin_fmaxf(x, lo); }
-__device__ __forceinline__ double maxr_(double x, double lo) { return x < lo ? lo : x; }
+__device__ __forceinline__ double maxr_(double x, double lo) { return __builtin_fmax(x, lo); }
+// `a > b ? a : b`; in fp64 as v_max_f64 (equal for every pair but +0 / -0, which compare equal
+// wherever the bounds use it)
 template <typename Real>
-__device__ __forceinline__ Real fmaxr_(Real a, Real b) { return a > b ? a : b; }
+__device__ __forceinline__ Real fmaxr_(Real a, Real b) {
+    if constexpr (sizeof(Real) == 8) return __builtin_fmax(a, b);
+    else return a > b ? a : b;
+}
 __device__ __forceinline__ float radf_(float d) { return (3.14159265358979323846f / 180.0f) * d; }
 __device__ __forceinline__ float degf_(float r) { return (180.0f / 3.14159265358979323846f) * r; }
 

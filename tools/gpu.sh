@@ -52,7 +52,7 @@ pmc() {     # name counters cmd...   (one counter group per rocprofv3 run, its o
 case "$CMD" in
   check)
     steps "bench_k20|420|python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_k20.json" \
-          "tests|500|python -u -m pytest -x -v --timeout 200 --timeout-method thread -s ${TESTS:-tests/test_sharding_gpu.py tests/test_persistent_gpu.py}" ;;
+          "tests|500|python -u -m pytest -x -v --timeout 200 --timeout-method thread -s ${TESTS:-tests -m gpu}" ;;
   evidence)
     steps "pytest_gpu|900|python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread" \
           "smoke|200|python -c 'import __graft_entry__ as g; g.smoke()'" \
