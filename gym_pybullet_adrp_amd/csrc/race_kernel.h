@@ -447,7 +447,7 @@ __device__ __forceinline__ Shape<double> shape_f64(const Shape<Real>& s) {
 // origin, the upper bound, convergence) keep the float answer, and range queries (0.45 m) stay
 // float.
 // out of line: one copy per code object for the rare rerun (inlined at the three query sites it
-// grew the fp32 kernels by ~10 % of code and made them no faster; tools/gpu_r3_t16.sh)
+// grew the fp32 kernels by ~10 % of code and made them no faster; a round-3 A/B)
 __device__ __noinline__ bool gjk_within_f64_call(Shape<double> A, Shape<double> B, double cut, V3<double> v0, bool seeded) {
     return gjk_within_impl<double>(A, B, cut, nullptr, seeded ? &v0 : nullptr);
 }

@@ -4,7 +4,7 @@
 #include "adrp_internal.h"
 
 // the quad kernel's physical constants are compiled in (race_cf2x_phys) for fp64, where that took
-// config 4 from 98.2 to 95.5 us; for fp32 it measured 0.5 us slower (tools/gpu_r3_t17.sh)
+// config 4 from 98.2 to 95.5 us; for fp32 it measured 0.5 us slower (round-3 A/B)
 template <typename Real>
 constexpr bool kQuadDef = sizeof(Real) == 8;
 

@@ -967,7 +967,7 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
                 for (int j = 0; j < (G + 3) / 4; ++j) {
                     const int k = ql + 4 * j;
                     // ds_bpermute: DPP row broadcasts of the four partners' positions (row_newbcast +
-                    // selects) measured 2.5-3 us slower on config 4 (tools/gpu_r3_t20.sh)
+                    // selects) measured 2.5-3 us slower on config 4 (round-3 A/B)
                     const int src = (tl & ~(4 * G - 1)) + 4 * (k < G ? k : 0);
                     const Real ox = __shfl(pos.x, src), oy = __shfl(pos.y, src), oz = __shfl(pos.z, src);
                     const Real dz = oz - pos.z, dx = ox - pos.x, dy = oy - pos.y;
@@ -1057,9 +1057,10 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     }
     // the state the post-loop phases do not change goes out now, so its registers are free for the
     // track queries and the reset (a done env's auto-reset overwrites it below)
-    // fp64: config 4 95 -> 80.5 us; fp32 keeps the store at the end (0.5 us faster there;
-    // tools/gpu_r3_t21.sh)
-    constexpr bool kEarlyStore = !F32;   // (fp32 early store re-measured round 4: +0.3 us)
+    // (fp64 since round 3: config 4 95 -> 80.5 us; fp32 since round 5, with the auto-reset copying
+    // images: config 3 30.4 -> 30.0 us, config 3 + actor 54.5 -> 53.7 us, config 4 unchanged, where
+    // rounds 3 and 4 had measured it +0.3-0.5 us)
+    constexpr bool kEarlyStore = true;
     if constexpr (kEarlyStore) {
         if (owner) store_drone_body<Real, PH == ADRP_PHYS_DYN>(a, EN, slot, d);
     }
