@@ -81,3 +81,26 @@ def test_persistent_restart_and_close_order():
     p.step(act)
     env.close()          # ends the resident kernel
     p.close()            # no-op after the env is gone
+
+
+def test_persistent_long_run_no_stale_outputs(monkeypatch):
+    """3,000 steps at E = 70 (the case where, without the release before `done`, the host once read
+    the previous step's obs rows): every step's outputs bit for bit the launched kernel's"""
+    a, b = _pair(70, "fp64", Physics.PYB_GND_DRAG_DW, ActionType.ONE_D_RPM, monkeypatch)
+    a.reset()
+    b.reset()
+    rng = np.random.default_rng(9)
+    bad = []
+    with b.persistent() as p:
+        for k in range(3000):
+            act = rng.uniform(-1, 1, (70, 1, 1)).astype(np.float32)
+            if (k // 50) % 4 == 1:
+                act[:] = 1.0
+            oa, ra, ta, tra, _ = a.step(torch.from_numpy(act).to(a.device))
+            ob, rb, tb, trb, _ = p.step(act)
+            if not (np.array_equal(ob, oa.cpu().numpy()) and np.array_equal(rb, ra.cpu().numpy())
+                    and np.array_equal(tb, ta.cpu().numpy()) and np.array_equal(trb, tra.cpu().numpy())):
+                bad.append(k)
+    assert not bad, f"{len(bad)} steps differ, first {bad[:5]}"
+    a.close()
+    b.close()
