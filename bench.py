@@ -893,7 +893,7 @@ def summary(result):
                                     else None}
     if "config1" in cf:
         c1 = cf["config1"]
-        out["config1"] = {"sync_v": _sig((c1.get("gpu_persistent_sync_per_step") or {}).get("value")),
+        out["config1"] = {"persistent_sync_v": _sig((c1.get("gpu_persistent_sync_per_step") or {}).get("value")),
                           "launch_sync_v": _sig((c1.get("gpu_sync_per_step") or {}).get("value")),
                           "graph_v": _sig((c1.get("gpu_graph") or {}).get("value")),
                           "cpu_1core_v": _sig((c1.get("cpu_oracle_1env") or {}).get("value"))} if "error" not in c1 \

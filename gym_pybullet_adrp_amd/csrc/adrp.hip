@@ -469,6 +469,9 @@ static int images_invalidate(adrp_t* h, hipStream_t s) {
 
 extern "C" int adrp_reseed(adrp_t* h, uint64_t seed, void* stream) {
     if (!h) return seterr(h, ADRP_ERR_INVALID, "adrp_reseed: NULL handle");
+    // the resident kernel owns the episode counters and fixed its seed at launch: refuse
+    // before any change (a half-applied reseed would race with it)
+    if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_reseed: persistent mode is active (adrp_persistent_end first)");
     DeviceGuard g(h->device);
     h->cfg.seed = seed;   // read into the kernel arguments at every launch
     const size_t EN = size_t(h->E) * h->N;
@@ -479,6 +482,7 @@ extern "C" int adrp_reseed(adrp_t* h, uint64_t seed, void* stream) {
 
 extern "C" int adrp_set_wrappers(adrp_t* h, int reward_wrapper, int obs_wrapper) {
     if (!h) return seterr(h, ADRP_ERR_INVALID, "adrp_set_wrappers: NULL handle");
+    if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_set_wrappers: persistent mode is active (adrp_persistent_end first)");
     if (h->cfg.task != ADRP_TASK_RACE) return seterr(h, ADRP_ERR_INVALID, "wrappers are MultiRaceAviary's");
     if (obs_wrapper < 0 || obs_wrapper > 2) return seterr(h, ADRP_ERR_INVALID, "obs_wrapper must be 0, 1 or 2");
     DeviceGuard g(h->device);
@@ -492,6 +496,7 @@ extern "C" int adrp_set_wrappers(adrp_t* h, int reward_wrapper, int obs_wrapper)
 
 extern "C" int adrp_set_noise(adrp_t* h, const double* act_noise_dev, const double* force_dev) {
     if (!h) return seterr(h, ADRP_ERR_INVALID, "adrp_set_noise: NULL handle");
+    if (h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_set_noise: persistent mode is active (adrp_persistent_end first)");
     if (h->cfg.task != ADRP_TASK_RACE) return seterr(h, ADRP_ERR_INVALID, "noise injection is MultiRaceAviary's");
     if ((act_noise_dev == nullptr) != (force_dev == nullptr))
         return seterr(h, ADRP_ERR_INVALID, "adrp_set_noise: both arrays or neither");
@@ -809,6 +814,9 @@ extern "C" int adrp_persistent_begin(adrp_t* h, void** act, void** obs, void** r
 extern "C" int adrp_persistent_step(adrp_t* h) {
     if (!h || !h->pbox) return seterr(h, ADRP_ERR_INVALID, "adrp_persistent_step: persistent mode is not active");
     PersistCtl* ctl = (PersistCtl*)h->pbox;
+    if (__atomic_load_n(&ctl->kstop, __ATOMIC_ACQUIRE) != 0u || __atomic_load_n(&ctl->status, __ATOMIC_ACQUIRE) == 2u)
+        return seterr(h, ADRP_ERR_DEVICE, "adrp_persistent_step: the persistent kernel has exited "
+                                          "(idle timeout); adrp_persistent_end, then begin again");
     uint32_t seq = h->pseq + 1;
     if (seq == kPersistStop) seq = 1;
     h->pseq = seq;
@@ -821,9 +829,13 @@ extern "C" int adrp_persistent_step(adrp_t* h) {
             __builtin_ia32_pause();
             if ((++spins & 4095u) == 0) {
                 if (t0 == decltype(t0){}) t0 = std::chrono::steady_clock::now();
-                if (__atomic_load_n(&ctl->status, __ATOMIC_ACQUIRE) == 2u)
+                // workgroup b left on the grid-wide idle timeout without this request: the step
+                // may have run on the other workgroups' envs only
+                if (__atomic_load_n(&ctl->exited[b], __ATOMIC_ACQUIRE) != 0u &&
+                    __atomic_load_n(&ctl->done[b], __ATOMIC_ACQUIRE) != seq)
                     return seterr(h, ADRP_ERR_DEVICE, "adrp_persistent_step: the persistent kernel has exited "
-                                                      "(idle timeout); adrp_persistent_end, then begin again");
+                                                      "(idle timeout) before completing this step, whose envs may "
+                                                      "be partially stepped; adrp_persistent_end, then begin again");
                 if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
                     return seterr(h, ADRP_ERR_DEVICE, "adrp_persistent_step: no completion within 10 s");
             }

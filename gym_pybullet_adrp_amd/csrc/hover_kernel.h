@@ -128,6 +128,23 @@ struct Body {
     Real prev_rpm[4];
 };
 
+// Explicit fused multiply-adds of the PYB sub-step chain.  The hover TUs contract a*b+c only
+// within one source expression (csrc/Makefile CONTRACT: the same bits in every dispatch variant),
+// so the fusions across the V3 operators that the chain wants are written out here.
+__device__ __forceinline__ float fmx(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fmx(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+// rot(q) with its products folded into FMAs (20 operations instead of 24)
+template <typename Real>
+__device__ __forceinline__ M3<Real> rot_fm(Q4<Real> q) {
+    const Real x2 = q.x + q.x, y2 = q.y + q.y, z2 = q.z + q.z;
+    const Real xx = q.x * x2, zz = q.z * z2;
+    const Real wx = q.w * x2, wy = q.w * y2, wz = q.w * z2;
+    return {Real(1) - fmx(q.y, y2, zz), fmx(q.x, y2, -wz), fmx(q.x, z2, wy),
+            fmx(q.x, y2, wz), Real(1) - fmx(q.x, x2, zz), fmx(q.y, z2, -wx),
+            fmx(q.x, z2, -wy), fmx(q.y, z2, wx), Real(1) - fmx(q.y, y2, xx)};
+}
+
 // float32 1 + 0.05 a, two roundings as NumPy does it (no FMA contraction)
 __device__ __forceinline__ float rpm_gain(float a) {
 #pragma clang fp contract(off)
@@ -152,7 +169,9 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     const V3<Real> zs = col2(Rs);
     V3<Real> Fw = v3(sum_f * zs.x, sum_f * zs.y, sum_f * zs.z - a.mass * a.gravity);
     const V3<Real> m3 = mulT(R, zs);
-    V3<Real> nb = cross(P, m3) + tau_z * m3;
+    // P x m3 + tau_z m3
+    V3<Real> nb = v3(fmx(tau_z, m3.x, fmx(P.y, m3.z, -(P.z * m3.y))), fmx(tau_z, m3.y, fmx(P.z, m3.x, -(P.x * m3.z))),
+                     fmx(tau_z, m3.z, fmx(P.x, m3.y, -(P.y * m3.x))));
     bool cur_basis = false;
     if constexpr (GND) {
         // getLinkStates(computeForwardKinematics=1) refreshes the cached basis first
@@ -191,14 +210,18 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
     const V3<Real> wb = mulT(R, b.w);
     const V3<Real> Iw = v3(a.ixx * wb.x, a.iyy * wb.y, a.izz * wb.z);
     const Real kw = K.k004 + K.k004 * wn;
-    const V3<Real> rhs = nb - kw * Iw - cross(wb, Iw);
+    // nb - kw Iw - wb x Iw
+    const V3<Real> rhs = v3(fmx(wb.z, Iw.y, fmx(-wb.y, Iw.z, fmx(-kw, Iw.x, nb.x))),
+                            fmx(wb.x, Iw.z, fmx(-wb.z, Iw.x, fmx(-kw, Iw.y, nb.y))),
+                            fmx(wb.y, Iw.x, fmx(-wb.x, Iw.y, fmx(-kw, Iw.z, nb.z))));
     const V3<Real> wdot = mul(R, v3(rhs.x * a.inv_ixx, rhs.y * a.inv_iyy, rhs.z * a.inv_izz));
     const Real kv = K.k004 + K.k004 * hsqrt_nn_(dot(b.vel, b.vel), K);
-    const V3<Real> acc = a.inv_mass * Fw - kv * b.vel;
+    const V3<Real> acc = v3(fmx(-kv, b.vel.x, a.inv_mass * Fw.x), fmx(-kv, b.vel.y, a.inv_mass * Fw.y),
+                            fmx(-kv, b.vel.z, a.inv_mass * Fw.z));
     b.w = v3(b.w.x + a.dt * wdot.x, b.w.y + a.dt * wdot.y, b.w.z + a.dt * wdot.z);
     b.vel = v3(b.vel.x + a.dt * acc.x, b.vel.y + a.dt * acc.y, b.vel.z + a.dt * acc.z);
     clamp100_wv(b.w, b.vel, K);
-    b.pos = b.pos + a.dt * b.vel;
+    b.pos = v3(fmx(a.dt, b.vel.x, b.pos.x), fmx(a.dt, b.vel.y, b.pos.y), fmx(a.dt, b.vel.z, b.pos.z));
     // exp-map quaternion update (btMultiBody::stepPositionsMultiDof)
     Real ang = hsqrt_nn_(dot(b.w, b.w), K);
     wn = ang;
@@ -221,7 +244,7 @@ __device__ __forceinline__ bool pyb_substep(const HoverConst<Real>& a, Body<Real
         Rs = R;
     }
     b.q = {q1.x * inv, q1.y * inv, q1.z * inv, q1.w * inv};
-    R = rot(b.q);
+    R = rot_fm(b.q);
     if (!a.link_lag) Rs = R;
     // plane contact model: non-penetration, no inward velocity.
     // lowest point of the body cylinder: cos(tilt) = R22, sin(tilt) = |(R02, R12)|.  It is at
@@ -689,8 +712,8 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
             t2 += (i & 1) ? -r2 : r2;
         }
         const Real tau_z = t2 * C.km;    // KM*(rpm0^2 - rpm1^2 + rpm2^2 - rpm3^2), IROS sign
-        M3<Real> R = rot(b.q);
-        M3<Real> Rs = lag ? rot(b.ql) : R;
+        M3<Real> R = rot_fm(b.q);
+        M3<Real> Rs = lag ? rot_fm(b.ql) : R;
         // the chain's constants in VGPRs for the whole loop (fp64: no 64-bit literal operands)
         ChainK<Real> K = chain_consts<Real>();
         HoverConst<Real> Cp = C;

@@ -9,9 +9,13 @@
 // reward / flags straight into mapped memory and publishes `done`.  The host spins on `done` in its
 // own memory, so one env.step is two PCIe crossings and the step itself.
 //
-// Exit: the host's stop request, or no request for kPersistIdleTicks (s_memrealtime, 100 MHz): every
-// wave reaches one of the two, so the grid always drains (a host that died leaves a kernel that
-// ends by itself).
+// Exit: the host's stop request, or no request for kPersistIdleTicks (s_memrealtime, 100 MHz).  The
+// idle exit is ONE grid-wide decision: only workgroup 0 times out; it publishes `kstop` before it
+// leaves and the other workgroups leave when they see it.  Every workgroup marks `exited[b]` on
+// its way out, so a host that posted a request just as workgroup 0 timed out fails fast (the
+// step may be partial) instead of waiting on a done word that never comes.  Every wave reaches
+// one of the exits, so the grid always drains (a host that died leaves a kernel that ends by
+// itself).
 #pragma once
 
 #include "hover_kernel.h"
@@ -26,8 +30,10 @@ constexpr uint64_t kPersistIdleTicks = 1000000000ull;     // 10 s without a requ
 struct PersistCtl {
     uint32_t req;                        // host: sequence number of the requested step, kPersistStop
     uint32_t status;                     // device: 1 running, 2 exited
-    uint32_t pad[14];
+    uint32_t kstop;                      // device (workgroup 0): idle timeout, every workgroup leaves
+    uint32_t pad[13];
     uint32_t done[kPersistMaxBlocks];    // device: per workgroup, the last request it finished
+    uint32_t exited[kPersistMaxBlocks];  // device: per workgroup, 1 once it has left the loop
 };
 
 // a: HoverArgs whose act / obs / rew / term / trunc / tobs point into the mapped mailbox (device
@@ -55,7 +61,13 @@ __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Rea
             for (;;) {
                 r = __hip_atomic_load(&ctl->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (r != last) break;
-                if (__builtin_amdgcn_s_memrealtime() - t_idle > kPersistIdleTicks) {
+                if (blockIdx.x == 0) {
+                    if (__builtin_amdgcn_s_memrealtime() - t_idle > kPersistIdleTicks) {
+                        __hip_atomic_store(&ctl->kstop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        r = kPersistStop;
+                        break;
+                    }
+                } else if (__hip_atomic_load(&ctl->kstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
                     r = kPersistStop;
                     break;
                 }
@@ -90,6 +102,8 @@ __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Rea
     // the env state the next launch / get_state reads (kernel end releases it too)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&ctl->exited[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_store(&ctl->status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -16,13 +16,13 @@ from gym_pybullet_adrp_amd.envs.hover import HoverAviary  # noqa: E402
 from gym_pybullet_adrp_amd.utils.enums import ActionType, Physics  # noqa: E402
 
 
-def _pair(E, precision, physics=Physics.PYB, act=ActionType.RPM, monkeypatch=None):
-    """the launched env on the row-store step kernel (the template the persistent kernel runs: the
-    LDS-staged variant, chosen at E % 64 == 0, may contract a * b + c differently, 1-ulp differences,
-    test_hover_gpu.test_reset_helper_same_results), and its persistent twin"""
+def _pair(E, precision, physics=Physics.PYB, act=ActionType.RPM):
+    """the launched env on its default kernel (the LDS-staged one with the reset-helper wave when
+    E % 64 == 0, the row-store one otherwise) and its persistent twin: the hover TUs contract a*b+c
+    only within one source expression (csrc/Makefile CONTRACT), so every dispatch form of the step
+    body gives the same bits"""
     kw = dict(num_envs=E, physics=physics, act=act, precision=precision, seed=31, initial_xyzs=[0, 0, 1.0],
               init_noise={"xyz": 0.1, "rpy": 0.2, "vel": 0.3, "omega": 1.0})
-    monkeypatch.setenv("ADRP_STAGE_ROWS", "0")   # (both: b also steps by launch after its persistent run)
     return HoverAviary(**kw), HoverAviary(**kw)
 
 
@@ -30,9 +30,10 @@ def _pair(E, precision, physics=Physics.PYB, act=ActionType.RPM, monkeypatch=Non
 @pytest.mark.parametrize("E,physics,act", [(1, Physics.PYB, ActionType.RPM), (100, Physics.PYB, ActionType.RPM),
                                            (128, Physics.PYB, ActionType.RPM),
                                            (70, Physics.PYB_GND_DRAG_DW, ActionType.ONE_D_RPM),
-                                           (3, Physics.DYN, ActionType.RPM)])
-def test_persistent_bit_identical_to_launched(monkeypatch, E, physics, act, precision):
-    a, b = _pair(E, precision, physics, act, monkeypatch)
+                                           (3, Physics.DYN, ActionType.RPM),
+                                           (192, Physics.PYB, ActionType.RPM)])
+def test_persistent_bit_identical_to_launched(E, physics, act, precision):
+    a, b = _pair(E, precision, physics, act)
     a.reset()
     b.reset()
     A = a.h.A
@@ -83,10 +84,10 @@ def test_persistent_restart_and_close_order():
     p.close()            # no-op after the env is gone
 
 
-def test_persistent_long_run_no_stale_outputs(monkeypatch):
+def test_persistent_long_run_no_stale_outputs():
     """3,000 steps at E = 70 (the case where, without the release before `done`, the host once read
     the previous step's obs rows): every step's outputs bit for bit the launched kernel's"""
-    a, b = _pair(70, "fp64", Physics.PYB_GND_DRAG_DW, ActionType.ONE_D_RPM, monkeypatch)
+    a, b = _pair(70, "fp64", Physics.PYB_GND_DRAG_DW, ActionType.ONE_D_RPM)
     a.reset()
     b.reset()
     rng = np.random.default_rng(9)
@@ -102,5 +103,35 @@ def test_persistent_long_run_no_stale_outputs(monkeypatch):
                     and np.array_equal(tb, ta.cpu().numpy()) and np.array_equal(trb, tra.cpu().numpy())):
                 bad.append(k)
     assert not bad, f"{len(bad)} steps differ, first {bad[:5]}"
+    a.close()
+    b.close()
+
+
+def test_persistent_refuses_reseed_and_state_changes():
+    """while the resident kernel owns the env, reset(seed=...) (adrp_reseed), reset(),
+    set_state and step are refused before any change: the persistent run continues bit for bit like
+    a launched twin that never saw the calls"""
+    a, b = _pair(64, "fp64")
+    a.reset()
+    b.reset()
+    rng = np.random.default_rng(3)
+    acts = rng.uniform(-1, 1, (30, 64, 1, 4)).astype(np.float32)
+    with b.persistent() as p:
+        for k in range(30):
+            if k == 10:
+                with pytest.raises(_lib.AdrpError):
+                    b.reset(seed=123)
+                with pytest.raises(_lib.AdrpError):
+                    b.reset()
+                with pytest.raises(_lib.AdrpError):
+                    b.get_state()
+            oa, ra, _, _, _ = a.step(torch.from_numpy(acts[k]).to(a.device))
+            ob, rb, _, _, _ = p.step(acts[k])
+            np.testing.assert_array_equal(ob, oa.cpu().numpy(), err_msg=f"obs at step {k}")
+            np.testing.assert_array_equal(rb, ra.cpu().numpy(), err_msg=f"reward at step {k}")
+    fa, ia_ = a.get_state()
+    fb, ib_ = b.get_state()
+    np.testing.assert_array_equal(fa.cpu().numpy(), fb.cpu().numpy())
+    np.testing.assert_array_equal(ia_.cpu().numpy(), ib_.cpu().numpy())
     a.close()
     b.close()

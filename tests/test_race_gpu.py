@@ -47,6 +47,18 @@ FLOORS = {"pos": 1e-3, "quat": 1e-3, "vel": 1e-3, "omega": 1e-3, "rpm": 1.0}
 RTOL = {"fp32": 2e-3, "fp64": 2e-3}    # the cap every drone stays under
 FP64_BAR = 1e-6                          # fp64 closed loop: every drone whose int16 firmware moments
                                          # all equal the oracle's (same moment hash) stays within it
+DIFFER_MAX = 0.08                        # ... and at most this fraction of the drone-steps may have a
+                                         # moment hash that differs (a kernel bug that changed
+                                         # the Mellinger output would change every hash, exempting itself
+                                         # from FP64_BAR; measured 2-4 %)
+
+
+def assert_witness_fraction(stats, where=""):
+    """the int16 exemption stays rare: int16_differ <= DIFFER_MAX of the drone-steps compared"""
+    if stats.get("drones"):
+        frac = stats["int16_differ"] / stats["drones"]
+        assert frac <= DIFFER_MAX, (f"{where}{stats['int16_differ']} of {stats['drones']} drone-steps ({frac:.1%}) "
+                                    f"have a firmware moment hash that differs from the oracle's (bound {DIFFER_MAX:.0%})")
 
 
 def pair(level, N, physics, mode, reward, E, **kw):
@@ -298,6 +310,7 @@ def test_teacher_forced_step(level, N, physics, mode, reward, precision):
         np.testing.assert_array_equal(tr_g.cpu().numpy(), tr_o)
         np.testing.assert_allclose(rew_g.cpu().numpy(), rew_o, rtol=1e-3, atol=1e-4)
     print(level, physics, precision, worst, stats)
+    assert_witness_fraction(stats, f"{level} {physics.name}: ")
     env.close()
 
 
@@ -622,6 +635,7 @@ def test_full_size_subset_vs_oracle(E, N, level, physics, mode, precision):
         for n in np.flatnonzero(ig[kf, sl] != io[kf]):
             assert abs(contact_margin(o.cfg, fo, names, n)) < 1e-4, f"env {e} drone {n}: flags differ"
     print(f"{level} {physics.name} {precision}: {48 * N} drones, int16 witness {stats}")
+    assert_witness_fraction(stats, f"{level} {physics.name}: ")
     env.close()
 
 

@@ -204,3 +204,47 @@ def test_bench_gather_record_graph_and_eager_fallback(refuse):
             assert "graph_capture_error" not in rec and "HIP graph" in rec["timed_region"]
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_hover_ragged_shards_bit_identical(precision):
+    """One env's step does not depend on its batch (envs/BaseAviary.py:262-387 steps each env on
+    its own): HoverAviary at BASELINE config 2's size, E = 4,096 on ONE handle (the LDS-staged kernel
+    with its reset-helper wave, E % 64 == 0) against two ragged env_offset shards of 1,000 + 3,096
+    (the row-store kernel, partial last wave).  The hover TUs contract a*b+c only within one source
+    expression (csrc/Makefile CONTRACT), so obs, reward, flags, terminal obs and the whole SoA state
+    are bit for bit equal over 60 env.steps with auto-resets."""
+    from gym_pybullet_adrp_amd.envs.hover import HoverAviary
+    kw = dict(precision=precision, seed=4242, initial_xyzs=[0, 0, 1.0],
+              init_noise={"xyz": 0.1, "rpy": 0.3, "vel": 0.3, "omega": 1.0})
+    one = HoverAviary(num_envs=4096, **kw)
+    parts = [HoverAviary(num_envs=1000, env_offset=0, **kw), HoverAviary(num_envs=3096, env_offset=1000, **kw)]
+    cut = [0, 1000, 4096]
+    o1, _ = one.reset()
+    os_ = torch.cat([p.reset()[0] for p in parts])
+    assert torch.equal(o1, os_)
+    rng = np.random.default_rng(17)
+    done = 0
+    for k in range(60):
+        a = rng.uniform(-1, 1, (4096, 1, 4)).astype(np.float32)
+        if k % 20 >= 12:
+            a[::3] = 1.0                       # climb out of bounds: truncations, auto-resets
+        at = torch.from_numpy(a).to(one.device)
+        o1, r1, te1, tr1, i1 = one.step(at)
+        outs = [p.step(at[cut[j]:cut[j + 1]].contiguous()) for j, p in enumerate(parts)]
+        assert torch.equal(o1, torch.cat([o[0] for o in outs])), f"obs differ at step {k}"
+        assert torch.equal(r1, torch.cat([o[1] for o in outs])), f"reward differs at step {k}"
+        assert torch.equal(te1, torch.cat([o[2] for o in outs])) and torch.equal(tr1, torch.cat([o[3] for o in outs]))
+        d = te1 | tr1
+        tob = torch.cat([o[4]["terminal_observation"] for o in outs])
+        assert torch.equal(i1["terminal_observation"][d], tob[d]), f"terminal obs differ at step {k}"
+        done += int(d.sum())
+    assert done > 0, "the run should exercise auto-reset"
+    f1, n1 = one.get_state()
+    fs = torch.cat([p.get_state()[0] for p in parts], 1)
+    ns = torch.cat([p.get_state()[1] for p in parts], 1)
+    assert torch.equal(n1, ns)
+    np.testing.assert_array_equal(f1.cpu().numpy(), fs.cpu().numpy())
+    for p in parts:
+        p.close()
+    one.close()
