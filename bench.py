@@ -682,17 +682,20 @@ def bench_config1(args, dev, cpu_seconds, with_cpu):
 def bench_sb3_loop(args, dev, E=ENVS_PER_GPU, K=200, W=20):
     """SB3's side of the boundary (examples/learn.py:53-57 make_vec_env + PPO.collect_rollouts):
     numpy actions in, numpy obs / rewards / dones / infos out, through vec_env.AviaryVecEnv, on
-    the `value` workload.  packed = one packed device buffer, one async copy into pinned memory,
-    one wait, lazy infos; legacy = per-tensor .cpu() copies and a dict per env."""
+    the `value` workload.  packed = the adapter's default: one C call per step (adrp_vec_step: the
+    kernels read the actions from and write the outputs into pinned host blocks, a ring of 3 whose
+    views are returned), lazy infos; packed_copy = one packed device buffer, one async copy into
+    pinned memory, one wait, fresh arrays (DummyVecEnv's copy semantics); legacy = per-tensor .cpu()
+    copies and a dict per env."""
     from gym_pybullet_adrp_amd.vec_env import AviaryVecEnv
     make = hover_make(args.precision, args.physics, dev)
     rng = np.random.default_rng(1)
     acts = rng.uniform(-1, 1, (16, E, 1, 4)).astype(np.float32)
     rec = {"workload": f"HoverAviary {E} envs ({args.precision}) stepped through the SB3 VecEnv protocol "
                        "(numpy actions in, numpy obs / rewards / dones / infos out, auto-reset infos)"}
-    for name, packed in (("packed", True), ("legacy", False)):
+    for name, kw in (("packed", {}), ("packed_copy", {"direct": False}), ("legacy", {"packed": False})):
         env = make(num_envs=E, env_offset=0)
-        v = AviaryVecEnv(env, packed=packed)
+        v = AviaryVecEnv(env, **kw)
         v.reset()
         for k in range(W):
             v.step(acts[k % 16])

@@ -110,6 +110,10 @@ def load():
     lib.adrp_memcpy_async.restype = I
     lib.adrp_stream_synchronize.argtypes = [P]
     lib.adrp_stream_synchronize.restype = I
+    lib.adrp_vec_bind.argtypes = [P, I, ctypes.POINTER(abi.AdrpVecIO)]
+    lib.adrp_vec_bind.restype = I
+    lib.adrp_vec_step.argtypes = [P, I, P]
+    lib.adrp_vec_step.restype = I
     if hasattr(lib, "adrp_math_probe"):      # (A/B runs may load an older build without it)
         lib.adrp_math_probe.argtypes = [I, P, P, I, P]
         lib.adrp_math_probe.restype = I

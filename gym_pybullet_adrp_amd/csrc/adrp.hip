@@ -537,6 +537,59 @@ extern "C" int adrp_step(adrp_t* h, const float* act_dev, float* obs_dev, float*
 }
 
 // ---------------------------------------------------------------------------------------------
+// SB3 host path in one call per step (vec_env.py): pinned host blocks mapped into the device
+// ---------------------------------------------------------------------------------------------
+int vec_compact_launch(const adrp_vec_io& d, int n, int rf, hipStream_t s);
+
+extern "C" int adrp_vec_bind(adrp_t* h, int slot, const adrp_vec_io* io) {
+    if (!h || !io || slot < 0 || slot >= ADRP_VEC_SLOTS) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: arguments");
+    if (!io->act || !io->obs || !io->rew || !io->term || !io->trunc || !io->done || !io->count || !io->idx ||
+        (io->cap > 0 && !io->rows) || io->cap < 0 || !io->term_dev || !io->trunc_dev || !io->tobs_dev || !io->idx_dev)
+        return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: NULL pointer");
+    DeviceGuard g(h->device);
+    adrp_vec_io d = *io;
+    // host addresses -> the device's view of the same pinned pages
+    auto map = [&](const void* p, void** out) { return hipHostGetDevicePointer(out, const_cast<void*>(p), 0); };
+    void* t = nullptr;
+    if (map(io->act, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: act is not pinned host memory");
+    d.act = (const float*)t;
+    if (map(io->obs, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: obs is not pinned host memory");
+    d.obs = (float*)t;
+    if (map(io->rew, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: rew is not pinned host memory");
+    d.rew = (float*)t;
+    if (map(io->term, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: term is not pinned host memory");
+    d.term = (uint8_t*)t;
+    if (map(io->trunc, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: trunc is not pinned host memory");
+    d.trunc = (uint8_t*)t;
+    if (map(io->done, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: done is not pinned host memory");
+    d.done = (uint8_t*)t;
+    if (map(io->count, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: count is not pinned host memory");
+    d.count = (int32_t*)t;
+    if (map(io->idx, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: idx is not pinned host memory");
+    d.idx = (int32_t*)t;
+    if (io->cap > 0) {
+        if (map(io->rows, &t) != hipSuccess) return seterr(h, ADRP_ERR_INVALID, "adrp_vec_bind: rows is not pinned host memory");
+        d.rows = (float*)t;
+    }
+    h->vio[slot] = d;
+    h->vbound[slot] = true;
+    return ADRP_OK;
+}
+
+extern "C" int adrp_vec_step(adrp_t* h, int slot, void* stream) {
+    if (!h || slot < 0 || slot >= ADRP_VEC_SLOTS || !h->vbound[slot])
+        return seterr(h, ADRP_ERR_INVALID, "adrp_vec_step: slot not bound (adrp_vec_bind)");
+    const adrp_vec_io& d = h->vio[slot];
+    int rc = adrp_step(h, d.act, d.obs, d.rew, d.term_dev, d.trunc_dev, d.tobs_dev, stream);
+    if (rc != ADRP_OK) return rc;
+    DeviceGuard g(h->device);
+    if (vec_compact_launch(d, h->E, h->N * h->D, (hipStream_t)stream) != ADRP_OK)
+        return seterr(h, ADRP_ERR_DEVICE, "adrp_vec_step: compaction launch");
+    HIPCHK(h, hipStreamSynchronize((hipStream_t)stream));
+    return ADRP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
 // high-level command mode (commander.h)
 // ---------------------------------------------------------------------------------------------
 extern "C" int adrp_enable_commands(adrp_t* h) {
@@ -748,8 +801,12 @@ extern "C" int adrp_persistent_begin(adrp_t* h, void** act, void** obs, void** r
     DeviceGuard g(h->device);
     HIPCHK(h, hipDeviceSynchronize());   // every step / reset / set_state issued before is in the state
     const size_t E = size_t(h->E), D = size_t(h->D), A = size_t(h->A);
+    // line mode (BASELINE config 1: E = 1): the actions and the request tag in one 64-byte line
+    // (ADRP_PERSIST_LINE=0 keeps the request word + action rows form)
+    const char* lm = getenv("ADRP_PERSIST_LINE");
+    h->pline = E * A <= size_t(kPersistLineWords - 1) && !(lm && atoi(lm) == 0);
     size_t off = a64(sizeof(PersistCtl));
-    const size_t sizes[6] = {E * A * 4, E * D * 4, E * 4, E, E, E * D * 4};
+    const size_t sizes[6] = {h->pline ? size_t(4 * kPersistLineWords) : E * A * 4, E * D * 4, E * 4, E, E, E * D * 4};
     for (int k = 0; k < 6; ++k) {
         h->poff[k] = off;
         off += a64(sizes[k]);
@@ -820,7 +877,9 @@ extern "C" int adrp_persistent_step(adrp_t* h) {
     uint32_t seq = h->pseq + 1;
     if (seq == kPersistStop) seq = 1;
     h->pseq = seq;
-    __atomic_store_n(&ctl->req, seq, __ATOMIC_RELEASE);   // the action bytes written before it are visible first
+    // the action bytes written before it are visible first (x86 stores are not reordered; release)
+    if (h->pline) __atomic_store_n((uint32_t*)((char*)h->pbox + h->poff[0]) + (kPersistLineWords - 1), seq, __ATOMIC_RELEASE);
+    else __atomic_store_n(&ctl->req, seq, __ATOMIC_RELEASE);
     const int nb = (h->E + kStepBlock - 1) / kStepBlock;
     for (int b = 0; b < nb; ++b) {
         unsigned spins = 0;
@@ -849,6 +908,7 @@ extern "C" int adrp_persistent_end(adrp_t* h) {
     DeviceGuard g(h->device);
     PersistCtl* ctl = (PersistCtl*)h->pbox;
     __atomic_store_n(&ctl->req, kPersistStop, __ATOMIC_RELEASE);
+    if (h->pline) __atomic_store_n((uint32_t*)((char*)h->pbox + h->poff[0]) + (kPersistLineWords - 1), kPersistStop, __ATOMIC_RELEASE);
     const hipError_t e = hipStreamSynchronize(h->pstream);
     hipStreamDestroy(h->pstream);
     hipHostFree(h->pbox);

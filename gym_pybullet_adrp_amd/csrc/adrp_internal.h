@@ -58,7 +58,11 @@ struct adrp_handle {
     void* pbox = nullptr;         // host address of the mapped mailbox (PersistCtl + buffers), or null
     hipStream_t pstream = nullptr;
     uint32_t pseq = 0;
+    bool pline = false;           // line mode: action + request tag in one 64-byte line (E * A <= 15)
     size_t poff[6] = {0, 0, 0, 0, 0, 0};   // act, obs, rew, term, trunc, tobs byte offsets in pbox
+    // SB3 host path (adrp_vec_bind / adrp_vec_step): the bound slots, host pointers translated
+    adrp_vec_io vio[ADRP_VEC_SLOTS];
+    bool vbound[ADRP_VEC_SLOTS] = {false, false, false, false};
     // kernel timing (adrp_profile_begin/end)
     std::vector<hipEvent_t> ev_start, ev_stop;
     int prof_cap = 0, prof_n = 0;

@@ -565,9 +565,11 @@ __device__ __forceinline__ void stage_row(float4* lds_row, const float o12[12], 
 // stream at E = 4096, where nearly every wave has a done lane) on another SIMD, into LDS; the
 // chain wave, issue-bound at one instruction per 4 cycles, only copies it for its done lanes.
 // SYS: the action rows live in host-mapped memory written by the host while the kernel runs
-// (hover_persist.h): they are read with system-scope loads, which no GPU cache serves.
-template <typename Real, int PH, int A, int B, int SC, bool STG = false, int CTL = 0, bool HELP = false, bool SYS = false>
-__device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const HoverConst<Real>& C) {
+// (hover_persist.h): 1 = they are read with system-scope loads, which no GPU cache serves; 2 = the
+// caller already read them (pre[0..A-1], the persistent kernel's line mode).
+template <typename Real, int PH, int A, int B, int SC, bool STG = false, int CTL = 0, bool HELP = false, int SYS = 0>
+__device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const HoverConst<Real>& C,
+                                                const float* pre = nullptr) {
     constexpr int BR = B > 0 ? B : 1;
     constexpr bool DRAG = (PH == ADRP_PHYS_PYB_DRAG || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
     constexpr bool DYN = (PH == ADRP_PHYS_DYN);
@@ -643,7 +645,10 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     RACE_MARK(t0);
     // ---- issue every load up front: action, the whole ring, ints, state ----
     float act[A];
-    if constexpr (SYS) {
+    if constexpr (SYS == 2) {
+#pragma unroll
+        for (int j = 0; j < A; ++j) act[j] = pre[j];
+    } else if constexpr (SYS == 1) {
         uint32_t* sa = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(a.act)) + size_t(e) * A;
 #pragma unroll
         for (int j = 0; j < A; ++j)

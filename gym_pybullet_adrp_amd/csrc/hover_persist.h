@@ -25,6 +25,7 @@ namespace adrp {
 constexpr uint32_t kPersistStop = 0xFFFFFFFFu;
 constexpr int kPersistMaxBlocks = 16;                     // E <= 16 * 64 envs
 constexpr uint64_t kPersistIdleTicks = 1000000000ull;     // 10 s without a request ends the kernel
+constexpr int kPersistLineWords = 16;                     // line mode: 64-byte action line, tag in word 15
 
 // the control block at the head of the mapped mailbox
 struct PersistCtl {
@@ -48,13 +49,62 @@ struct PersistCtl {
 //     become clean, they are not evicted) and stores done; the host reads the outputs after it
 //     sees done.  Without the release the done word could reach host memory before the last
 //     output rows (seen once in the E = 70 bit-identity test: 69 stale obs words at step 1).
-template <typename Real, int PH, int A, int B, bool DEF>
+//
+// LINE (E * A <= 15, one workgroup: BASELINE config 1's single env): the action floats and the
+// request tag share ONE 64-byte line of the mailbox (tag in its last word, written by the host after
+// the floats).  The wave polls the whole line with one 16-lane load, so the load that sees the new
+// tag has already brought the action: one host round trip per step instead of two (tag, then rows).
+template <typename Real, int PH, int A, int B, bool DEF, bool LINE>
 __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Real> a, PersistCtl* ctl) {
     __shared__ uint32_t cmd;
     if (blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_store(&ctl->status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t last = 0;
     uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+    if constexpr (LINE) {
+        static_assert(kStepBlock == 64, "line mode: one wave per workgroup");
+        const uint32_t* line = reinterpret_cast<const uint32_t*>(a.act);
+        const int lane = threadIdx.x;
+        for (;;) {
+            uint32_t v = 0, r;
+            for (;;) {
+                if (lane < kPersistLineWords)
+                    v = __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                r = __builtin_amdgcn_readlane(v, kPersistLineWords - 1);
+                if (r != last) break;
+                if (__builtin_amdgcn_s_memrealtime() - t_idle > kPersistIdleTicks) {
+                    r = kPersistStop;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (r == kPersistStop) break;
+            float pre[A];
+            const int src = lane * A <= kPersistLineWords - 1 - A ? lane * A : 0;   // lanes >= E leave the body at once
+#pragma unroll
+            for (int j = 0; j < A; ++j) pre[j] = __uint_as_float(__shfl(v, src + j));
+            if constexpr (DEF) {
+                constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
+                hover_step_body<Real, PH, A, B, C.S, false, 0, false, 2>(a, C, pre);
+            } else {
+                hover_step_body<Real, PH, A, B, 0, false, 0, false, 2>(a, *a.c, pre);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&ctl->done[0], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            last = r;
+            t_idle = __builtin_amdgcn_s_memrealtime();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0) {
+            __hip_atomic_store(&ctl->exited[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&ctl->status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
     for (;;) {
         if (threadIdx.x == 0) {
             uint32_t r;
@@ -81,9 +131,9 @@ __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Rea
         if (r == kPersistStop) break;
         if constexpr (DEF) {
             constexpr HoverConst<Real> C = cf2x_consts<Real>(PH);
-            hover_step_body<Real, PH, A, B, C.S, false, 0, false, true>(a, C);
+            hover_step_body<Real, PH, A, B, C.S, false, 0, false, 1>(a, C);
         } else {
-            hover_step_body<Real, PH, A, B, 0, false, 0, false, true>(a, *a.c);
+            hover_step_body<Real, PH, A, B, 0, false, 0, false, 1>(a, *a.c);
         }
         // every output store of every wave has completed, then ONE system-scope release makes them
         // visible to the host before done: a completed store is not yet a visible one (the flag can

@@ -9,16 +9,16 @@
 #include "adrp_internal.h"
 #include "hover_persist.h"
 
-template <typename Real, int A, int B, bool DEF>
+template <typename Real, int A, int B, bool DEF, bool LINE>
 static void launch_persist_ph(const HoverArgs<Real>& a, PersistCtl* ctl, int physics, dim3 grid, hipStream_t s) {
     const dim3 blk(kStepBlock);
     switch (physics) {
-        case ADRP_PHYS_PYB: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB, A, B, DEF>), grid, blk, 0, s, a, ctl); break;
-        case ADRP_PHYS_DYN: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_DYN, A, B, DEF>), grid, blk, 0, s, a, ctl); break;
-        case ADRP_PHYS_PYB_GND: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB_GND, A, B, DEF>), grid, blk, 0, s, a, ctl); break;
-        case ADRP_PHYS_PYB_DRAG: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B, DEF>), grid, blk, 0, s, a, ctl); break;
-        case ADRP_PHYS_PYB_DW: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB_DW, A, B, DEF>), grid, blk, 0, s, a, ctl); break;
-        default: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B, DEF>), grid, blk, 0, s, a, ctl); break;
+        case ADRP_PHYS_PYB: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB, A, B, DEF, LINE>), grid, blk, 0, s, a, ctl); break;
+        case ADRP_PHYS_DYN: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_DYN, A, B, DEF, LINE>), grid, blk, 0, s, a, ctl); break;
+        case ADRP_PHYS_PYB_GND: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB_GND, A, B, DEF, LINE>), grid, blk, 0, s, a, ctl); break;
+        case ADRP_PHYS_PYB_DRAG: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB_DRAG, A, B, DEF, LINE>), grid, blk, 0, s, a, ctl); break;
+        case ADRP_PHYS_PYB_DW: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB_DW, A, B, DEF, LINE>), grid, blk, 0, s, a, ctl); break;
+        default: hipLaunchKernelGGL((hover_persist_kernel<Real, ADRP_PHYS_PYB_GND_DRAG_DW, A, B, DEF, LINE>), grid, blk, 0, s, a, ctl); break;
     }
 }
 
@@ -27,12 +27,20 @@ int hover_persist_launch(adrp_t* h, const HoverArgs<Real>& a, void* ctl, hipStre
     const dim3 grid((h->E + kStepBlock - 1) / kStepBlock);
     PersistCtl* c = (PersistCtl*)ctl;
     const int ph = h->cfg.physics;
-    if (h->cf2x && h->B == 15) {
-        if (h->A == 1) launch_persist_ph<Real, 1, 15, true>(a, c, ph, grid, s);
-        else launch_persist_ph<Real, 4, 15, true>(a, c, ph, grid, s);
+    if (h->pline) {   // line mode (E * A <= 15): the action and its request tag in one 64-byte line
+        if (h->cf2x && h->B == 15) {
+            if (h->A == 1) launch_persist_ph<Real, 1, 15, true, true>(a, c, ph, grid, s);
+            else launch_persist_ph<Real, 4, 15, true, true>(a, c, ph, grid, s);
+        } else {
+            if (h->A == 1) launch_persist_ph<Real, 1, 0, false, true>(a, c, ph, grid, s);
+            else launch_persist_ph<Real, 4, 0, false, true>(a, c, ph, grid, s);
+        }
+    } else if (h->cf2x && h->B == 15) {
+        if (h->A == 1) launch_persist_ph<Real, 1, 15, true, false>(a, c, ph, grid, s);
+        else launch_persist_ph<Real, 4, 15, true, false>(a, c, ph, grid, s);
     } else {
-        if (h->A == 1) launch_persist_ph<Real, 1, 0, false>(a, c, ph, grid, s);
-        else launch_persist_ph<Real, 4, 0, false>(a, c, ph, grid, s);
+        if (h->A == 1) launch_persist_ph<Real, 1, 0, false, false>(a, c, ph, grid, s);
+        else launch_persist_ph<Real, 4, 0, false, false>(a, c, ph, grid, s);
     }
     HIPCHK(h, hipGetLastError());
     return ADRP_OK;

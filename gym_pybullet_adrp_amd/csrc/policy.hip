@@ -353,6 +353,67 @@ extern "C" int adrp_compact_rows(const uint8_t* term, const uint8_t* trunc, cons
     return ADRP_OK;
 }
 
+// adrp_vec_step's compaction (the host block of one step): flags term / trunc / done copied out of the
+// device, the finished envs' ids into the device scratch (the row gather reads them from there) and
+// the host block, the first min(count, cap) terminal rows into the host block.  Same ranking as
+// compact_rows_kernel.
+__global__ void __launch_bounds__(1024) vec_compact_kernel(const uint8_t* __restrict__ term, const uint8_t* __restrict__ trunc,
+                                                           const float* __restrict__ rows, int n, int rf, int cap,
+                                                           uint8_t* __restrict__ term_o, uint8_t* __restrict__ trunc_o,
+                                                           uint8_t* __restrict__ done_o, int32_t* __restrict__ count,
+                                                           int32_t* __restrict__ idx_dev, int32_t* __restrict__ idx_o,
+                                                           float* __restrict__ out) {
+    __shared__ int wsum[16];
+    __shared__ int total;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int base = 0;
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+        const int i = c0 + tid;
+        const uint8_t te = i < n ? term[i] : 0, tr = i < n ? trunc[i] : 0;
+        const bool f = (te | tr) != 0;
+        if (i < n) {
+            term_o[i] = te;
+            trunc_o[i] = tr;
+            done_o[i] = f;
+        }
+        const uint64_t b = __ballot(f);
+        if (lane == 0) wsum[wave] = __popcll(b);
+        __syncthreads();
+        int off = base, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const int c = wsum[w];
+            off += w < wave ? c : 0;
+            tot += c;
+        }
+        if (f) {
+            const int r = off + __popcll(b & ((uint64_t(1) << lane) - 1));
+            idx_dev[r] = i;
+            idx_o[r] = i;
+        }
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        count[0] = base;
+        total = base;
+    }
+    __syncthreads();
+    const int m = total < cap ? total : cap;
+    const long long nf = (long long)m * rf;
+    for (long long k = tid; k < nf; k += 1024) {
+        const int j = int(k / rf), c = int(k - (long long)j * rf);
+        out[k] = rows[(long long)idx_dev[j] * rf + c];
+    }
+}
+
+int vec_compact_launch(const adrp_vec_io& d, int n, int rf, hipStream_t s) {
+    hipLaunchKernelGGL(vec_compact_kernel, dim3(1), dim3(1024), 0, s, d.term_dev, d.trunc_dev, d.tobs_dev, n, rf, d.cap,
+                       d.term, d.trunc, d.done, d.count, d.idx_dev, d.idx, d.rows);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ADRP_OK : ADRP_ERR_DEVICE;
+}
+
 // the host path's copies and wait without a framework dispatch in between (vec_env.py): kind 1 =
 // host -> device, 2 = device -> host (pinned host memory: asynchronous on the stream)
 extern "C" int adrp_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream) {

@@ -23,6 +23,7 @@ MATH_EXP_TAB, MATH_ATAN2_NC, MATH_FDIV_RCP = 21, 22, 23
 RACE_COMPARE, RACE_COMPETE = 0, 1
 POLICY_TANH, POLICY_RELU = 0, 1
 POLICY_RAW, POLICY_RELATIVE, POLICY_ABSOLUTE = 0, 1, 2
+VEC_SLOTS = 4   # ADRP_VEC_SLOTS
 
 _d = ctypes.c_double
 _i32 = ctypes.c_int32
@@ -122,3 +123,11 @@ def to_list(arr):
     for x in arr:
         out.append(to_list(x) if hasattr(x, "__len__") else x)
     return out
+
+
+class AdrpVecIO(ctypes.Structure):
+    """adrp_vec_io (include/adrp.h): one host block of the SB3 host path (adrp_vec_bind)"""
+    _p = ctypes.c_void_p
+    _fields_ = [("act", _p), ("obs", _p), ("rew", _p), ("term", _p), ("trunc", _p), ("done", _p),
+                ("count", _p), ("idx", _p), ("rows", _p), ("cap", ctypes.c_int),
+                ("term_dev", _p), ("trunc_dev", _p), ("tobs_dev", _p), ("idx_dev", _p)]

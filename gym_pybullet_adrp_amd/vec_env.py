@@ -16,7 +16,16 @@ returns the device tensors untouched (for torch-native learners).  When
 stable_baselines3 is importable the class derives from its ``VecEnv`` so
 ``isinstance`` checks in SB3 pass; otherwise it is a plain class with the same methods.
 
-Host path (SURVEY.md §7 hard part 7).  The env writes obs / reward / terminated / truncated into
+Host path (SURVEY.md §7 hard part 7).  Default (``direct``): ONE C call per step
+(include/adrp.h ``adrp_vec_step``): the step kernel reads the actions from and writes obs / reward
+straight into a pinned host block (mapped into the device: no copy engine, no separate copy call), a
+compaction kernel writes the flags, the finished envs' ids and their terminal rows into the same
+block, and the host waits once.  The blocks form a ring of ``ring`` (default 3, at most 4): the
+returned obs / rewards / dones and the infos' terminal observations are views of the block the step
+wrote, valid until ``ring`` more steps have been taken (SB3's OnPolicyAlgorithm.collect_rollouts
+copies obs into its rollout buffer one step later and reads the infos at once, so the default ring
+is safe for it; ``zero_copy=False`` returns fresh copies, DummyVecEnv's semantics, at ~15 us more
+per step for 4,096 envs).  Fallback (``direct=False``, or a library without adrp_vec_step): the env writes obs / reward / terminated / truncated into
 ONE packed device buffer (``bind_outputs``) and its terminal observations into a device buffer of
 their own; ``adrp_compact_rows`` then gathers the finished envs' ids and terminal rows behind the
 flags in the packed buffer, so ``step_wait`` issues one asynchronous copy of about the obs size into
@@ -29,6 +38,7 @@ arrays are fresh copies (DummyVecEnv semantics) unless ``zero_copy=True``: then 
 of a ring of ``ring`` pinned buffers, valid until ``ring`` more steps have been taken.
 """
 import contextlib
+import ctypes
 import types
 from collections.abc import Sequence
 
@@ -36,6 +46,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .utils import abi
 
 _NO_INFO = types.MappingProxyType({})
 
@@ -93,21 +104,27 @@ except ImportError:  # pragma: no cover
 class AviaryVecEnv(_VecEnvBase):
     """SB3 VecEnv over one batched aviary (HoverAviary / MultiRaceAviary of this package)."""
 
-    def __init__(self, env, as_torch=False, zero_copy=False, ring=2, packed=None, terminal_rows=None):
+    def __init__(self, env, as_torch=False, zero_copy=None, ring=3, packed=None, terminal_rows=None, direct=None):
         self.env = env
         self.num_envs = env.num_envs
         self.observation_space = env.observation_space
         self.action_space = env.action_space
         self.render_mode = None
         self.as_torch = as_torch
-        self.zero_copy = zero_copy
         self._actions = None
         self._seed = None
         # packed host path: numpy outputs of an env that can write into caller buffers (None: auto)
         self._packed = (not as_torch) and hasattr(env, "bind_outputs") and packed is not False
+        # direct: the step kernel reads / writes the pinned host blocks itself (adrp_vec_step)
+        lib = _lib.load() if self._packed and env._obs.is_cuda else None
+        self._direct = self._packed and direct is not False and getattr(lib, "adrp_vec_step", None) is not None
+        # zero_copy (None: auto) - views of the ring blocks on the direct path, copies otherwise
+        self.zero_copy = self._direct if zero_copy is None else bool(zero_copy)
         if terminal_rows is not None:   # initial terminal-row capacity of the packed copy (it grows)
             self._cap_req = max(1, min(self.num_envs, int(terminal_rows)))
-        if self._packed:
+        if self._direct:
+            self._bind_direct(max(1, min(int(ring), abi.VEC_SLOTS)))
+        elif self._packed:
             self._bind_packed(max(1, int(ring)))
         if _VecEnvBase is not object:  # pragma: no cover
             _VecEnvBase.__init__(self, self.num_envs, self.observation_space, self.action_space)
@@ -172,6 +189,85 @@ class AviaryVecEnv(_VecEnvBase):
         else:
             self._event = None
 
+    def _bind_direct(self, ring):
+        """adrp_vec_bind of `ring` pinned host blocks [obs | reward | terminated | truncated | done |
+        count | done env ids | terminal rows] and the pinned action block; the step's own flags,
+        terminal obs and the compaction's id scratch stay on the device"""
+        env, E = self.env, self.num_envs
+        obs_shape = tuple(env._obs.shape)
+        dev = env._obs.device
+        rf = int(np.prod(obs_shape[1:]))
+        self._rf = rf
+        self._cap = getattr(self, "_cap_req", min(E, max(64, E // 16)))
+        a16 = lambda x: (x + 15) // 16 * 16   # noqa: E731
+        nobs = E * rf * 4
+        o_rew = nobs
+        o_term = a16(o_rew + 4 * E)
+        o_trunc = o_term + E
+        o_done = o_trunc + E
+        o_cnt = a16(o_done + E)
+        o_idx = o_cnt + 16
+        o_rows = a16(o_idx + 4 * E)
+        self._nbytes = a16(o_rows + 4 * rf * self._cap)
+        self._term_dev = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self._trunc_dev = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self._tobs_dev = torch.zeros(obs_shape, dtype=torch.float32, device=dev)
+        self._idx_dev = torch.zeros(E, dtype=torch.int32, device=dev)
+        act_shape = tuple(env._act_shape)
+        if getattr(self, "_act_host", None) is None or tuple(self._act_host.shape) != act_shape:
+            self._act_host = torch.zeros(act_shape, dtype=torch.float32, pin_memory=True)
+            self._act_np = self._act_host.numpy()
+        self._host = [torch.zeros(self._nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(ring)]
+        self._views = []
+        lib = _lib.load()
+        h = env.h.h
+        for k, hb in enumerate(self._host):
+            hn = hb.numpy()
+            base = hb.data_ptr()
+            io = abi.AdrpVecIO(act=self._act_host.data_ptr(), obs=base, rew=base + o_rew, term=base + o_term,
+                               trunc=base + o_trunc, done=base + o_done, count=base + o_cnt, idx=base + o_idx,
+                               rows=base + o_rows, cap=self._cap, term_dev=self._term_dev.data_ptr(),
+                               trunc_dev=self._trunc_dev.data_ptr(), tobs_dev=self._tobs_dev.data_ptr(),
+                               idx_dev=self._idx_dev.data_ptr())
+            if lib.adrp_vec_bind(h, k, ctypes.byref(io)) != 0:
+                raise _lib.AdrpError(f"adrp_vec_bind: {lib.adrp_last_error(h).decode()}")
+            self._views.append((hn[:nobs].view(np.float32).reshape(obs_shape), hn[o_rew:o_rew + 4 * E].view(np.float32),
+                                hn[o_term:o_trunc].view(np.bool_), hn[o_trunc:o_done].view(np.bool_),
+                                hn[o_done:o_done + E].view(np.bool_), hn[o_cnt:o_cnt + 4].view(np.int32),
+                                hn[o_idx:o_idx + 4 * E].view(np.int32),
+                                hn[o_rows:o_rows + 4 * rf * self._cap].view(np.float32).reshape((self._cap,) + obs_shape[1:])))
+        self._slot = 0
+        self._vec_step = lib.adrp_vec_step
+        self._h = h
+        self._dev_index = dev.index
+
+    def _step_wait_direct(self):
+        a = self._actions
+        if isinstance(a, torch.Tensor):
+            self._act_host.copy_(a.reshape(self._act_host.shape))
+        else:
+            self._act_np[...] = np.asarray(a, np.float32).reshape(self._act_np.shape)
+        self._slot = (self._slot + 1) % len(self._host)
+        if self._vec_step(self._h, self._slot, _lib._raw_stream(self._dev_index)) != 0:
+            raise _lib.AdrpError(f"adrp_vec_step: {_lib.load().adrp_last_error(self._h).decode()}")
+        obs, rew, term, trunc, done, cnt, idx_all, rows = self._views[self._slot]
+        n = int(cnt[0])
+        idx = idx_all[:n]
+        if n <= self._cap:
+            tobs = rows[:n]
+        else:   # more finished envs than the block carries: the rest from the device, and a larger
+            # terminal-row region from the next step on (the blocks are re-bound; the env state stays)
+            rest = torch.as_tensor(idx[self._cap:], dtype=torch.long, device=self._tobs_dev.device)
+            tobs = np.concatenate([rows.copy(), self._tobs_dev[rest].cpu().numpy()])
+            self._cap_req = min(self.num_envs, max(2 * self._cap, n + n // 4))
+            idx = idx.copy()
+            self._bind_direct(len(self._host))
+        infos = _StepInfos(self.num_envs, idx, tobs, trunc[idx] & ~term[idx])
+        if not self.zero_copy:
+            obs, rew, done = obs.copy(), rew.copy(), done.copy()
+            infos = _StepInfos(self.num_envs, idx.copy(), tobs.copy(), trunc[idx] & ~term[idx])
+        return obs, rew, done, infos
+
     # ---- conversion ----
     def _out(self, x):
         return x if self.as_torch else x.detach().cpu().numpy()
@@ -180,6 +276,8 @@ class AviaryVecEnv(_VecEnvBase):
     def reset(self):
         seed, self._seed = self._seed, None
         obs, _ = self.env.reset(seed=seed)
+        if self._direct:
+            return obs.cpu().numpy()
         if self._packed:
             with self._on_device():
                 o = self._copy_out()[0]
@@ -260,9 +358,12 @@ class AviaryVecEnv(_VecEnvBase):
     def _on_device(self):
         """the env's device current while the raw C-ABI copies / compaction run: a null (default)
         stream names the current device's, so the work then lands on the env's"""
-        return torch.cuda.device(self._dev.device) if self._dev.is_cuda else contextlib.nullcontext()
+        dev = self.env._obs.device
+        return torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()
 
     def step_wait(self):
+        if self._direct:   # (adrp_vec_step makes the handle's device current itself)
+            return self._step_wait_direct()
         if self._packed:
             with self._on_device():
                 return self._step_wait_packed()
@@ -323,12 +424,12 @@ class AviaryVecEnv(_VecEnvBase):
         return list(indices)
 
 
-def HoverAviaryVec(n_envs=1, as_torch=False, zero_copy=False, **env_kwargs):
+def HoverAviaryVec(n_envs=1, as_torch=False, zero_copy=None, **env_kwargs):
     """``make_vec_env(HoverAviary, env_kwargs=..., n_envs=...)`` counterpart"""
     from .envs.hover import HoverAviary
     return AviaryVecEnv(HoverAviary(num_envs=n_envs, **env_kwargs), as_torch=as_torch, zero_copy=zero_copy)
 
 
-def MultiRaceAviaryVec(n_envs=1, as_torch=False, zero_copy=False, **env_kwargs):
+def MultiRaceAviaryVec(n_envs=1, as_torch=False, zero_copy=None, **env_kwargs):
     from .envs.race import MultiRaceAviary
     return AviaryVecEnv(MultiRaceAviary(num_envs=n_envs, **env_kwargs), as_torch=as_torch, zero_copy=zero_copy)

@@ -378,6 +378,38 @@ int adrp_compact_rows(const uint8_t* term, const uint8_t* trunc, const float* ro
 int adrp_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream);
 int adrp_stream_synchronize(void* stream);
 
+/* SB3 VecEnv host path in ONE call per step (vec_env.py AviaryVecEnv; replaces what
+ * stable_baselines3 DummyVecEnv.step_async / step_wait do around the reference's env.step,
+ * examples/learn.py:53-57, 72): the step kernel reads the actions from, and writes obs / reward
+ * straight into, pinned host memory (device-mapped: no copy engine on the path), a compaction
+ * writes the terminated / truncated / done flags, the finished envs' count and ids and their
+ * terminal rows into the same host block, and the host waits once.  A handle holds
+ * ADRP_VEC_SLOTS such host blocks (a ring: the caller's views of slot k stay valid until slot k is
+ * stepped again); adrp_vec_bind records one (host pointers of hipHostMalloc'd / pinned memory,
+ * translated to device addresses here), adrp_vec_step(h, k, stream) steps into it.  term_dev /
+ * trunc_dev / tobs_dev / idx_dev are the caller's device buffers ([E] u8, [E] u8, [E][N][D] f32,
+ * [E] i32): the step's own flags and terminal obs, the compaction's scratch.  Rows beyond cap are
+ * left in tobs_dev (count says how many envs finished).  Stream-ordered; returns after the wait. */
+#define ADRP_VEC_SLOTS 4
+typedef struct adrp_vec_io {
+    const float* act;            /* host [E][N][A] float32 (read by the step kernel) */
+    float* obs;                  /* host [E][N][D] */
+    float* rew;                  /* host [E] */
+    uint8_t* term;               /* host [E] terminated */
+    uint8_t* trunc;              /* host [E] truncated */
+    uint8_t* done;               /* host [E] terminated | truncated */
+    int32_t* count;              /* host [1] finished envs */
+    int32_t* idx;                /* host [E] their ids, ascending */
+    float* rows;                 /* host [cap][N*D] their terminal rows */
+    int cap;
+    uint8_t* term_dev;
+    uint8_t* trunc_dev;
+    float* tobs_dev;
+    int32_t* idx_dev;
+} adrp_vec_io;
+int adrp_vec_bind(adrp_t* h, int slot, const adrp_vec_io* io);
+int adrp_vec_step(adrp_t* h, int slot, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Parity mode noise (MultiRaceAviary).  The reference draws, per sub-step, the disturbance force
  * of every drone (np_random.<distrib>(low, high), MultiRaceAviary.py:532-537) and then the (N, 4)

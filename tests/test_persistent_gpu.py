@@ -31,7 +31,8 @@ def _pair(E, precision, physics=Physics.PYB, act=ActionType.RPM):
                                            (128, Physics.PYB, ActionType.RPM),
                                            (70, Physics.PYB_GND_DRAG_DW, ActionType.ONE_D_RPM),
                                            (3, Physics.DYN, ActionType.RPM),
-                                           (192, Physics.PYB, ActionType.RPM)])
+                                           (192, Physics.PYB, ActionType.RPM),
+                                           (5, Physics.PYB_GND, ActionType.ONE_D_RPM)])
 def test_persistent_bit_identical_to_launched(E, physics, act, precision):
     a, b = _pair(E, precision, physics, act)
     a.reset()
@@ -84,17 +85,22 @@ def test_persistent_restart_and_close_order():
     p.close()            # no-op after the env is gone
 
 
-def test_persistent_long_run_no_stale_outputs():
+@pytest.mark.parametrize("E,physics,act,steps", [(70, Physics.PYB_GND_DRAG_DW, ActionType.ONE_D_RPM, 3000),
+                                                 (1, Physics.PYB, ActionType.RPM, 5000)])
+def test_persistent_long_run_no_stale_outputs(E, physics, act, steps):
     """3,000 steps at E = 70 (the case where, without the release before `done`, the host once read
-    the previous step's obs rows): every step's outputs bit for bit the launched kernel's"""
-    a, b = _pair(70, "fp64", Physics.PYB_GND_DRAG_DW, ActionType.ONE_D_RPM)
+    the previous step's obs rows), and 5,000 at E = 1 in line mode (the action and its request tag
+    in one 64-byte line, read by one load: a torn read would step on a stale action): every step's
+    outputs bit for bit the launched kernel's, with a fresh random action every step"""
+    a, b = _pair(E, "fp64", physics, act)
     a.reset()
     b.reset()
+    A = a.h.A
     rng = np.random.default_rng(9)
     bad = []
     with b.persistent() as p:
-        for k in range(3000):
-            act = rng.uniform(-1, 1, (70, 1, 1)).astype(np.float32)
+        for k in range(steps):
+            act = rng.uniform(-1, 1, (E, 1, A)).astype(np.float32)
             if (k // 50) % 4 == 1:
                 act[:] = 1.0
             oa, ra, ta, tra, _ = a.step(torch.from_numpy(act).to(a.device))

@@ -118,18 +118,22 @@ def test_hover_and_race_vecenv_on_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["hover", "race"])
 def test_packed_host_path_matches_legacy(kind):
-    """the packed pinned-copy host path returns what the per-tensor .cpu() path returns: same obs,
-    rewards, dones, terminal observations and TimeLimit.truncated (same seed, same actions)"""
+    """the host paths return the same thing: the direct path (adrp_vec_step: the kernels read / write
+    pinned host blocks, views of a ring), the packed pinned-copy path and the per-tensor .cpu() path
+    give the same obs, rewards, dones, terminal observations and TimeLimit.truncated (same seed, same
+    actions); the direct and packed paths start with 2 terminal rows, so steps with more finished envs
+    take the overflow copy and re-bind with a larger region"""
     from gym_pybullet_adrp_amd.vec_env import HoverAviaryVec, MultiRaceAviaryVec
     outs = []
-    for packed in (True, False):
+    for mode in ("direct", "packed", "legacy"):
         if kind == "hover":
             v = HoverAviaryVec(n_envs=256, seed=3, initial_xyzs=[0, 0, 1.0], init_noise={"rpy": 0.3, "omega": 1.0})
         else:
             v = MultiRaceAviaryVec(n_envs=128, race_config="level3", num_drones=4, seed=3)
-        # packed: start with 2 terminal rows, so steps with more finished envs take the second copy
-        v = type(v)(v.env, packed=packed, terminal_rows=2 if packed else None)
-        assert v._packed == packed
+        v = type(v)(v.env, packed=mode != "legacy", direct=mode == "direct",
+                    terminal_rows=2 if mode != "legacy" else None)
+        assert v._packed == (mode != "legacy") and v._direct == (mode == "direct")
+        assert v.zero_copy == (mode == "direct")
         obs = v.reset()
         rng = np.random.default_rng(0)
         seq = [obs.copy()]
@@ -141,23 +145,47 @@ def test_packed_host_path_matches_legacy(kind):
                                    -1).astype(np.float32)
             obs, rew, done, infos = v.step(a)
             seq.append((obs.copy(), rew.copy(), done.copy(),
-                        [(bool(i.get("TimeLimit.truncated")), i.get("terminal_observation")) for i in infos]))
+                        [(bool(i.get("TimeLimit.truncated")), None if i.get("terminal_observation") is None
+                          else np.array(i.get("terminal_observation"))) for i in infos]))
         outs.append(seq)
-        if packed:
+        if mode != "legacy":
             assert v._cap > 2   # more finished envs than terminal rows in some step: grown
         v.close()
-    np.testing.assert_array_equal(outs[0][0], outs[1][0])
-    ndone = 0
-    for (o1, r1, d1, i1), (o2, r2, d2, i2) in zip(outs[0][1:], outs[1][1:]):
-        np.testing.assert_array_equal(o1, o2)
-        np.testing.assert_array_equal(r1, r2)
-        np.testing.assert_array_equal(d1, d2)
-        ndone += int(d1.sum())
-        for (t1, x1), (t2, x2) in zip(i1, i2):
-            assert t1 == t2 and (x1 is None) == (x2 is None)
-            if x1 is not None:
-                np.testing.assert_array_equal(x1, x2)
-    assert ndone > 0
+    for other in outs[1:]:
+        np.testing.assert_array_equal(outs[0][0], other[0])
+        ndone = 0
+        for (o1, r1, d1, i1), (o2, r2, d2, i2) in zip(outs[0][1:], other[1:]):
+            np.testing.assert_array_equal(o1, o2)
+            np.testing.assert_array_equal(r1, r2)
+            np.testing.assert_array_equal(d1, d2)
+            ndone += int(d1.sum())
+            for (t1, x1), (t2, x2) in zip(i1, i2):
+                assert t1 == t2 and (x1 is None) == (x2 is None)
+                if x1 is not None:
+                    np.testing.assert_array_equal(x1, x2)
+        assert ndone > 0
+
+
+@pytest.mark.gpu
+def test_direct_ring_lifetime():
+    """direct host path, ring of 3: the obs / rewards / dones a step returned are still intact two
+    steps later (SB3 copies obs into its rollout buffer one step after), and the third step after
+    reuses the block"""
+    from gym_pybullet_adrp_amd.vec_env import HoverAviaryVec
+    v = HoverAviaryVec(n_envs=128, seed=5, initial_xyzs=[0, 0, 1.0])
+    assert v._direct and v.zero_copy and len(v._host) == 3
+    v.reset()
+    rng = np.random.default_rng(1)
+    hist = []
+    for k in range(6):
+        o, r, d, _ = v.step(rng.uniform(-1, 1, (128, 1, 4)).astype(np.float32))
+        hist.append((o, r, d, o.copy(), r.copy(), d.copy()))
+        for j in range(max(0, k - 2), k + 1):          # the last three steps' views are intact
+            np.testing.assert_array_equal(hist[j][0], hist[j][3])
+            np.testing.assert_array_equal(hist[j][1], hist[j][4])
+            np.testing.assert_array_equal(hist[j][2], hist[j][5])
+    assert np.shares_memory(hist[0][0], hist[3][0])    # the ring wrapped
+    v.close()
 
 
 @pytest.mark.gpu

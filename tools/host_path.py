@@ -60,26 +60,34 @@ for prec in ("fp64", "fp32"):
     env.close()
 
 E = 4096
-env = HoverAviary(num_envs=E, precision="fp64", initial_xyzs=[0, 0, 1.0], seed=1,
-                  init_noise={"rpy": 0.3, "omega": 1.0})
-v = AviaryVecEnv(env, packed=True)
-v.reset()
 acts = np.random.default_rng(1).uniform(-1, 1, (16, E, 1, 4)).astype(np.float32)
 k = [0]
+for name, kw in (("direct", {}), ("packed_copy", {"direct": False})):
+    env = HoverAviary(num_envs=E, precision="fp64", initial_xyzs=[0, 0, 1.0], seed=1,
+                      init_noise={"rpy": 0.3, "omega": 1.0})
+    v = AviaryVecEnv(env, packed=True, **kw)
+    v.reset()
 
+    def vstep():
+        k[0] += 1
+        return v.step(acts[k[0] % 16])
 
-def vstep():
-    k[0] += 1
-    return v.step(acts[k[0] % 16])
-
-
-r = {"vecenv_step_us": per_call(vstep, 300)}
-r["act_in_us"] = per_call(lambda: v._act_in(acts[3]), 300)
-r["env_step_us"] = per_call(lambda: env.step(v._act_dev), 300)
-r["copy_out_us"] = per_call(lambda: v._copy_out(), 300)
-o = v._views[0][0]
-r["obs_numpy_copy_us"] = per_call(lambda: o.copy(), 300)
-out["E4096_vecenv_fp64"] = r
+    r = {"vecenv_step_us": per_call(vstep, 300)}
+    if name == "direct":
+        r["vec_step_call_us"] = per_call(lambda: v._vec_step(v._h, 1, 0), 300)
+        r["act_write_us"] = per_call(lambda: v._act_np.__setitem__(Ellipsis, acts[3]), 300)
+    else:
+        r["act_in_us"] = per_call(lambda: v._act_in(acts[3]), 300)
+        r["env_step_us"] = per_call(lambda: env.step(v._act_dev), 300)
+        r["copy_out_us"] = per_call(lambda: v._copy_out(), 300)
+        o = v._views[0][0]
+        r["obs_numpy_copy_us"] = per_call(lambda: o.copy(), 300)
+    out[f"E4096_vecenv_fp64_{name}"] = r
+    if name == "direct":
+        break_v = v
+        continue
+    v.close()
+v = break_v
 if os.environ.get("HOST_PATH_PROFILE"):
     import cProfile
     import io
