@@ -87,6 +87,8 @@ def load():
     lib.adrp_persistent_end.restype = I
     lib.adrp_race_moment_hash.argtypes = [P, P, ctypes.c_size_t]
     lib.adrp_race_moment_hash.restype = I
+    lib.adrp_race_moment_log.argtypes = [P, P, P, ctypes.c_size_t, I]
+    lib.adrp_race_moment_log.restype = I
     lib.adrp_race_reset_counts.argtypes = [P, P, I]
     lib.adrp_race_reset_counts.restype = I
     lib.adrp_policy_create.argtypes = [I, I, I, I, I, P, P, P, P, P, P, ctypes.POINTER(P)]
@@ -164,6 +166,7 @@ class Handle:
         self.h = h
         self.cfg = cfg
         self.E, self.N = cfg.num_envs, cfg.num_drones
+        self.S = cfg.pyb_freq // cfg.ctrl_freq     # sub-steps per env.step
         self.D = self.lib.adrp_obs_dim(h)
         self.A = self.lib.adrp_act_dim(h)
         nf, ni = ctypes.c_int(), ctypes.c_int()
@@ -283,7 +286,10 @@ class Handle:
         self.cfg.track.obs_wrapper = int(obs_wrapper)
 
     def set_diagnostics(self, enable=True):
-        self._check(self.lib.adrp_set_diagnostics(self.h, 1 if enable else 0), "adrp_set_diagnostics")
+        """True / 1: contact counter, race moment hash; 2: also the race firmware moment log (the
+        step then runs the one-lane race kernel)"""
+        level = int(enable) if not isinstance(enable, bool) else (1 if enable else 0)
+        self._check(self.lib.adrp_set_diagnostics(self.h, level), "adrp_set_diagnostics")
 
     def contact_count(self, reset=True):
         """env-steps that touched the plane contact model since the last reset (diagnostics on)"""
@@ -298,6 +304,17 @@ class Handle:
         self._check(self.lib.adrp_race_moment_hash(self.h, out.ctypes.data_as(ctypes.c_void_p), out.size),
                     "adrp_race_moment_hash")
         return out
+
+    def moment_log(self):
+        """race, diagnostics level 2: (moments int16 [E*N][S][3], calls int32 [E*N]) of the last
+        env.step, the int16 (roll, pitch, yaw) of every firmware call in call order"""
+        import numpy as np
+        n = self.E * self.N
+        out = np.zeros((n, self.S, 3), np.int16)
+        cnt = np.zeros(n, np.int32)
+        self._check(self.lib.adrp_race_moment_log(self.h, out.ctypes.data_as(ctypes.c_void_p),
+                                                  cnt.ctypes.data_as(ctypes.c_void_p), n, self.S), "adrp_race_moment_log")
+        return out, cnt
 
     def reset_counts(self, reset=True):
         """race, diagnostics on: (auto-resets copied from a next-reset image, auto-resets computed

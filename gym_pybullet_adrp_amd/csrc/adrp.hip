@@ -454,7 +454,7 @@ extern "C" void adrp_destroy(adrp_t* h) {
     for (auto e : h->ev_start) hipEventDestroy(e);
     for (auto e : h->ev_stop) hipEventDestroy(e);
     hipFree(h->f); hipFree(h->ring); hipFree(h->ist); hipFree(h->counters); hipFree(h->cblk);
-    hipFree(h->cmdf); hipFree(h->cmdi); hipFree(h->mom_hash);
+    hipFree(h->cmdf); hipFree(h->cmdi); hipFree(h->mom_hash); hipFree(h->mom_log); hipFree(h->mom_log_n);
     hipFree(h->img_f); hipFree(h->img_i); hipFree(h->img_row); hipFree(h->img_ep);
     delete h;
 }
@@ -960,7 +960,31 @@ extern "C" int adrp_set_diagnostics(adrp_t* h, int enable) {
         }
         if (hipMemset(h->mom_hash, 0, bytes) != hipSuccess) return seterr(h, ADRP_ERR_DEVICE, "adrp_set_diagnostics");
     }
-    h->diagnostics = enable ? 1 : 0;
+    if (enable >= 2 && h->cfg.task == ADRP_TASK_RACE && !h->mom_log) {
+        DeviceGuard g(h->device);
+        const size_t EN = size_t(h->E) * h->N;
+        if (hipMalloc((void**)&h->mom_log, EN * size_t(h->S) * 3 * sizeof(int16_t)) != hipSuccess ||
+            hipMalloc((void**)&h->mom_log_n, EN * sizeof(int32_t)) != hipSuccess)
+            return seterr(h, ADRP_ERR_OOM, "adrp_set_diagnostics: hipMalloc failed (moment log)");
+        if (hipMemset(h->mom_log_n, 0, EN * sizeof(int32_t)) != hipSuccess)
+            return seterr(h, ADRP_ERR_DEVICE, "adrp_set_diagnostics");
+    }
+    h->diagnostics = enable >= 2 && h->cfg.task == ADRP_TASK_RACE ? 2 : enable ? 1 : 0;
+    return ADRP_OK;
+}
+
+// race diagnostics level 2: the int16 (roll, pitch, yaw) moments of every firmware call of the last
+// env.step, per drone in call order, and the number of calls (the one-lane kernel records them)
+extern "C" int adrp_race_moment_log(adrp_t* h, int16_t* out, int32_t* counts, size_t n, int max_calls) {
+    if (!h || !out || !counts) return seterr(h, ADRP_ERR_INVALID, "adrp_race_moment_log: NULL argument");
+    if (h->cfg.task != ADRP_TASK_RACE || !h->mom_log || h->diagnostics < 2)
+        return seterr(h, ADRP_ERR_INVALID, "adrp_race_moment_log: a race handle with diagnostics level 2");
+    if (n != size_t(h->E) * h->N || max_calls != h->S)
+        return seterr(h, ADRP_ERR_INVALID, "adrp_race_moment_log: n != E * N or max_calls != sub-steps");
+    DeviceGuard g(h->device);
+    HIPCHK(h, hipDeviceSynchronize());
+    HIPCHK(h, hipMemcpy(out, h->mom_log, n * size_t(max_calls) * 3 * sizeof(int16_t), hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(counts, h->mom_log_n, n * sizeof(int32_t), hipMemcpyDeviceToHost));
     return ADRP_OK;
 }
 

@@ -46,6 +46,8 @@ struct adrp_handle {
     const double* inj_force = nullptr;
     int diagnostics = 0;
     uint32_t* mom_hash = nullptr; // race diagnostics: [E*N] firmware int16-moment hash of the last step
+    int16_t* mom_log = nullptr;   // race diagnostics level 2: [E*N][S][3] the last step's int16 moments
+    int32_t* mom_log_n = nullptr; //   [E*N] firmware calls per drone
     // race next-reset images (race_quad.h race_refill_q4; four-lane kernel with auto-reset): refilled
     // by a launch every img_period steps (ADRP_RESET_IMAGES=K, 0 = off)
     void* img_f = nullptr;        // Real [RF_N][E*N]
@@ -88,7 +90,8 @@ inline int race_group(int n) { return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : 8; 
 // injection (adrp_set_noise).  Every other handle runs the one-lane kernel (race_kernel.h), which
 // covers all of these with the same arithmetic (test_quad_matches_lane).
 inline bool race_quad_ok(const adrp_t* h) {
-    return h->race_quad && (h->race_cf2x || h->real_size == 4) && !h->inj_force &&
+    // (diagnostics level 2, the firmware moment log, is the one-lane kernel's)
+    return h->race_quad && h->diagnostics < 2 && (h->race_cf2x || h->real_size == 4) && !h->inj_force &&
            !(h->cfg.track.disturbances && (h->S > kRacePreS || !h->race_predraw));
 }
 
@@ -136,6 +139,8 @@ inline RaceArgs<Real> race_args(const adrp_t* h) {
     a.inj_act = h->inj_act;
     a.inj_force = h->inj_force;
     a.mom_hash = h->diagnostics ? h->mom_hash : nullptr;
+    a.mom_log = h->diagnostics >= 2 ? h->mom_log : nullptr;
+    a.mom_log_n = h->diagnostics >= 2 ? h->mom_log_n : nullptr;
     a.img_f = (Real*)h->img_f;
     a.img_i = h->img_i;
     a.img_row = h->img_row;

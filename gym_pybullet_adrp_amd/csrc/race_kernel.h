@@ -99,6 +99,8 @@ struct RaceArgs {
     int64_t env_offset;
     int E;
     uint32_t* mom_hash;  // diagnostics (adrp_set_diagnostics): [E*N] fw_moment_hash of the step, or null
+    int16_t* mom_log;    // diagnostics level 2 (one-lane kernel): [E*N][S][3] int16 moments of every
+    int32_t* mom_log_n;  //   firmware call of the step, in call order; [E*N] the number of calls
     // next-reset images (race_quad.h, race_refill_q4): what the auto-reset at the end of episode
     // img_ep[e] writes for env e, computed ahead of time; null when off
     Real* img_f;         // [RF_N][E*N]
@@ -833,7 +835,7 @@ template <typename Real, bool CMD = false>
 __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lpf, const float sp[3], float xc_x,
                                                   float xc_y, V3<Real> rpy, const Real noise[4],
                                                   CmdState* cs = nullptr, const float* coef = nullptr, size_t EN = 0,
-                                                  size_t slot = 0) {
+                                                  size_t slot = 0, int16_t* mlog = nullptr, int* mcount = nullptr) {
 #pragma clang fp contract(off)   // numpy / C arithmetic of the reference wrapper and firmware
     constexpr bool F32 = sizeof(Real) == 4;   // fp32 kernel: reciprocal multiplies; fp64: numpy's divisions
     const Real fdt = Real(0.002);
@@ -898,6 +900,11 @@ __device__ __forceinline__ void mellinger_compute(RDrone<Real>& d, const Lpf& lp
             const float pos[3] = {float(d.pos.x), float(d.pos.y), float(d.pos.z)};
             const float vel[3] = {float(d.vel.x), float(d.vel.y), float(d.vel.z)};
             mellinger_fw<Real, sizeof(Real) == 4, CMD>(d, sp, xc_x, xc_y, gyro, pos, vel, Rm, cs);
+            if (mlog) {   // diagnostics level 2: this call's int16 moments (the oracle can replay them)
+                const int c = *mcount;
+                mlog[3 * c] = int16_t(d.ctl[0]); mlog[3 * c + 1] = int16_t(d.ctl[1]); mlog[3 * c + 2] = int16_t(d.ctl[2]);
+                *mcount = c + 1;
+            }
         }
         d.tick += 1;
         // _compute_pwms (423-442)
@@ -1804,6 +1811,9 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
     }
     const Lpf lpf = {C.lpf[0], C.lpf[1], C.lpf[2], C.lpf[3], C.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
     if constexpr (PRE == 2) __syncthreads();   // the helpers' first half of the draws is in LDS
+    // diagnostics level 2: the step's firmware moments, call by call (adrp_race_moment_log)
+    int16_t* mlog = a.mom_log ? a.mom_log + slot * size_t(3 * H.S) : nullptr;
+    int mcount = 0;
     RACE_MARK(t1);
 #ifdef ADRP_RACE_TIMING
     uint64_t acc_phys = 0;
@@ -1884,11 +1894,13 @@ __global__ void __launch_bounds__(kRaceBlock * (PRE ? 1 + kRaceHelpers : 1)) rac
                     else race_substep_draws(H, a.seed, gid, ep, dn, idx, f3, noise);
                 }
             }
-            mellinger_compute<Real, CMD>(d, lpf, sp, xc_x, xc_y, euler_xyz_fast_u(d.q), noise, &cs, coefp, EN, slot);
+            mellinger_compute<Real, CMD>(d, lpf, sp, xc_x, xc_y, euler_xyz_fast_u(d.q), noise, &cs, coefp, EN, slot,
+                                         mlog, &mcount);
         }
     }
     }
     RACE_MARK(t2);
+    if (mlog) a.mom_log_n[slot] = mcount;
     if constexpr (PRE == 1) __syncthreads();   // the helpers' track copy is in LDS
     const TrackSrc<Real, PRE == 1> T{a.f, EN, slot, trk_lds, tl};
     // ---- _gate_progress (471-506): rays of my current gate vs every drone of the env ----

@@ -299,6 +299,14 @@ int adrp_diagnostic_contact_count(adrp_t* h, int reset);
  * Parity tests use it as the causal witness of an int16 truncation difference.  Copies E * N values
  * of the last step to `out` (host memory); n must be E * N.  Replaces nothing in the reference. */
 int adrp_race_moment_hash(adrp_t* h, uint32_t* out, size_t n);
+/* Race handles, diagnostics level 2 (adrp_set_diagnostics(h, 2); the step then runs the one-lane
+ * kernel): each env.step also records per drone the int16 (roll, pitch, yaw) of every firmware
+ * controllerMellinger call, in call order (MellingerControl.py:413-415: control_t's moments).
+ * Copies them to `out` [E*N][max_calls][3] and the number of calls to `counts` [E*N] (host memory);
+ * n must be E * N and max_calls the sub-steps per env.step.  The oracle replays them
+ * (oracle/race.c orc_race_set_moment_replay) to show that a drone whose truncation differs agrees
+ * once the same integers are used.  Replaces nothing in the reference. */
+int adrp_race_moment_log(adrp_t* h, int16_t* out, int32_t* counts, size_t n, int max_calls);
 /* Race handles, diagnostics on: auto-resets of the four-lane kernel since the last read, out[0]
  * copied from a next-reset image (computed ahead by the refill launch every ADRP_RESET_IMAGES
  * steps, default 32, 0 = off), out[1] computed inline.  Replaces nothing in the reference. */

@@ -247,6 +247,8 @@ struct orc_handle {
     struct renv_s* re;      /* [E] MultiRace per-env state */
     const double* inj_act;    /* orc_set_noise: [E*N][S][4] action noise, or NULL (Philox) */
     const double* inj_force;  /* [E*N][S][3] disturbance force, or NULL */
+    const int16_t* rp_mom;    /* orc_race_set_moment_replay: [E*N][S][3] int16 firmware moments, or NULL */
+    const int32_t* rp_n;      /* [E*N] calls recorded per drone */
 };
 
 /* MultiRaceAviary (race.c, included at the end of this file) */

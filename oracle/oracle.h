@@ -46,6 +46,8 @@ int orc_race_command(orc_t* o, const int32_t* cmd, const double* args);
    and the disturbance force [E*N][S][3] of sub-step s of drone slot e*N+n from these host arrays
    (kept by pointer) instead of the Philox draws; NULL, NULL returns to Philox */
 int orc_set_noise(orc_t* o, const double* act_noise, const double* force);
+/* firmware int16 moments replayed from the kernel's log ([E*N][S][3] + counts; NULL, NULL: off) */
+int orc_race_set_moment_replay(orc_t* o, const int16_t* mom, const int32_t* counts);
 int orc_race_moment_margin(const orc_t* o, float* out);
 int orc_race_moment_hash(const orc_t* o, uint32_t* out);   /* fw_moment_hash of the last step, per drone */
 int orc_normal_pair(uint32_t x0, uint32_t x1, float* z);

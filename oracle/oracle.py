@@ -76,6 +76,7 @@ def _load():
     lib.orc_race_reward.restype = D
     lib.orc_race_command.argtypes = [P, P, P]
     lib.orc_set_noise.argtypes = [P, P, P]
+    lib.orc_race_set_moment_replay.argtypes = [P, P, P]
     lib.orc_race_moment_margin.argtypes = [P, P]
     lib.orc_race_moment_hash.argtypes = [P, P]
     lib.orc_normal_pair.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P]
@@ -113,6 +114,7 @@ class Oracle:
             raise ValueError(lib().orc_last_error().decode())
         self.h = h
         self.E, self.N = cfg.num_envs, cfg.num_drones
+        self.S = cfg.pyb_freq // cfg.ctrl_freq     # sub-steps per env.step
         self.D = lib().orc_obs_dim(h)
         self.A = lib().orc_act_dim(h)
         nf, ni = ctypes.c_int(), ctypes.c_int()
@@ -160,6 +162,18 @@ class Oracle:
             return
         self._noise = (np.ascontiguousarray(act_noise, np.float64), np.ascontiguousarray(force, np.float64))
         assert lib().orc_set_noise(self.h, _ptr(self._noise[0]), _ptr(self._noise[1])) == 0
+
+    def set_moment_replay(self, moments=None, counts=None):
+        """diagnostics (orc_race_set_moment_replay): the next steps use these int16 firmware moments
+        ([E*N][S][3], call order, counts [E*N]; the kernel's Handle.moment_log()) instead of their own
+        truncation; None, None turns it off"""
+        if moments is None:
+            self._replay = None
+            assert lib().orc_race_set_moment_replay(self.h, None, None) == 0
+            return
+        self._replay = (np.ascontiguousarray(moments, np.int16), np.ascontiguousarray(counts, np.int32))
+        assert self._replay[0].shape == (self.E * self.N, self.S, 3)
+        assert lib().orc_race_set_moment_replay(self.h, _ptr(self._replay[0]), _ptr(self._replay[1])) == 0
 
     def command(self, cmd, args):
         """One high-level command per drone: cmd int32 [E, N], args float64 [E, N, 14]."""

@@ -76,6 +76,10 @@ typedef struct rdrone_s {
                                         truncation changes (a nonzero integer) */
     uint32_t mom_hash;               /* diagnostic, not state: fw_moment_hash over this env.step's firmware
                                         calls (the kernel's adrp_race_moment_hash) */
+    const int16_t* rp_mom;           /* diagnostic, not state: the kernel's int16 moments of this env.step's
+                                        firmware calls to use instead of this restatement's truncation
+                                        (orc_race_set_moment_replay), or NULL */
+    int rp_n, rp_call;               /* calls recorded, calls made so far this env.step */
     /* race progress */
     int gate, elim, fin;
     /* command state (adrp.h ADRP_CMD_NF / ADRP_CMD_NI order): setpoint_t fields the controller
@@ -241,10 +245,17 @@ static void mellinger_fw(rdrone_t* d, const float gyro[3], const float st_pos[3]
         d->ctl[0] = (float)(int16_t)mc[0];
         d->ctl[1] = (float)(int16_t)mc[1];
         d->ctl[2] = (float)(int16_t)mc[2];
+        if (d->rp_mom && d->rp_call < d->rp_n) {   /* replay: the kernel's integers for this call */
+            const int16_t* m = d->rp_mom + 3 * d->rp_call;
+            d->ctl[0] = (float)m[0];
+            d->ctl[1] = (float)m[1];
+            d->ctl[2] = (float)m[2];
+        }
     } else {
         d->ctl[0] = d->ctl[1] = d->ctl[2] = 0;
         mellinger_reset(d);
     }
+    d->rp_call += 1;
     d->mom_hash = fw_moment_hash(d->mom_hash, d->ctl[0], d->ctl[1], d->ctl[2]);
 }
 
@@ -1132,7 +1143,14 @@ static void race_step_env(orc_t* o, int e, const float* act, float* obs_env, flo
     body_t* bs = &o->b[(size_t)e * N];
     rdrone_t* ds = &o->rd[(size_t)e * N];
     int touched = 0;
-    for (int i = 0; i < N; ++i) { ds[i].mom_margin = INFINITY; ds[i].mom_hash = MOM_HASH_SEED; }
+    for (int i = 0; i < N; ++i) {
+        ds[i].mom_margin = INFINITY;
+        ds[i].mom_hash = MOM_HASH_SEED;
+        const size_t slot = (size_t)e * N + i;
+        ds[i].rp_mom = o->rp_mom ? o->rp_mom + slot * (size_t)o->S * 3 : NULL;
+        ds[i].rp_n = o->rp_mom ? o->rp_n[slot] : 0;
+        ds[i].rp_call = 0;
+    }
     /* the command message per drone (190-210): FULLSTATE (act[:3], 0, 0, act[3], 0, step_counter)
        from an ndarray action (act = NULL: the commands adrp_race_command / orc_race_command sent);
        eliminated drones get STOP [step_counter] */
@@ -1333,6 +1351,17 @@ int orc_race_moment_margin(const orc_t* o, float* out) {
 int orc_race_moment_hash(const orc_t* o, uint32_t* out) {
     if (!o || !o->rd) return -1;
     for (size_t k = 0; k < (size_t)o->E * o->N; ++k) out[k] = o->rd[k].mom_hash;
+    return 0;
+}
+
+/* diagnostics: the next steps take the firmware's int16 moments from `mom` ([E*N][S][3], call order,
+   counts[E*N] calls per drone; the kernel's adrp_race_moment_log) instead of truncating their own;
+   NULL turns it off.  The arrays are the caller's and must stay alive while it is on. */
+int orc_race_set_moment_replay(orc_t* o, const int16_t* mom, const int32_t* counts) {
+    if (o->cfg.task != ADRP_TASK_RACE) return fail("moment replay: MultiRaceAviary only");
+    if ((mom == NULL) != (counts == NULL)) return fail("moment replay: both arrays or neither");
+    o->rp_mom = mom;
+    o->rp_n = counts;
     return 0;
 }
 

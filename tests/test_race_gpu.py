@@ -745,3 +745,124 @@ def test_support_bounds_bit_identical(monkeypatch, variant, level, N, physics, m
     gates = outs[0][..., [k * env.h.D + 48 for k in range(N)]]
     assert gates.max() >= 1, "the actor passed no gate: the test would not reach the gate parts"
     assert torch.equal(outs[0], outs[1])
+
+
+def _replay_errors(env, orc, f0, i0, act, floors=None):
+    """re-run the oracle's step from (f0, i0) with the kernel's int16 firmware moments of the same
+    step (diagnostics level 2: Handle.moment_log -> orc_race_set_moment_replay); returns the per-drone
+    max relative error over the field groups, the flag agreement and the number of drones whose own
+    truncation had differed"""
+    differ = env.h.moment_hash() != orc.moment_hash()
+    moms, cnt = env.h.moment_log()
+    orc.set_state(f0, i0)
+    orc.set_moment_replay(moms, cnt)
+    orc.step(act)
+    orc.set_moment_replay()
+    # with the kernel's integers the restatement's moment sequences are the kernel's, call for call
+    np.testing.assert_array_equal(env.h.moment_hash(), orc.moment_hash())
+    err = np.max(np.stack(list(state_errors(env, orc, floors).values())), axis=0)
+    _, io = orc.get_state()
+    _, inames = orc.field_names()
+    flags_same = env.get_state()[1].cpu().numpy()[inames.index("flags")] == io[inames.index("flags")]
+    return err, flags_same, int(differ.sum())
+
+
+@pytest.mark.parametrize("level,N,physics,mode,reward", CASES)
+def test_fp64_closed_loop_replay(level, N, physics, mode, reward):
+    """VERDICT r5 item 6, the fp64 closed loop with no escape hatch: teacher-forced env.steps as in
+    test_teacher_forced_step, where the kernel also logs the int16 (roll, pitch, yaw) of every
+    firmware call (diagnostics level 2, the one-lane kernel, which test_quad_matches_lane ties to the
+    four-lane one); the oracle re-runs each step from the same state with those integers
+    (MellingerControl.py:413-415 is where control_t's int16 moments leave the firmware).  EVERY drone
+    (same elimination flags) is then within FP64_BAR = 1e-6, and the replayed moment hashes equal the
+    kernel's.  Prints how many drone-steps needed the replay (their own truncation differed)."""
+    E = 64
+    rng = np.random.default_rng(3)
+    env, orc = pair(level, N, physics, mode, reward, E, precision="fp64")
+    env.h.set_diagnostics(2)
+    assert "Q4" not in env.kernel_name   # the one-lane kernel (it logs the moments)
+    env.reset()
+    obs0 = orc.reset()
+    act = targets(rng, obs0, E, N)
+    for _ in range(20):                  # take-off on the oracle
+        orc.step(act)
+    replayed = drones = 0
+    worst = 0.0
+    for k in range(6):
+        sync(env, orc)
+        f0, i0 = orc.get_state()
+        if k == 3:
+            act = targets(rng, obs0, E, N)
+        orc.step(act)
+        env.step(torch.from_numpy(act).to(env.device))
+        err, flags_same, n = _replay_errors(env, orc, f0, i0, act)
+        bad = np.flatnonzero((err > FP64_BAR) & flags_same)
+        assert len(bad) == 0, f"step {k}: {len(bad)} drones over {FP64_BAR:g} with the kernel's moments: slots {bad[:8]}, errors {err[bad[:8]]}"
+        replayed += n
+        drones += err.size
+        worst = max(worst, float(err[flags_same].max(initial=0)))
+    print(f"{level} {physics.name}: {drones} drone-steps, {replayed} with a different own truncation, "
+          f"max error with the kernel's moments {worst:.2e}")
+
+
+@pytest.mark.parametrize("E,N,level,physics,mode", [(2048, 2, "level0", Physics.PYB, RaceMode.COMPARE),
+                                                    (4096, 4, "level3", Physics.PYB_DW, RaceMode.COMPETE),
+                                                    (4096, 4, "level3", Physics.PYB_GND_DRAG_DW, RaceMode.COMPETE)])
+def test_full_size_subset_replay_fp64(E, N, level, physics, mode):
+    """BASELINE configs 3 / 4 at full size in float64 with the firmware moment log (diagnostics level
+    2): after 0.8 s of flight, 48 random envs are teacher-forced one env.step against single-env
+    oracles that replay the kernel's int16 moments: every drone (same flags) within 1e-6 (omega
+    floor 0.1 rad/s as in test_full_size_subset_vs_oracle)."""
+    rng = np.random.default_rng(17)
+    env = MultiRaceAviary(level, num_drones=N, physics=physics, racemode=mode, num_envs=E, seed=7, autoreset=False,
+                          precision="fp64")
+    env.h.set_diagnostics(2)
+    obs, _ = env.reset()
+    act = targets(rng, obs.cpu().numpy(), E, N)
+    at = torch.from_numpy(act).to(env.device)
+    for _ in range(20):
+        env.step(at)
+    f, i = env.get_state()
+    f, i = f.double().cpu().numpy(), i.cpu().numpy()
+    sub = np.sort(rng.choice(E, 48, replace=False))
+    env.step(at)
+    fg, ig = env.get_state()
+    fg, ig = fg.double().cpu().numpy(), ig.cpu().numpy()
+    moms, cnt = env.h.moment_log()
+    hash_g = env.h.moment_hash()
+    floors = dict(FLOORS, omega=0.1)
+    replayed = 0
+    worst = 0.0
+    for e in sub:
+        c = env.cfg.copy()
+        c.num_envs, c.env_offset = 1, int(e)
+        o = O.Oracle(c)
+        o.reset()
+        sl = slice(e * N, (e + 1) * N)
+        o.set_state(np.ascontiguousarray(f[:, sl]), np.ascontiguousarray(i[:, sl]))
+        o.set_moment_replay(moms[sl], cnt[sl])
+        o.step(act[e:e + 1])
+        np.testing.assert_array_equal(hash_g[sl], o.moment_hash())
+        fo, io = o.get_state()
+        names, inames = o.field_names()
+        idx = {n: k for k, n in enumerate(names)}
+        kf = inames.index("flags")
+        flags_same = ig[kf, sl] == io[kf]
+        errs = []
+        for g, fields in GROUPS.items():
+            rows = [idx[n] for n in fields]
+            errs.append(np.linalg.norm(fg[rows, sl] - fo[rows], axis=0) /
+                        np.maximum(np.linalg.norm(fo[rows], axis=0), floors[g]))
+        err = np.max(np.stack(errs), axis=0)
+        bad = np.flatnonzero((err > FP64_BAR) & flags_same)
+        assert len(bad) == 0, f"env {e}: drones {bad} over {FP64_BAR:g} with the kernel's moments: {err[bad]}"
+        worst = max(worst, float(err[flags_same].max(initial=0)))
+        # (how many of these drones' own truncation would have differed: run without the replay)
+        o2 = O.Oracle(c)
+        o2.reset()
+        o2.set_state(np.ascontiguousarray(f[:, sl]), np.ascontiguousarray(i[:, sl]))
+        o2.step(act[e:e + 1])
+        replayed += int((o2.moment_hash() != hash_g[sl]).sum())
+    print(f"{level} {physics.name} fp64 full size: {48 * N} drones, {replayed} with a different own truncation, "
+          f"max error with the kernel's moments {worst:.2e}")
+    env.close()
