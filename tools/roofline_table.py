@@ -1,6 +1,7 @@
 """Fold a `tools/gpu.sh prof TAG` run into per-grid rocprof statistics and one roofline table.
 
-usage: python tools/roofline_table.py gpurun_out/TAG ROUND   (e.g. gpurun_out/r6p r6)
+usage: python tools/roofline_table.py gpurun_out/TAG ROUND [BENCH_JSON ...]
+       (e.g. gpurun_out/r6p r6 profiles/r6_bench.json profiles/r6_bench_k20.json)
 
 For every workload directory prof_<cfg>/ of the run (rocprofv3 --kernel-trace of `bench.py
 --graph-only ...`, whose JSON line is in prof_<cfg>.log):
@@ -12,7 +13,9 @@ For every workload directory prof_<cfg>/ of the run (rocprofv3 --kernel-trace of
     from the bench record, the rocprof mean / median at the benched grid, the frac recomputed from
     them, the bench line's own frac (HIP events around the graph-replayed timed region / K) and the
     ratio of the two, and the PMC counter traffic (profiles/pmc_traffic.json); for the hover line
-    the sweep rows with their own rocprof means and fractions.
+    the sweep rows with their own rocprof means and fractions;
+  - for every BENCH_JSON given (full bench lines, not under the profiler): each workload's `frac`
+    from that line's summary next to the rocprof-recomputed one.
 """
 import csv
 import json
@@ -51,7 +54,12 @@ def short(name):
     return s.replace("void adrp::", "").replace("adrp::", "")
 
 
-def main(run_dir, rnd):
+SUMMARY_KEY = {"c2_fp64": "value", "c2_fp32": "config2_f32", "c3_fp64": "config3", "c3_fp32": "config3_f32",
+               "c3p_fp64": "config3_policy", "c3p_fp32": "config3_policy_f32", "c4_fp64": "config5",
+               "c4_fp32": "config5_f32"}
+
+
+def main(run_dir, rnd, benches=()):
     pmc = {}
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(p):
@@ -127,6 +135,19 @@ def main(run_dir, rnd):
                             w.writerow(r)
             ent["sweep"] = srows
         table["workloads"][cfg] = ent
+    for b in benches:
+        line = bench_line(b)
+        if line is None or "summary" not in line:
+            continue
+        name = os.path.relpath(b, ROOT)
+        table.setdefault("bench_records", {})[name] = {
+            "cmd_form": f"K = {line['steps']}, W = {line['warmup']}", "value": line["value"]}
+        for cfg, ent in table["workloads"].items():
+            rec = line["summary"].get(SUMMARY_KEY.get(cfg, ""), {})
+            if "frac" in rec and rec["frac"] and ent.get("frac_rocprof"):
+                ent.setdefault("bench_lines", {})[name] = {
+                    "kernel_us": rec.get("k_us"), "frac": rec["frac"],
+                    "frac_over_rocprof": rec["frac"] / ent["frac_rocprof"]}
     out = os.path.join(ROOT, "profiles", f"{rnd}_roofline.json")
     with open(out, "w") as fh:
         json.dump(table, fh, indent=1)
@@ -134,6 +155,8 @@ def main(run_dir, rnd):
         print(f"{cfg:10s} {e['kernel'][:60]:60s} E={e['envs']:6d} n={e['launches']:5d} rocprof {e['rocprof_mean_us']:7.2f} us "
               f"bench {e['bench_kernel_us']:7.2f} us frac_rocprof {e.get('frac_rocprof') or 0:.4f} "
               f"frac_bench {e.get('frac_bench') or 0:.4f}")
+        for bn, bl in e.get("bench_lines", {}).items():
+            print(f"{'':10s} {bn}: kernel {bl['kernel_us']} us frac {bl['frac']:.4f} ({bl['frac_over_rocprof']:.3f} x rocprof)")
         for s in e.get("sweep", []):
             print(f"{'':10s} sweep E={s['envs']:8d} rocprof {s['rocprof_mean_us']:8.2f} us frac {s['frac_rocprof']:.3f} "
                   f"(bench {s['frac_bench']:.3f})")
@@ -141,4 +164,4 @@ def main(run_dir, rnd):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3:])
