@@ -896,12 +896,21 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     float xc_x, xc_y;
     {
 #pragma clang fp contract(off)
-        Real qs, qc;
-        sincos_(Real(CG.obs_wrapper ? 0.0f : av.w) * Real(0.5), &qs, &qc);   // DroneObservationWrapper: yaw 0
-        const float qz = float(qs), qw = float(qc);
-        const float yaw_deg = degf_(atan2f(2.0f * (qw * qz + 0.0f * 0.0f), 1 - 2 * (0.0f * 0.0f + qz * qz)));
-        xc_x = cosf(radf_(yaw_deg));
-        xc_y = sinf(radf_(yaw_deg));
+        const float yaw = CG.obs_wrapper ? 0.0f : av.w;   // DroneObservationWrapper: yaw 0
+        if (__builtin_expect(__all(yaw == 0.0f), 1)) {
+            // yaw +-0 (the wrapper, or a FULLSTATE target without yaw, in every lane of the wave):
+            // sincos(+-0) = (+-0, 1), 2 (1 (+-0) + 0 0) = +0, atan2f(+0, 1) = +0, (cos, sin)(+0) = (1, +0):
+            // the general form's bits without its four libm calls
+            xc_x = 1.0f;
+            xc_y = 0.0f;
+        } else {
+            Real qs, qc;
+            sincos_(Real(yaw) * Real(0.5), &qs, &qc);
+            const float qz = float(qs), qw = float(qc);
+            const float yaw_deg = degf_(atan2f(2.0f * (qw * qz + 0.0f * 0.0f), 1 - 2 * (0.0f * 0.0f + qz * qz)));
+            xc_x = cosf(radf_(yaw_deg));
+            xc_y = sinf(radf_(yaw_deg));
+        }
     }
     const Lpf lpf = {CG.lpf[0], CG.lpf[1], CG.lpf[2], CG.lpf[3], CG.lpf[4]};   // lpf2pInit(gyrolpf, 500, 30), host
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
