@@ -643,10 +643,13 @@ def test_full_size_subset_vs_oracle(E, N, level, physics, mode, precision):
 @pytest.mark.parametrize("level,N,physics,mode", [("level0", 2, Physics.PYB, RaceMode.COMPARE),
                                                   ("level3", 4, Physics.PYB_DW, RaceMode.COMPETE),
                                                   ("level2", 3, Physics.PYB_GND_DRAG_DW, RaceMode.COMPETE)])
-def test_quad_matches_lane(monkeypatch, level, N, physics, mode, precision):
+@pytest.mark.parametrize("yaw", [False, True])
+def test_quad_matches_lane(monkeypatch, level, N, physics, mode, precision, yaw):
     """the race step in its two layouts, four lanes per drone (default, race_quad.h) and one
     (ADRP_RACE_QUAD=0), teacher-forced from the same states, in both precisions: the per-element
-    arithmetic is the same, so one env.step agrees to rounding and every discrete output is identical"""
+    arithmetic is the same, so one env.step agrees to rounding and every discrete output is identical.
+    yaw: FULLSTATE yaw targets in every other env (waves mixing zero and nonzero yaw: the quad kernel's
+    yaw-0 heading shortcut is wave-uniform, the general heading runs here)"""
     E = 256
     rng = np.random.default_rng(23)
     orc = None
@@ -664,6 +667,8 @@ def test_quad_matches_lane(monkeypatch, level, N, physics, mode, precision):
                 orc.step(act)
             f, i = orc.get_state()
             f = f.astype(np.float32) if precision == "fp32" else f
+            if yaw:
+                act[1::2, :, 3] = rng.uniform(-0.5, 0.5, act[1::2, :, 3].shape).astype(np.float32)
         env.reset()
         env.set_state(torch.from_numpy(f), torch.from_numpy(i))
         o, r, te, tr, _ = env.step(torch.from_numpy(act).to(env.device))
@@ -866,3 +871,32 @@ def test_full_size_subset_replay_fp64(E, N, level, physics, mode):
     print(f"{level} {physics.name} fp64 full size: {48 * N} drones, {replayed} with a different own truncation, "
           f"max error with the kernel's moments {worst:.2e}")
     env.close()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+def test_teacher_forced_step_yaw(precision):
+    """FULLSTATE targets with a yaw (the firmware heading from sincos / atan2f / cosf / sinf,
+    MellingerControl.py:510-543) in every other env, level0 PYB, the default four-lane kernel:
+    teacher-forced env.steps against the oracle at the closed-loop bars, discrete outputs exact"""
+    E, N = 64, 2
+    rng = np.random.default_rng(41)
+    env, orc = pair("level0", N, Physics.PYB, RaceMode.COMPARE, "env", E, precision=precision)
+    assert env.kernel_name.endswith(",Q4>")
+    env.reset()
+    obs0 = orc.reset()
+    act = targets(rng, obs0, E, N)
+    act[1::2, :, 3] = rng.uniform(-0.6, 0.6, act[1::2, :, 3].shape).astype(np.float32)
+    for _ in range(20):
+        orc.step(act)
+    stats = {}
+    for k in range(4):
+        sync(env, orc)
+        obs_o, rew_o, te_o, tr_o, _ = orc.step(act)
+        obs_g, rew_g, te_g, tr_g, _ = env.step(torch.from_numpy(act).to(env.device))
+        check_closed_loop(env, orc, precision, stats)
+        og = obs_g.cpu().numpy()
+        np.testing.assert_allclose(og[..., :3], obs_o[..., :3], rtol=1e-4, atol=1e-4)
+        np.testing.assert_array_equal(og[..., 48], obs_o[..., 48])
+        np.testing.assert_array_equal(te_g.cpu().numpy(), te_o)
+        np.testing.assert_array_equal(tr_g.cpu().numpy(), tr_o)
+    assert_witness_fraction(stats, "yaw: ")
