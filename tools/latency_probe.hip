@@ -6,11 +6,18 @@
 #include <cstdio>
 #include <cstdint>
 
+// one v_mad_u64_u32 (x * 0xD2511F53 + 0, 64-bit result)
+__device__ __forceinline__ uint64_t __builtin_amdgcn_mad_u64_u32_probe(uint32_t x) {
+    uint64_t r;
+    asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(x), "v"(0xD2511F53u) : "vcc");
+    return r;
+}
+
 constexpr int kIters = 256;
 
 #define CHAIN(NAME, T, INIT, STEP)                                                                   \
     __global__ void NAME##_dep(T* out, uint64_t* cyc, T seed) {                                      \
-        T x = seed + T(threadIdx.x) * T(1e-7);                                                       \
+        T x = seed + T(threadIdx.x) * T(1e-7) + T(T(0.5) == T(0) ? threadIdx.x : 0);  /* integer T: lane-varying */                                                       \
         const T a = seed * T(0.999), b = seed * T(1e-3);                                             \
         (void)a; (void)b;                                                                            \
         const uint64_t t0 = __builtin_amdgcn_s_memtime();                                            \
@@ -20,7 +27,7 @@ constexpr int kIters = 256;
         if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;                                             \
     }                                                                                                \
     __global__ void NAME##_ind(T* out, uint64_t* cyc, T seed) {                                      \
-        T x = seed + T(threadIdx.x) * T(1e-7), y = x + T(1e-3), z = x + T(2e-3), w = x + T(3e-3);    \
+        T x = seed + T(threadIdx.x) * T(1e-7) + T(T(0.5) == T(0) ? threadIdx.x : 0), y = x + T(1e-3), z = x + T(2e-3), w = x + T(3e-3);    \
         const T a = seed * T(0.999), b = seed * T(1e-3);                                             \
         (void)a; (void)b;                                                                            \
         const uint64_t t0 = __builtin_amdgcn_s_memtime();                                            \
@@ -45,6 +52,10 @@ constexpr int kIters = 256;
 #define SMOV_STEP(x) do { int lo_, hi_; asm volatile("s_mov_b32 %0, 0x3ff00001" : "=s"(lo_)); \
     asm volatile("s_mov_b32 %0, 0x3ff00000" : "=s"(hi_)); x = __builtin_fma(x, __hiloint2double(hi_, lo_), b); } while (0)
 
+// Philox's 32 x 32 -> 64 products: v_mul_hi_u32 + v_mul_lo_u32, or one v_mad_u64_u32
+#define MULHL_STEP(x) do { const uint32_t h_ = __umulhi(x, 0xD2511F53u), l_ = x * 0xD2511F53u; x = h_ ^ l_ ^ b; } while (0)
+#define MAD64_STEP(x) do { const uint64_t p_ = __builtin_amdgcn_mad_u64_u32_probe(x); x = uint32_t(p_ >> 32) ^ uint32_t(p_) ^ b; } while (0)
+
 CHAIN(fma64, double, 0, FMA_STEP)
 CHAIN(fma32, float, 0, FMAF_STEP)
 CHAIN(mul64, double, 0, MUL_STEP)
@@ -57,6 +68,8 @@ CHAIN(div32, float, 0, DIV32_STEP)
 CHAIN(div64, double, 0, DIV64_STEP)
 CHAIN(cvt64, double, 0, CVT_STEP)
 CHAIN(smov64, double, 0, SMOV_STEP)
+CHAIN(mulhl32, uint32_t, 0, MULHL_STEP)
+CHAIN(mad64u32, uint32_t, 0, MAD64_STEP)
 
 template <typename T>
 static void run(const char* name, void (*dep)(T*, uint64_t*, T), void (*ind)(T*, uint64_t*, T), T seed,
@@ -96,6 +109,8 @@ int main() {
     run<double>("ieee_div_f64", div64_dep, div64_ind, 1.0001);
     run<double>("cvt_f32_f64+mul", cvt64_dep, cvt64_ind, 1.0001);
     run<double>("2x s_mov_b32+v_fma_f64", smov64_dep, smov64_ind, 1.0001);
+    run<uint32_t>("v_mul_hi_u32+v_mul_lo_u32+2xor", mulhl32_dep, mulhl32_ind, 12345u);
+    run<uint32_t>("v_mad_u64_u32+2xor", mad64u32_dep, mad64u32_ind, 12345u);
     // several waves per SIMD: cycles per op of each wave (throughput per SIMD = waves / this)
     run<double>("v_fma_f64", fma64_dep, fma64_ind, 1.0001, 4);
     run<double>("v_fma_f64", fma64_dep, fma64_ind, 1.0001, 8);

@@ -101,7 +101,9 @@ def main(run_dir, rnd, benches=()):
         bpl = rl.get("bytes_per_launch") or (rl.get("hbm") or {}).get("bytes_per_launch")
         ent = {"kernel": short(main_key[0]), "grid": main_key[1], "envs": E, "launches": len(L[main_key]),
                "rocprof_mean_us": mean_us, "rocprof_median_us": float(np.median(L[main_key])) / 1e3,
+               "rocprof_p99_us": float(np.percentile(L[main_key], 99)) / 1e3,
                "rocprof_max_us": float(np.max(L[main_key])) / 1e3,
+               "max_over_mean": float(np.max(L[main_key])) / float(np.mean(L[main_key])),
                "bytes_per_launch": bpl, "bench_kernel_us": rl["kernel_us"],
                "stats_csv": os.path.relpath(out_csv, ROOT)}
         if rl["bound"] == "hbm":
