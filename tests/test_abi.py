@@ -60,6 +60,23 @@ def test_invalid_config_rejected(lib):
     assert lib.adrp_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == abi.ERR_INVALID
 
 
+@pytest.mark.parametrize("task,field,value,msg", [
+    (abi.TASK_HOVER, "num_envs", 0, b"num_envs"), (abi.TASK_HOVER, "num_envs", -4, b"num_envs"),
+    (abi.TASK_HOVER, "precision", 2, b"precision"), (abi.TASK_HOVER, "physics", 9, b"physics"),
+    (abi.TASK_HOVER, "num_drones", 2, b"exactly one drone"), (abi.TASK_RACE, "num_drones", 9, b"num_drones"),
+    (abi.TASK_RACE, "num_drones", 0, b"num_drones")])
+def test_invalid_sizes_rejected_before_device(lib, task, field, value, msg):
+    """empty / negative env counts and out-of-range sizes are refused by the config check, before
+    any device call (so the same error on a GPU box and here)"""
+    from gym_pybullet_adrp_amd import _lib
+    cfg = _lib.default_config(task)
+    setattr(cfg, field, value)
+    h = ctypes.c_void_p()
+    assert lib.adrp_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == abi.ERR_INVALID
+    assert msg in lib.adrp_last_error(None)
+    assert not h.value
+
+
 def test_no_cpu_fallback(lib):
     import torch
     if torch.cuda.is_available():
