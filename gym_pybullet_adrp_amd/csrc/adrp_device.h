@@ -36,9 +36,13 @@ constexpr int kWaveSlots = 16384;
 __device__ unsigned long long g_race_wave[kWaveSlots * 8];
 #define RACE_WAVE(i, dt) do { if (blockIdx.x < kWaveSlots) g_race_wave[blockIdx.x * 8 + (i)] = (unsigned long long)(dt); } while (0)
 #ifdef ADRP_RACE_GJK_STATS
-// GJK queries that reached the iteration cap: the first kGjkDumps of them (two shapes, the cut,
-// the last |v|^2 and v.w), for a CPU replay (tools/gjk_replay.py)
-constexpr int kGjkDumps = 64, kGjkDumpF = 40;
+// GJK queries that ran at least ADRP_GJK_DUMP_MIN_IT iterations (default: the cap): the first
+// kGjkDumps of them (two shapes, the cut, the last |v|^2, the iterations, the decision and the seed),
+// for a CPU replay (tools/gjk_replay.py, tools/gjk_slow.py)
+#ifndef ADRP_GJK_DUMP_MIN_IT
+#define ADRP_GJK_DUMP_MIN_IT 48
+#endif
+constexpr int kGjkDumps = 512, kGjkDumpF = 44;
 __device__ double g_gjk_dump[kGjkDumps * kGjkDumpF];
 __device__ unsigned int g_gjk_dump_n;
 #endif

@@ -35,7 +35,8 @@ __shared__ unsigned int g_gjk_wave_iters;
         atomicAdd(&g_race_phase[9], 1ull); atomicAdd(&g_race_phase[18], (unsigned long long)(n)); \
         atomicMax(&g_race_phase[19], (unsigned long long)(n)); \
         if (cut < Real(1e-3)) { atomicAdd(&g_race_phase[20], 1ull); atomicMax(&g_race_phase[21], (unsigned long long)(n)); } \
-        if ((n) >= 48) atomicAdd(&g_race_phase[22], 1ull); } while (0)
+        if ((n) >= 48) atomicAdd(&g_race_phase[22], 1ull); \
+        if (nout) *nout = (n); } while (0)
 #else
 #define GJK_STAT(n)
 #endif
@@ -316,9 +317,9 @@ __device__ __forceinline__ V3<Real> tri_closest(V3<Real> a, V3<Real> b, V3<Real>
 // closest to it, gjk_seed): near a long part it starts the iteration next to the closest features
 // instead of along the centre difference
 template <typename Real>
-__device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
-                                                bool* undecided = nullptr, const V3<Real>* v0 = nullptr,
-                                                int max_it = 48) {
+__device__ __forceinline__ bool gjk_within_body(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
+                                                bool* undecided, const V3<Real>* v0, int max_it,
+                                                int* nout) {
     // in A's centre frame: support points stay O(shape size), so the fp32 termination test
     // is not swamped by rounding of world coordinates (which stalled convergence)
     Shape<Real> A = A0, B = B0;
@@ -408,8 +409,17 @@ __device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Sha
     }
     GJK_STAT(max_it);
     if (undecided) *undecided = true;
+    return dot(v, v) < cut2;
+}
+
+template <typename Real>
+__device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
+                                                bool* undecided = nullptr, const V3<Real>* v0 = nullptr,
+                                                int max_it = 48) {
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
-    {
+    int n = 0;
+    const bool r = gjk_within_body<Real>(A0, B0, cut, undecided, v0, max_it, &n);
+    if (n >= ADRP_GJK_DUMP_MIN_IT) {   // the query, for a CPU replay (tools/gjk_slow.py)
         const unsigned int k = atomicAdd(&g_gjk_dump_n, 1u);
         if (k < unsigned(kGjkDumps)) {
             double* o = g_gjk_dump + size_t(k) * kGjkDumpF;
@@ -422,11 +432,15 @@ __device__ __forceinline__ bool gjk_within_impl(const Shape<Real>& A0, const Sha
                 p[9] = q.R.a20; p[10] = q.R.a21; p[11] = q.R.a22;
                 p[12] = q.h.x; p[13] = q.h.y; p[14] = q.h.z; p[15] = q.r; p[16] = q.cyl;
             }
-            o[34] = cut; o[35] = dot(v, v); o[36] = double(sizeof(Real));
+            o[34] = cut; o[35] = 0.0; o[36] = double(sizeof(Real)); o[37] = n; o[38] = r ? 1.0 : 0.0;
+            o[39] = v0 ? double(v0->x) : 0.0; o[40] = v0 ? double(v0->y) : 0.0; o[41] = v0 ? double(v0->z) : 0.0;
+            o[42] = v0 ? 1.0 : 0.0; o[43] = double(max_it);
         }
     }
+    return r;
+#else
+    return gjk_within_body<Real>(A0, B0, cut, undecided, v0, max_it, nullptr);
 #endif
-    return dot(v, v) < cut2;
 }
 
 template <typename Real>
@@ -444,7 +458,7 @@ __device__ __forceinline__ Shape<double> shape_f64(const Shape<Real>& s) {
 // "distance(A, B) < cut".  A contact query (cut 1 um) that the fp32 iteration leaves undecided is
 // run again by the float64 GJK on the same float shapes: near contact the float iteration can not
 // resolve |v| against the O(0.1 m) support points and cycles one triangle (|v| 1e-6 .. 4e-4 m where
-// the oracle's distance was 0 .. 2e-4 m; tools/gjk_capped.py, tools/gjk_replay.py), so those
+// the oracle's distance was 0 .. 2e-4 m; tools/gjk_slow.py, tools/gjk_replay.py), so those
 // queries are decided as the oracle decides them.  Decided queries (the lower bound, the enclosed
 // origin, the upper bound, convergence) keep the float answer, and range queries (0.45 m) stay
 // float.
@@ -457,12 +471,24 @@ __device__ __noinline__ bool gjk_within_f64_call(Shape<double> A, Shape<double> 
 #ifndef ADRP_GJK_CAP_F32
 #define ADRP_GJK_CAP_F32 24
 #endif
+#ifndef ADRP_GJK_CONTACT_F64   // 0: the float contact iteration first, float64 only for undecided queries
+#define ADRP_GJK_CONTACT_F64 1
+#endif
 constexpr int kGjkContactCapF32 = ADRP_GJK_CAP_F32;
 template <typename Real>
 __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Real>& B0, Real cut,
                                            const V3<Real>* v0 = nullptr) {
     if constexpr (sizeof(Real) == 4) {
         if (cut < Real(1e-3)) {
+#if ADRP_GJK_CONTACT_F64
+            // contact queries (cut 1 um) run in float64 from the start: near contact the float
+            // iteration stalls (|v| not resolvable against O(0.1 m) support points) and was rerun in
+            // float64 after up to 24 float iterations; the slow actor-driven queries (tools/gjk_slow.py:
+            // 691 of >= 8 iterations in 400 launches) take 8.8 float64 iterations on average, at most 14,
+            // against 10.7 / 31 for the float iteration plus its rerun (CPU replay, tools/gjk_replay.py)
+            const V3<double> v0d = v0 ? v3(double(v0->x), double(v0->y), double(v0->z)) : v3(0.0, 0.0, 0.0);
+            return gjk_within_f64_call(shape_f64(A0), shape_f64(B0), double(cut), v0d, v0 != nullptr);
+#else
             // a float contact query still open after 24 iterations goes to the float64 rerun (which
             // decides as the oracle does) instead of running the float iteration to 48: the actor-driven
             // tail was one such query per few hundred launches (48 fp32 iterations + the rerun)
@@ -471,6 +497,7 @@ __device__ __forceinline__ bool gjk_within(const Shape<Real>& A0, const Shape<Re
             if (__builtin_expect(!undecided, 1)) return r;
             const V3<double> v0d = v0 ? v3(double(v0->x), double(v0->y), double(v0->z)) : v3(0.0, 0.0, 0.0);
             return gjk_within_f64_call(shape_f64(A0), shape_f64(B0), double(cut), v0d, v0 != nullptr);
+#endif
         }
     }
     return gjk_within_impl<Real>(A0, B0, cut, nullptr, v0);

@@ -1,8 +1,8 @@
 """CPU replay of the kernels' gjk_within (csrc/race_kernel.h) in float32 or float64, for the capped
-queries tools/gjk_capped.py dumps: prints the per-iteration |v|, the lower bound v.w / |v| and the
+queries tools/gjk_slow.py dumps: prints the per-iteration |v|, the lower bound v.w / |v| and the
 simplex size, so the cause of a 48-iteration run can be read off.
 
-usage: python tools/gjk_replay.py gpurun_out/gjk_capped_fp32.npz [INDEX] [f32|f64]
+usage: python tools/gjk_replay.py gpurun_out/gjk_slow_level0_2_PYB_fp32_example.npz [INDEX] [f32|f64]
 """
 import sys
 
@@ -49,18 +49,20 @@ def tri_closest(a, b, c):
     return a + (vb * den) * ab + (vc * den) * ac, [a, b, c]
 
 
-def gjk_within(A0, B0, cut, T, trace=False, stall=True):
+def gjk_within(A0, B0, cut, T, trace=False, stall=True, v0=None, max_it=48):
     A, B = dict(A0), dict(B0)
     B["c"] = B0["c"] - A0["c"]
     A["c"] = np.zeros(3, T)
     eps, tol2 = (T(4e-6), T(1e-14)) if T == np.float32 else (T(1e-13), T(1e-26))
     W = []
     v = A["c"] - B["c"]
+    if v0 is not None:
+        v = np.asarray(v0, T)
     cut2 = T(cut) * T(cut)
     if v @ v < 1e-20:
         v = np.array([1, 0, 0], T)
     vv_prev = T(3e38)
-    for it in range(48):
+    for it in range(max_it):
         w = support(A, -v, T) - support(B, v, T)
         vv, vw = v @ v, v @ w
         if stall and vv == vv_prev:
@@ -111,7 +113,7 @@ def gjk_within(A0, B0, cut, T, trace=False, stall=True):
             v, W = bv, bW
         if v @ v < cut2:
             return True, it + 1, "upper"
-    return v @ v < cut2, 48, "cap"
+    return v @ v < cut2, max_it, "cap"
 
 
 if __name__ == "__main__":
@@ -122,6 +124,8 @@ if __name__ == "__main__":
     for i in which:
         r = rec[i]
         A, B = shape(r, 0, T), shape(r, 1, T)
-        res = gjk_within(A, B, r[34], T, trace=len(which) == 1)
+        seeded = len(r) > 42 and r[42] > 0
+        res = gjk_within(A, B, r[34], T, trace=len(which) == 1, v0=r[39:42] if seeded else None,
+                         max_it=int(r[43]) if len(r) > 43 else 48)
         print(i, "cut", r[34], "kinds", A["cyl"], B["cyl"], "A h/r", A["h"], A["r"], "B h/r", B["h"], B["r"],
               "|dc|", np.linalg.norm(B["c"] - A["c"]), "->", res)
