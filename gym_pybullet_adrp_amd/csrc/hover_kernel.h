@@ -99,6 +99,18 @@ struct HoverReset {
 // launch, so it is cold in every cache: keep it to two 64-byte lines)
 constexpr int kStepBlock = 64;   // envs per workgroup: one chain wave (E = 4096 -> 64 CUs)
 constexpr int kResetFields = 16; // pos 3, quat 4, vel 3, w 3, angv 3 of a reset state (HELP)
+// HELP kernels: two more helper waves beside the reset helper compute the obs row's pitch and yaw
+// from the chain's final quaternion while the chain computes the roll (ADRP_HOVER_ANGLE_HELPERS=0:
+// the chain computes all three, one helper wave)
+#ifndef ADRP_HOVER_ANGLE_HELPERS
+#define ADRP_HOVER_ANGLE_HELPERS 1
+#endif
+// (float64 only: in float32 the two extra barriers cost more than the two atan2 they take off the
+// chain, +1.2 % against -1.2 % in float64, A/B round 6)
+template <typename Real>
+constexpr bool angle_helpers() { return ADRP_HOVER_ANGLE_HELPERS != 0 && sizeof(Real) == 8; }
+template <typename Real>
+constexpr int help_waves() { return angle_helpers<Real>() ? 3 : 1; }   // helper waves of a HELP workgroup
 
 template <typename Real>
 struct HoverArgs {
@@ -336,6 +348,29 @@ __device__ __forceinline__ void hover_reset_state(const HoverArgs<Real>& args, c
     for (int i = 0; i < 4; ++i) b.prev_rpm[i] = Real(0);
     sc = 0;
     ep += 1;
+}
+
+// euler_xyz_fast_u's angles one at a time: the same expressions (the same contraction, so the same
+// bits) and the same wave-uniform gimbal-lock branch, for the HELP kernel's angle helpers
+template <typename Real>
+__device__ __forceinline__ Real euler_roll_u(Q4<Real> q) {
+    const Real sarg = Real(-2) * (q.x * q.z - q.w * q.y);
+    if (__builtin_expect(__any(fabs_(sarg) >= Real(0.99999)), 0)) return euler_xyz_fast(q).x;
+    const Real sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
+    return fatan2_(Real(2) * (q.y * q.z + q.w * q.x), squ - sqx - sqy + sqz);
+}
+template <typename Real>
+__device__ __forceinline__ Real euler_pitch_u(Q4<Real> q) {
+    const Real sarg = Real(-2) * (q.x * q.z - q.w * q.y);
+    if (__builtin_expect(__any(fabs_(sarg) >= Real(0.99999)), 0)) return euler_xyz_fast(q).y;
+    return fasin_(sarg);
+}
+template <typename Real>
+__device__ __forceinline__ Real euler_yaw_u(Q4<Real> q) {
+    const Real sarg = Real(-2) * (q.x * q.z - q.w * q.y);
+    if (__builtin_expect(__any(fabs_(sarg) >= Real(0.99999)), 0)) return euler_xyz_fast(q).z;
+    const Real sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
+    return fatan2_(Real(2) * (q.x * q.y + q.w * q.z), squ + sqx - sqy - sqz);
 }
 
 template <typename Real>
@@ -577,7 +612,30 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     __shared__ Real rs_body[HELP ? kResetFields * kStepBlock : 1];
     __shared__ float rs_obs[HELP ? 12 * kStepBlock : 1];
     __shared__ float4 rows[STG ? kStepBlock * kRowF4 : 1];
+    // ANG: the obs row's pitch / yaw are computed by two more helper waves from the chain's final
+    // quaternion (LDS) while the chain computes the roll: the chain's tail holds one of the three
+    // float64 atan2-class evaluations instead of three
+    constexpr bool ANG = HELP && angle_helpers<Real>();
+    __shared__ Real ang_q[ANG ? 4 * kStepBlock : 1];
+    __shared__ Real ang_p[ANG ? kStepBlock : 1];
+    __shared__ float ang_y[ANG ? kStepBlock : 1];
+    // the block's coalesced copy-out dealt over its waves: float4 columns [cb(w), cb(w + 1)) of the
+    // rows; with the angle helpers the chain wave takes 3 of the 18, the helpers 5 each
+    constexpr int kWaves = HELP ? 1 + help_waves<Real>() : 1;
+    constexpr auto cb = [](int w) { return w == 0 ? 0 : (w >= kWaves ? kRowF4 : (kWaves == 2 ? kRowF4 / 2 : 5 * w - 2)); };
     if constexpr (HELP) {
+        if (ANG && threadIdx.x >= 2 * kStepBlock) {   // angle helpers: pitch (wave 2), yaw (wave 3)
+            const int tl = threadIdx.x & (kStepBlock - 1), wv = threadIdx.x / kStepBlock;
+            __syncthreads();   // A: the chain's final quaternion
+            const Q4<Real> q = {ang_q[tl], ang_q[kStepBlock + tl], ang_q[2 * kStepBlock + tl], ang_q[3 * kStepBlock + tl]};
+            if (wv == 2) ang_p[tl] = euler_pitch_u(q);
+            else ang_y[tl] = float(euler_yaw_u(q));
+            __syncthreads();   // C: pitch and yaw
+            __syncthreads();   // B: the final rows
+            float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
+            for (int k = cb(wv); k < cb(wv + 1); ++k) store_out(dst + tl + kStepBlock * k, rows[tl + kStepBlock * k]);
+            return;
+        }
         if (threadIdx.x >= kStepBlock) {
             const int tl = threadIdx.x - kStepBlock;
             const int he = blockIdx.x * kStepBlock + tl;
@@ -630,11 +688,12 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
             }
             reinterpret_cast<float4*>(a.ring)[size_t(head) * E + he] = av;
             __syncthreads();   // A: reset states and ring rows in LDS
+            if constexpr (ANG) __syncthreads();   // C
             __syncthreads();   // B: the chain wave's kinematic parts and reset rows
-            // second half of the block's coalesced copy-out
+            // this wave's part of the block's coalesced copy-out
             float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
 #pragma unroll
-            for (int k = kRowF4 / 2; k < kRowF4; ++k) store_out(dst + tl + kStepBlock * k, rows[tl + kStepBlock * k]);
+            for (int k = cb(1); k < cb(2); ++k) store_out(dst + tl + kStepBlock * k, rows[tl + kStepBlock * k]);
             return;
         }
     }
@@ -755,14 +814,34 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
     const int head1 = head + 1 == BB ? 0 : head + 1;
     // ---- obs / reward / terminated / truncated (HoverAviary.py:68-117) ----
     float o12[12];
-    const V3<Real> rpy = hover_obs12(C, b, o12);
+    V3<Real> rpy;
+    if constexpr (ANG) {
+        const int tl = threadIdx.x;
+        ang_q[tl] = b.q.x; ang_q[kStepBlock + tl] = b.q.y; ang_q[2 * kStepBlock + tl] = b.q.z;
+        ang_q[3 * kStepBlock + tl] = b.q.w;
+        __syncthreads();   // A: the quaternion out; the reset helper's states and ring rows in
+        rpy.x = euler_roll_u(b.q);
+        const V3<Real> w = C.physics == ADRP_PHYS_DYN ? b.angv : b.w;   // hover_obs12's row, pitch / yaw below
+        o12[0] = float(b.pos.x); o12[1] = float(b.pos.y); o12[2] = float(b.pos.z); o12[3] = float(rpy.x);
+        o12[6] = float(b.vel.x); o12[7] = float(b.vel.y); o12[8] = float(b.vel.z);
+        o12[9] = float(w.x);     o12[10] = float(w.y);    o12[11] = float(w.z);
+    } else {
+        rpy = hover_obs12(C, b, o12);
+    }
     const Real dx = C.target[0] - b.pos.x, dy = C.target[1] - b.pos.y, dz = C.target[2] - b.pos.z;
     const Real d2 = dx * dx + dy * dy + dz * dz;
     const Real r = Real(2) - d2 * d2;
     a.rew[e] = float(r > Real(0) ? r : Real(0));
     const bool te = d2 < Real(1e-8);   // |target - pos| < 1e-4
-    const bool tr = fabs_(b.pos.x) > Real(1.5) || fabs_(b.pos.y) > Real(1.5) || b.pos.z > Real(2.0) ||
-                    fabs_(rpy.x) > Real(0.4) || fabs_(rpy.y) > Real(0.4) || sc >= C.trunc_steps;
+    bool tr = fabs_(b.pos.x) > Real(1.5) || fabs_(b.pos.y) > Real(1.5) || b.pos.z > Real(2.0) ||
+              fabs_(rpy.x) > Real(0.4) || sc >= C.trunc_steps;
+    if constexpr (ANG) {
+        __syncthreads();   // C: the helpers' pitch and yaw
+        rpy.y = ang_p[threadIdx.x];
+        o12[4] = float(rpy.y);
+        o12[5] = ang_y[threadIdx.x];
+    }
+    tr = tr || fabs_(rpy.y) > Real(0.4);
     a.term[e] = te;
     a.trunc[e] = tr;
     sc += C.S;
@@ -803,7 +882,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         my[0] = make_float4(o12[0], o12[1], o12[2], o12[3]);
         my[1] = make_float4(o12[4], o12[5], o12[6], o12[7]);
         my[2] = make_float4(o12[8], o12[9], o12[10], o12[11]);
-        if constexpr (HELP) __syncthreads();   // A: the helper wave's reset states
+        if constexpr (HELP && !ANG) __syncthreads();   // A: the helper wave's reset states
         if (done) {
             if (a.tobs) {   // terminal obs = the row just staged (this lane's own LDS row)
                 float4 t[kRowF4];
@@ -847,7 +926,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         a.ist[HI_RING_HEAD * E + e] = head1;
         __syncthreads();
         float4* dst = reinterpret_cast<float4*>(a.obs) + size_t(blockIdx.x) * kStepBlock * kRowF4;
-        constexpr int KC = HELP ? kRowF4 / 2 : kRowF4;   // HELP: the helper copies the other half
+        constexpr int KC = cb(1);   // HELP: the helper waves copy the other columns
 #pragma unroll
         for (int k = 0; k < KC; ++k) store_out(dst + threadIdx.x + kStepBlock * k, rows[threadIdx.x + kStepBlock * k]);
     } else {

@@ -25,7 +25,7 @@ static void launch(K kernel, dim3 grid, dim3 blk, hipStream_t s, const HoverArgs
 
 template <typename Real, int A, int B, bool DEF, bool STG = false, int CTL = 0, bool HELP = false>
 static void launch_step_ph(const HoverArgs<Real>& a, int physics, dim3 grid, hipStream_t s, adrp_t* h) {
-    const dim3 blk(HELP ? 2 * kBlock : kBlock);   // HELP: + the reset helper wave
+    const dim3 blk(HELP ? (1 + help_waves<Real>()) * kBlock : kBlock);   // HELP: + the reset helper (and angle helper) waves
     switch (physics) {
         case ADRP_PHYS_PYB: launch(hover_step_kernel<Real, ADRP_PHYS_PYB, A, B, DEF, STG, CTL, HELP>, grid, blk, s, a, h); break;
         case ADRP_PHYS_DYN: launch(hover_step_kernel<Real, ADRP_PHYS_DYN, A, B, DEF, STG, CTL, HELP>, grid, blk, s, a, h); break;
