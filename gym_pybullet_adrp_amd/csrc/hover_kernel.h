@@ -102,6 +102,9 @@ constexpr int kResetFields = 16; // pos 3, quat 4, vel 3, w 3, angv 3 of a reset
 // HELP kernels: two more helper waves beside the reset helper compute the obs row's pitch and yaw
 // from the chain's final quaternion while the chain computes the roll (ADRP_HOVER_ANGLE_HELPERS=0:
 // the chain computes all three, one helper wave)
+#ifndef ADRP_PERSIST_SPLIT   // 0: the E = 1 persistent step computes its three obs angles on one lane
+#define ADRP_PERSIST_SPLIT 1
+#endif
 #ifndef ADRP_HOVER_ANGLE_HELPERS
 #define ADRP_HOVER_ANGLE_HELPERS 1
 #endif
@@ -371,6 +374,46 @@ __device__ __forceinline__ Real euler_yaw_u(Q4<Real> q) {
     if (__builtin_expect(__any(fabs_(sarg) >= Real(0.99999)), 0)) return euler_xyz_fast(q).z;
     const Real sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
     return fatan2_(Real(2) * (q.x * q.y + q.w * q.z), squ + sqx - sqy - sqz);
+}
+
+// E = 1 persistent step (SPLIT): lane L evaluates Euler angle min(L, 2) of the (duplicated) env with
+// ONE atan2 -- roll (y0, x0), pitch (sarg, sqrt((1 - sarg)(1 + sarg)), the atan2 form of fasin_),
+// yaw (y2, x2) -- and the three come back by readlane: the same expressions as euler_xyz_fast_u, so
+// the same bits, for one atan2 on the chain instead of three
+template <typename Real>
+__device__ __forceinline__ Real euler_axis_u(Q4<Real> q, int ax) {
+    const Real sarg = Real(-2) * (q.x * q.z - q.w * q.y);
+    if (__builtin_expect(__any(fabs_(sarg) >= Real(0.99999)), 0)) {
+        const V3<Real> r = euler_xyz_fast(q);
+        return ax == 0 ? r.x : (ax == 1 ? r.y : r.z);
+    }
+    const Real sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
+    const Real y0 = Real(2) * (q.y * q.z + q.w * q.x), x0 = squ - sqx - sqy + sqz;
+    const Real y2 = Real(2) * (q.x * q.y + q.w * q.z), x2 = squ + sqx - sqy - sqz;
+    Real x1;
+    if constexpr (sizeof(Real) == 8) x1 = f64::sqrt((1.0 - sarg) * (1.0 + sarg));
+    else x1 = __builtin_amdgcn_sqrtf((1.0f - sarg) * (1.0f + sarg));
+    const Real yy = ax == 0 ? y0 : (ax == 1 ? sarg : y2), xx = ax == 0 ? x0 : (ax == 1 ? x1 : x2);
+    return fatan2_(yy, xx);
+}
+__device__ __forceinline__ float readlane_r(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double readlane_r(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+// hover_obs12 with the angles dealt over lanes 0..2 (every lane holds the same env)
+template <typename Real>
+__device__ __forceinline__ V3<Real> hover_obs12_split(const HoverConst<Real>& a, const Body<Real>& b, float o[12]) {
+    const int l = int(threadIdx.x) & 63;
+    const Real ang = euler_axis_u(b.q, l < 2 ? l : 2);
+    const V3<Real> rpy = v3(readlane_r(ang, 0), readlane_r(ang, 1), readlane_r(ang, 2));
+    const V3<Real> w = a.physics == ADRP_PHYS_DYN ? b.angv : b.w;
+    o[0] = float(b.pos.x); o[1] = float(b.pos.y); o[2] = float(b.pos.z);
+    o[3] = float(rpy.x);   o[4] = float(rpy.y);   o[5] = float(rpy.z);
+    o[6] = float(b.vel.x); o[7] = float(b.vel.y); o[8] = float(b.vel.z);
+    o[9] = float(w.x);     o[10] = float(w.y);    o[11] = float(w.z);
+    return rpy;
 }
 
 template <typename Real>
@@ -697,8 +740,12 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
             return;
         }
     }
-    const int e = blockIdx.x * kStepBlock + threadIdx.x;
     const int E = a.E;
+    // SPLIT (line-mode persistent step of ONE env, BASELINE config 1): every lane of the wave runs env 0
+    // (the same inputs, the same code: the duplicate stores write the same values) so that three lanes
+    // can take the three obs angles at once; contacts are counted by lane 0 alone
+    const bool split = ADRP_PERSIST_SPLIT && SYS == 2 && E == 1;
+    const int e = split ? 0 : int(blockIdx.x) * kStepBlock + int(threadIdx.x);
     const int D = B > 0 ? 12 + B * A : a.D;
     if (e >= E) return;
     RACE_MARK(t0);
@@ -801,7 +848,7 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         }
     }
     RACE_MARK(t2);
-    if (touched && a.contact_count) atomicAdd(a.contact_count, 1);
+    if (touched && a.contact_count && (!split || threadIdx.x == 0)) atomicAdd(a.contact_count, 1);
     // ---- action ring: append this action at `head` (deque.append, BaseRLAviary.py:187) ----
     if constexpr (HELP) {
         // the helper wave appends
@@ -825,6 +872,8 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         o12[0] = float(b.pos.x); o12[1] = float(b.pos.y); o12[2] = float(b.pos.z); o12[3] = float(rpy.x);
         o12[6] = float(b.vel.x); o12[7] = float(b.vel.y); o12[8] = float(b.vel.z);
         o12[9] = float(w.x);     o12[10] = float(w.y);    o12[11] = float(w.z);
+    } else if (split) {
+        rpy = hover_obs12_split(C, b, o12);
     } else {
         rpy = hover_obs12(C, b, o12);
     }
@@ -942,7 +991,8 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
                 else write_row_generic<A>(a.tobs + size_t(e) * D, o12, a.ring, a.B, E, e, head1, act, true);
             }
             hover_reset_state(a, C, e, b, sc, ep);
-            hover_obs12(C, b, o12);
+            if (split) hover_obs12_split(C, b, o12);
+            else hover_obs12(C, b, o12);
         }
         RACE_SET(t4);
         if constexpr (B > 0) write_row<A, B>(a.obs + size_t(e) * D, o12, ring, head1);

@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(kStepBlock) hover_persist_kernel(HoverArgs<Rea
             }
             if (r == kPersistStop) break;
             float pre[A];
-            const int src = lane * A <= kPersistLineWords - 1 - A ? lane * A : 0;   // lanes >= E leave the body at once
+            const int src = (lane < a.E ? lane : a.E - 1) * A;   // lanes >= E: env E - 1's (E = 1: every lane runs env 0)
 #pragma unroll
             for (int j = 0; j < A; ++j) pre[j] = __uint_as_float(__shfl(v, src + j));
             if constexpr (DEF) {
