@@ -102,7 +102,7 @@ constexpr int kResetFields = 16; // pos 3, quat 4, vel 3, w 3, angv 3 of a reset
 // HELP kernels: two more helper waves beside the reset helper compute the obs row's pitch and yaw
 // from the chain's final quaternion while the chain computes the roll (ADRP_HOVER_ANGLE_HELPERS=0:
 // the chain computes all three, one helper wave)
-#ifndef ADRP_PERSIST_SPLIT   // 0: the E = 1 persistent step computes its three obs angles on one lane
+#ifndef ADRP_PERSIST_SPLIT   // 0: a step of one env (launched or persistent) computes its three obs angles on one lane
 #define ADRP_PERSIST_SPLIT 1
 #endif
 #ifndef ADRP_HOVER_ANGLE_HELPERS
@@ -741,10 +741,10 @@ __device__ __forceinline__ void hover_step_body(const HoverArgs<Real>& a, const 
         }
     }
     const int E = a.E;
-    // SPLIT (line-mode persistent step of ONE env, BASELINE config 1): every lane of the wave runs env 0
-    // (the same inputs, the same code: the duplicate stores write the same values) so that three lanes
-    // can take the three obs angles at once; contacts are counted by lane 0 alone
-    const bool split = ADRP_PERSIST_SPLIT && SYS == 2 && E == 1;
+    // SPLIT (a step of ONE env, BASELINE config 1: launched or persistent): every lane of the wave runs
+    // env 0 (the same inputs, the same code: the duplicate stores write the same values) so that three
+    // lanes can take the three obs angles at once; contacts are counted by lane 0 alone
+    const bool split = ADRP_PERSIST_SPLIT && !STG && !HELP && E == 1;
     const int e = split ? 0 : int(blockIdx.x) * kStepBlock + int(threadIdx.x);
     const int D = B > 0 ? 12 + B * A : a.D;
     if (e >= E) return;
