@@ -737,6 +737,38 @@ __device__ __forceinline__ void reset_from_image(const RaceArgs<Real>& a, size_t
 
 // The refill: the step's lane layout (a quad per drone, 4G lanes per env); an env whose image is not
 // for its current episode gets one.  Waves with nothing to refill end after two loads.
+// The constant block (RaceConst, ~2 KB) into LDS in two halves: load() issues every 16-byte chunk's
+// load before any store and store() writes them later, so the copy costs one memory latency, which
+// the step kernel overlaps with its state loads.  (The plain strided loop compiled to a load, a
+// vmcnt(0) wait and a store per 256 bytes: nine serialised misses at kernel start, where the
+// kernel-start acquire has just invalidated L2.)
+template <class T>
+struct LdsCopy {
+    static constexpr int NB = int(sizeof(T)), N4 = NB / 16, R = (NB % 16) / 4;
+    static constexpr int IT = (N4 + kRaceBlock - 1) / kRaceBlock;
+    uint4 v[IT];
+    uint32_t r;
+    __device__ __forceinline__ void load(const T* g, int tl) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(g);   // (the device allocation's start: aligned)
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const int i = tl + j * kRaceBlock;
+            if (i < N4) v[j] = s4[i];
+        }
+        r = 0;
+        if (R > 0 && tl < R) r = reinterpret_cast<const uint32_t*>(g)[N4 * 4 + tl];
+    }
+    __device__ __forceinline__ void store(T* lds, int tl) const {
+        uint4* d4 = reinterpret_cast<uint4*>(lds);
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const int i = tl + j * kRaceBlock;
+            if (i < N4) d4[i] = v[j];
+        }
+        if (R > 0 && tl < R) reinterpret_cast<uint32_t*>(lds)[N4 * 4 + tl] = r;
+    }
+};
+
 template <typename Real, int G>
 __global__ void __launch_bounds__(kRaceBlock) race_refill_q4(RaceArgs<Real> a) {
     const int tl = threadIdx.x;
@@ -757,10 +789,9 @@ __global__ void __launch_bounds__(kRaceBlock) race_refill_q4(RaceArgs<Real> a) {
     __shared__ float rows[kQuadDrones * (49 + 6 * (G - 1))];
     // (the wave that reaches here is the whole block: kRaceBlock = one wave)
     {
-        constexpr int nw = int(sizeof(RaceConst<Real>) / 4);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.c);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&c_lds);
-        for (int i = tl; i < nw; i += kRaceBlock) dst[i] = src[i];
+        LdsCopy<RaceConst<Real>> cc;
+        cc.load(a.c, tl);
+        cc.store(&c_lds, tl);
     }
     __syncthreads();
     const RaceConst<Real>& C = c_lds;
@@ -828,14 +859,13 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
     __shared__ __attribute__((aligned(16))) RaceConst<Real> c_lds;
     __shared__ double exp_lds[32];
     constexpr bool kDwF64 = !F32 && (PH == ADRP_PHYS_PYB_DW || PH == ADRP_PHYS_PYB_GND_DRAG_DW);
+    // the constant block and the exp table: loads issued here, LDS stores after the state loads
+    // (before the barrier ahead of the sub-step loop); C is read only after the loop
+    LdsCopy<RaceConst<Real>> ccopy;
+    ccopy.load(a.c, int(threadIdx.x));
+    double exp_v = 0.0;
     if constexpr (kDwF64) {
-        if (threadIdx.x < 32) exp_lds[threadIdx.x] = f64::kExp2Tab32[threadIdx.x];
-    }
-    {
-        constexpr int nw = int(sizeof(RaceConst<Real>) / 4);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.c);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&c_lds);
-        for (int i = threadIdx.x; i < nw; i += kRaceBlock) dst[i] = src[i];
+        if (threadIdx.x < 32) exp_v = f64::kExp2Tab32[threadIdx.x];
     }
     const RaceConst<Real>& CG = *a.c;   // uniform fields: scalar loads (SGPRs)
     const RaceConst<Real>& C = c_lds;   // after the loop
@@ -916,6 +946,10 @@ __global__ void __launch_bounds__(kRaceBlock) race_step_q4(RaceArgs<Real> a) {
 #if defined(ADRP_RACE_TIMING) && defined(ADRP_RACE_GJK_STATS)
     if (threadIdx.x == 0) g_gjk_wave_iters = 0;
 #endif
+    ccopy.store(&c_lds, tl);
+    if constexpr (kDwF64) {
+        if (tl < 32) exp_lds[tl] = exp_v;
+    }
     if constexpr (!DRAWS && kDwF64) __syncthreads();   // the exp table (DRAWS: the barrier below)
     if constexpr (DRAWS) {   // sub-steps s = ql, ql + 4, ... of this drone
         quad_draws<Real>(H, pre_draws, a.seed, gid, ep, dn, sc0, ql, qd, H.S);
